@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark: Chebyshev SpMM-chain edges*K/s on MI355X (BASELINE.json metric).
+
+One "step" = one full ``graph_wavelet_features`` pass (reference
+calibration/WATS.py:39-74) over a device-resident graph: permute the signal
+into the internal order, K fused Chebyshev steps (T_k = 2 L_hat T_{k-1} -
+T_{k-2}, S += alpha_k T_k), then S / H back to caller order.  The Laplacian
+prologue (a1-a3) is built once before timing, as the reference builds it once
+per WATS construction.
+
+Default workload (BASELINE.json configs[2], the one the metric is quoted on):
+ogbn-arxiv-size synthetic R-MAT graph (N=169,343, nnz~2.32M symmetrised), K=16,
+F=40 random-normal signal columns, s=0.8.
+
+value = total edges*K processed by all ranks / max-over-ranks wall time, where
+edges = nnz of the off-diagonal L_hat (= symmetrised adjacency without loops).
+Multi-GPU (torchrun, one process per GPU): each rank runs its own
+independently generated graph of the same size -- weak scaling over
+independent graphs, no data-path collective (the row-sharded single-graph
+path with RCCL halo exchange is `--mode sharded`).
+
+Also printed in the same JSON line:
+  roofline      -- the step kernel's algorithmic bytes (SURVEY.md 8(d):
+                   B_step = 8 nnz + 4 (N+1) + 20 N F) / its mean duration from
+                   HIP events recorded live around every step launch;
+  cpu_baseline  -- the oracle (scipy/numpy restatement of the reference, one
+                   thread) on the same graph, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "efficient-gnn_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="ogbn-arxiv")
+    ap.add_argument("--K", type=int, default=None)
+    ap.add_argument("--F", type=int, default=None)
+    ap.add_argument("--s", type=float, default=0.8)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(n: int, nnz: int, F: int) -> int:
+    """CSR indices+values 8 B/nnz, int32 row pointers, read
+    T_{k-1} once, read T_{k-2}, write T_k, read+write S (fp32)."""
+    return 8 * nnz + 4 * (n + 1) + 20 * n * F
+
+
+def cpu_baseline(g, K, F, s, X, seconds):
+    from oracle import wats_oracle as O
+    A = g.to_scipy()
+    L_hat = O.rescaled_laplacian(A)  # prologue, untimed (as on the GPU)
+    nnz = int(L_hat.nnz - np.count_nonzero(L_hat.diagonal()))
+    reps, t_total = 0, 0.0
+    while t_total < seconds and reps < 50:
+        t0 = time.perf_counter()
+        T = O.chebyshev_polynomials(L_hat, K, X)
+        S = O.heat_kernel_combine(T, s)
+        O.row_l1_normalize(np.asarray(S))
+        t_total += time.perf_counter() - t0
+        reps += 1
+        del T, S
+    return dict(value=nnz * K * reps / t_total, unit="edges*K/s", cores=1, kind="port",
+                sample=f"{reps} full graph_wavelet_features passes (chain + heat sum + L1 norm, prologue excluded) "
+                       f"of the same graph/signal, scipy {__import__('scipy').__version__} single-threaded CSR "
+                       f"matvecs, {t_total:.1f} s")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank if world > 1 else 0)
+    torch.cuda.set_device(device)
+
+    import wats_hip
+    from wats_hip.graphgen import NAMED_CONFIGS, named_graph
+
+    n_target, nnz_target, K_def, F_def = NAMED_CONFIGS[args.config]
+    K = args.K if args.K is not None else K_def
+    F = args.F if args.F is not None else F_def
+    g = named_graph(args.config, seed=args.seed + rank)   # independent graph per rank
+    st = g.stats()
+    L = wats_hip.NormalizedLaplacian.from_graph(g, device=device)
+    rng = np.random.default_rng(1 + rank)
+    if F == 1:
+        X_host = None  # the reference signal log1p(rowsum)
+        X = L.log1p_degree()
+    else:
+        X_host = rng.standard_normal((g.n, F)).astype(np.float32)
+        X = torch.from_numpy(X_host).to(device)
+    n, nnz = L.n, L.nnz
+    S = torch.empty(n, F, dtype=torch.float32, device=device)
+    H = torch.empty(n, F, dtype=torch.float32, device=device)
+    lib = wats_hip._lib.load()
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def step():
+        wats_hip._lib.check(lib.wg_wavelet_features(L.handle, X.data_ptr(), F, K, args.s, S.data_ptr(),
+                                                    H.data_ptr(), stream), "wavelet_features")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    L.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    prof = L.profile_collect()
+    L.profile_enable(False)
+    elapsed = t1 - t0
+    edges_k = float(nnz) * K * args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        e = torch.tensor([edges_k], dtype=torch.float64, device=device)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        edges_k = float(e.item())
+
+    if rank == 0:
+        avg_ms = prof["sum_ms"] / max(1, prof["launches"])
+        b_step = algorithmic_bytes(n, nnz, F)
+        achieved = b_step / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            traffic = json.load(open(args.traffic_json)).get("bytes_per_launch")
+        line = {
+            "metric": "Chebyshev SpMM-chain edges*K/s (ogbn-arxiv-size, K=16) + %HBM roofline",
+            "value": edges_k / elapsed,
+            "unit": "edges*K/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config}-size R-MAT graph (a=.57,b=c=.19), symmetrised, no self loops; "
+                            f"graph_wavelet_features K={K}, F={F} "
+                            f"{'log1p-degree signal' if F == 1 else 'randn signal columns'}, s={args.s}",
+                "N": n, "nnz": nnz, "isolated": st["isolated"], "max_degree": st["max_degree"],
+                "K": K, "F": F, "per_rank": "independent graph per rank (weak scaling, no collective)",
+                "parallelism": f"graphs x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "cheb_step_kernel",
+                "algorithmic_bytes_per_launch": b_step,
+                "avg_launch_us": avg_ms * 1e3,
+                "max_launch_us": prof["max_ms"] * 1e3,
+                "launches": prof["launches"],
+            },
+            "chain_ms": prof["sum_ms"] / args.steps,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            if X_host is None:
+                X_host = L.log1p_degree().cpu().numpy()
+            line["cpu_baseline"] = cpu_baseline(g, K, F, args.s, X_host, args.cpu_seconds)
+            line["cpu_baseline"]["host_cpu"] = _cpu_model()
+        js = json.dumps(line)
+        print(js, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(js + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

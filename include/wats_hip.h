@@ -1,0 +1,176 @@
+/*
+ * wats_hip.h -- C ABI of the MI355X (gfx950) graph-wavelet feature extractor.
+ *
+ * Drop-in boundary for the hot path of CaptainCuong/Efficient-GNN
+ * `calibration/WATS.py` (the reference is pure Python over scipy.sparse; this
+ * header lists the entry points a ctypes / cffi binding of that path binds).
+ * Each entry cites the reference function it replaces.
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer (hipMalloc / torch CUDA tensor
+ *     storage) unless its name ends in `_host`.  Buffers are caller-owned,
+ *     row-major, contiguous, F (signal columns) innermost.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).
+ *     All work is enqueued on it; no entry point synchronises the device
+ *     except the ones documented as "synchronous" (graph creation / dense
+ *     ingestion, which size device allocations from device-computed counts).
+ *   - Return value: WG_OK (0) or a negative WG_ERR_* code; the message of the
+ *     last failure on the calling host thread is wg_last_error().  No entry
+ *     point aborts the process.
+ *   - A wg_laplacian_t is not thread-safe: one host thread per handle.
+ *     Multi-GPU = one process per GPU, one handle per process (row shard).
+ */
+#ifndef WATS_HIP_H
+#define WATS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WG_ABI_VERSION 1
+
+enum wg_status {
+  WG_OK = 0,
+  WG_ERR_INVALID = -1,   /* bad argument (shape, null pointer, range) */
+  WG_ERR_HIP = -2,       /* a HIP runtime call failed */
+  WG_ERR_OOM = -3,       /* device allocation failed */
+  WG_ERR_UNSUPPORTED = -4
+};
+
+/* creation flags */
+#define WG_FLAG_NONE 0u
+#define WG_FLAG_NO_REORDER 1u   /* keep the caller's row order (no degree relabelling) */
+
+typedef struct wg_laplacian_s* wg_laplacian_t;
+
+typedef struct wg_laplacian_info {
+  int64_t n_rows;        /* rows owned by this handle (all N on one GPU) */
+  int64_t n_cols;        /* column space = n_rows + halo rows (== n_rows on one GPU) */
+  int64_t nnz_input;     /* stored entries of the input adjacency rows */
+  int64_t nnz;           /* off-diagonal entries of L_hat (self loops removed) */
+  int64_t n_isolated;    /* rows with w_i == 0 (L_hat_ii = -1) */
+  int64_t max_row_nnz;   /* longest L_hat row */
+  int32_t n_segments;    /* row-length bins of the step kernel */
+  int32_t reordered;     /* 1 if rows are relabelled by descending degree */
+} wg_laplacian_info;
+
+/* -------------------------------------------------------------------------
+ * Library
+ * ---------------------------------------------------------------------- */
+const char* wg_last_error(void);
+int wg_abi_version(void);
+
+/* -------------------------------------------------------------------------
+ * a8 / section 8(f)-1: dense adjacency ingestion.
+ * Replaces `csr_matrix(adj.cpu().numpy())` (calibration/WATS.py:99) with an
+ * on-device compaction.  Two calls: count (writes indptr[n+1], returns nnz in
+ * *nnz_host; synchronous), then fill (indices/values sized nnz; async).
+ * Entries != 0.0f are kept, in column order, exactly like scipy.
+ * ---------------------------------------------------------------------- */
+int wg_dense_to_csr_count(const float* adj, int64_t n_rows, int64_t n_cols, int64_t ld,
+                          int64_t* indptr, int64_t* nnz_host, void* stream);
+int wg_dense_to_csr_fill(const float* adj, int64_t n_rows, int64_t n_cols, int64_t ld,
+                         const int64_t* indptr, int32_t* indices, float* values, void* stream);
+
+/* -------------------------------------------------------------------------
+ * Degree helpers (used for row shards, where the Laplacian's column degree
+ * w_j = colsum_j(A) - A_jj spans every shard and is summed across ranks).
+ * wg_column_degree ACCUMULATES (+=) this shard's column sums into
+ * colsum_f64[n_cols_global] and its diagonal into diag_f64 (indexed by the
+ * global column id `row_offset + i` of local row i).  Column ids are global.
+ * scipy semantics: `_laplacian.py:467` (w = m.sum(axis=0) - m.diagonal()).
+ * ---------------------------------------------------------------------- */
+int wg_column_degree(int64_t n_rows, int64_t row_offset, const int64_t* indptr,
+                     const int32_t* indices, const float* values /* NULL = 1 */,
+                     double* colsum_f64, double* diag_f64, void* stream);
+
+/* -------------------------------------------------------------------------
+ * a1 + a2: compute_normalized_laplacian + rescale.
+ * Replaces `csgraph.laplacian(adj, normed=True)` (calibration/WATS.py:24-27,
+ * scipy _laplacian.py:467-475) followed by `(2/2.0)*L - identity(N)`
+ * (calibration/WATS.py:55).  Builds on the device:
+ *     L_hat_ij = -((a_ij / sqrt(w_i)) / sqrt(w_j))   (float32, scipy op order)
+ *     for i != j, with w = column sums minus diagonal and sqrt(w)=1 where w==0;
+ *     L_hat_ii = -1 for isolated rows (w_i == 0), 0 (dropped) otherwise.
+ * Inputs: CSR rows of A (int64 indptr[n_rows+1], int32 indices, float32
+ * values or NULL for an unweighted graph); column ids in [0, n_cols) where
+ * column i (< n_rows) is local row i (i.e. owned rows first, then halo rows).
+ * w_cols (float32[n_cols], nullable): precomputed column degree
+ * (colsum - diag) per column id; NULL = compute from this CSR (single GPU).
+ * Synchronous.  The handle owns its device copy of L_hat and workspaces.
+ * ---------------------------------------------------------------------- */
+int wg_laplacian_create(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                        const int64_t* indptr, const int32_t* indices, const float* values,
+                        const float* w_cols, uint32_t flags, void* stream,
+                        wg_laplacian_t* out);
+int wg_laplacian_destroy(wg_laplacian_t L);
+int wg_laplacian_get_info(wg_laplacian_t L, wg_laplacian_info* info_host);
+
+/* Export L_hat in the CALLER's row/column numbering: the off-diagonal
+ * entries as CSR (int64 indptr[n_rows+1], int32 indices / float32 values
+ * sized info.nnz, the input's column order) plus iso[n_rows] (1 where
+ * L_hat_ii = -1; nullable).  For bit-exact parity tests against scipy.  Async. */
+int wg_laplacian_export(wg_laplacian_t L, int64_t* indptr, int32_t* indices,
+                        float* values, uint8_t* iso, void* stream);
+
+/* -------------------------------------------------------------------------
+ * a3: input signal.  Replaces `X0 = log1p(adj.sum(axis=1))`
+ * (calibration/WATS.py:58-59): row sums INCLUDING self loops, float32 (N,1),
+ * in the caller's row order.
+ * ---------------------------------------------------------------------- */
+int wg_log1p_degree(wg_laplacian_t L, float* x0, void* stream);
+
+/* -------------------------------------------------------------------------
+ * a4 (+a5): one Chebyshev step of `chebyshev_polynomials`
+ * (calibration/WATS.py:29-37), in the handle's INTERNAL row order (see
+ * wg_permute_rows).  k == 1:  T_1 = L_hat T_0;  k >= 2:  T_k = 2 L_hat T_{k-1}
+ * - T_{k-2}.  t_km1 has n_cols rows (owned + halo), t_km2 / t_k n_rows rows,
+ * all with row stride F.  t_k may alias t_km2 (in-place).  If S != NULL the
+ * heat-kernel sum of calibration/WATS.py:65-68 is fused:
+ *   k == 1:  S = alpha0 * T_0 + alpha_k * T_1;    k >= 2:  S += alpha_k * T_k.
+ * If H != NULL (last step) the row-L1 normalisation of WATS.py:71-72 is fused:
+ *   H = S / (sum_f |S| + 1e-8).  Row sums accumulate in float64.
+ * ---------------------------------------------------------------------- */
+int wg_cheb_step(wg_laplacian_t L, int32_t k, int64_t F, const float* t_km1,
+                 const float* t_km2, float* t_k, float* S, float* H,
+                 double alpha0, double alpha_k, void* stream);
+
+/* Row permutation between the caller's order and the internal order:
+ * direction 0: dst[i_internal] = src[perm[i]]  (caller -> internal)
+ * direction 1: dst[perm[i]] = src[i_internal]  (internal -> caller). */
+int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float* src,
+                    float* dst, void* stream);
+
+/* -------------------------------------------------------------------------
+ * a7: graph_wavelet_features (calibration/WATS.py:39-74), fused:
+ *   T_0 = X0 (N,F) -> K Chebyshev steps -> S = sum_k exp(-s k) T_k ->
+ *   H = S / (||S||_1,row + 1e-8).
+ * X0, S, H in the caller's row order, row stride F.  S and H nullable (at
+ * least one non-NULL).  K >= 0.  Uses the handle's workspace (grown on first
+ * use for a given F -- call once untimed before capturing into a graph).
+ * ---------------------------------------------------------------------- */
+int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s,
+                        float* S, float* H, void* stream);
+
+/* Live kernel timing for benchmarks: while enabled, wg_wavelet_features
+ * records a HIP event pair on `stream` around every Chebyshev-step launch.
+ * wg_profile_collect waits for the recorded events (synchronous), returns
+ * the summed step-kernel time (ms), the number of step launches and the
+ * longest one since the last collect, and resets the pool. */
+int wg_profile_enable(wg_laplacian_t L, int32_t enable);
+int wg_profile_collect(wg_laplacian_t L, double* sum_ms_host, int64_t* launches_host,
+                       double* max_ms_host);
+
+/* a6 standalone: H = S / (||S||_1,row + 1e-8) (calibration/WATS.py:71-72). */
+int wg_row_l1_normalize(const float* S, float* H, int64_t n_rows, int64_t F, void* stream);
+
+/* Multi-GPU halo pack: dst[i] = src[rows[i]] for i < n (row stride F). */
+int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, float* dst,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WATS_HIP_H */

@@ -1,0 +1,67 @@
+"""Shared test setup: import paths, the `gpu` marker, golden-vector loading
+and the parity tolerance of SURVEY.md section 8(c)."""
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "efficient-gnn_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built HIP library")
+
+
+def golden_names(prefix=""):
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, prefix + "*.npz"))
+                  if not os.path.basename(p).startswith("wats_forward"))
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as d:
+        return {k: d[k] for k in d.files}
+
+
+def golden_csr(d):
+    import scipy.sparse as sp
+    n = int(d["n"])
+    return sp.csr_matrix((d["values"], d["indices"], d["indptr"]), shape=(n, n))
+
+
+# Parity tolerance (north_star: <= 1e-5 relative, fp32):
+#   max|got-ref| / max|ref| <= tol per column, and per-element relative
+#   error <= tol where |ref| > floor * max|ref| of that column.
+REL_TOL = 1e-5
+ELEM_FLOOR = 1e-3
+
+
+def assert_parity(got, ref, tol=REL_TOL, floor=ELEM_FLOOR, what=""):
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    if ref.ndim == 1:
+        ref = ref.reshape(-1, 1)
+    got = got.reshape(ref.shape)
+    assert np.all(np.isfinite(got)), f"{what}: non-finite output"
+    scale = np.max(np.abs(ref), axis=0) if ref.size else np.zeros(ref.shape[1])
+    err = np.max(np.abs(got - ref), axis=0) if ref.size else np.zeros(ref.shape[1])
+    for c in range(ref.shape[1]):
+        if scale[c] == 0:
+            assert err[c] == 0, f"{what}: column {c} should be exactly 0, max err {err[c]}"
+            continue
+        assert err[c] / scale[c] <= tol, f"{what}: column {c} max rel err {err[c] / scale[c]:.3e} > {tol}"
+        big = np.abs(ref[:, c]) > floor * scale[c]
+        if big.any():
+            rel = np.abs(got[big, c] - ref[big, c]) / np.abs(ref[big, c])
+            assert rel.max() <= tol, f"{what}: column {c} elementwise rel err {rel.max():.3e} > {tol}"
+
+
+@pytest.fixture(scope="session")
+def repo_root():
+    return REPO

@@ -1,0 +1,246 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the reference's
+golden vectors and the CPU oracle, on seeded inputs; size-independent
+properties (eigenvector KAT, determinism, relabelling invariance) at the
+named full sizes."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from conftest import assert_parity, golden_csr, golden_names, load_golden
+from oracle import wats_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import wats_hip  # noqa: E402
+from wats_hip import NormalizedLaplacian  # noqa: E402
+from wats_hip.graphgen import named_graph, random_graph, rmat_graph  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    wats_hip._lib.load()
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ----------------------------------------------------------------- prologue
+@pytest.mark.parametrize("name", golden_names())
+def test_laplacian_bit_exact_vs_scipy(name):
+    """L_hat values equal scipy's float32 values bit for bit (a1 + a2)."""
+    d = load_golden(name)
+    A = golden_csr(d)
+    L = NormalizedLaplacian.from_scipy(A)
+    indptr, indices, vals, iso = L.export()
+    r_indptr, r_indices, r_vals, r_iso, _ = O.laplacian_explicit(A)
+    np.testing.assert_array_equal(indptr, r_indptr)
+    np.testing.assert_array_equal(indices, r_indices)
+    np.testing.assert_array_equal(vals.view(np.uint32), r_vals.view(np.uint32))
+    np.testing.assert_array_equal(iso, r_iso)
+    assert L.info["n_isolated"] == int(r_iso.sum())
+    if "L_values" in d:
+        ref = sp.csr_matrix((d["L_values"], d["L_indices"], d["L_indptr"]), shape=A.shape)
+        got = L.to_scipy()
+        got.eliminate_zeros()
+        assert (got != ref).nnz == 0
+
+
+@pytest.mark.parametrize("seed,directed,weighted", [(0, True, True), (1, False, True), (2, True, False)])
+def test_laplacian_random_graphs(seed, directed, weighted):
+    g = random_graph(700, 0.01, seed=seed, directed=directed, weighted=weighted, self_loop_frac=0.05,
+                     isolated_frac=0.05)
+    A = g.to_scipy()
+    L = NormalizedLaplacian.from_graph(g)
+    _, indices, vals, iso = L.export()
+    _, r_indices, r_vals, r_iso, _ = O.laplacian_explicit(A)
+    np.testing.assert_array_equal(indices, r_indices)
+    np.testing.assert_array_equal(vals.view(np.uint32), r_vals.view(np.uint32))
+    np.testing.assert_array_equal(iso, r_iso)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_log1p_degree(name):
+    """X0 = log1p(rowsum) within 1 ulp of numpy's float32 log1p (numpy's SIMD
+    float32 log1p is itself 1 ulp from correctly rounded; we round correctly)."""
+    d = load_golden(name)
+    if "H_ref_fn" not in d:
+        pytest.skip("fixture uses an explicit signal")
+    L = NormalizedLaplacian.from_scipy(golden_csr(d))
+    x0 = _np(L.log1p_degree())
+    ulp = np.abs(x0.view(np.int32).astype(np.int64) - d["X0"].view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1
+
+
+def test_dense_ingestion_matches_scipy():
+    g = random_graph(300, 0.03, seed=9, directed=True, weighted=True, self_loop_frac=0.1)
+    dense = torch.tensor(g.to_scipy().toarray(), dtype=torch.float32, device="cuda")
+    indptr, indices, values = wats_hip.dense_to_csr(dense)
+    ref = sp.csr_matrix(dense.cpu().numpy())
+    np.testing.assert_array_equal(_np(indptr), ref.indptr)
+    np.testing.assert_array_equal(_np(indices), ref.indices)
+    np.testing.assert_array_equal(_np(values), ref.data)
+
+
+def test_dense_ingestion_strided_and_empty():
+    big = torch.zeros(50, 64, device="cuda")
+    big[3, 5] = 2.0
+    view = big[:, :50]  # ld = 64
+    indptr, indices, values = wats_hip.dense_to_csr(view)
+    assert _np(indptr)[-1] == 1 and _np(indices).tolist() == [5] and _np(values).tolist() == [2.0]
+    indptr, indices, values = wats_hip.dense_to_csr(torch.zeros(7, 7, device="cuda"))
+    assert _np(indptr).tolist() == [0] * 8 and indices.numel() == 0
+
+
+# ----------------------------------------------------------------- the chain
+@pytest.mark.parametrize("name", golden_names())
+def test_wavelet_features_vs_reference_golden(name):
+    """graph_wavelet_features on the GPU matches the reference's S and H."""
+    d = load_golden(name)
+    A = golden_csr(d)
+    k, s = int(d["k"]), float(d["s"])
+    X0 = None if "H_ref_fn" in d else torch.from_numpy(d["X0"])
+    H, S = wats_hip.graph_wavelet_features(A, k=k, s=s, X0=X0, return_S=True)
+    assert_parity(_np(S), d["S"], what=f"{name} S")
+    assert_parity(_np(H), d["H"], what=f"{name} H")
+    big = np.abs(d["S"]) > 1e-6
+    assert np.array_equal(np.sign(_np(H))[big], np.sign(d["H"])[big])
+
+
+@pytest.mark.parametrize("name", [n for n in golden_names() if "T" in load_golden(n)])
+def test_chebyshev_polynomials_vs_reference_golden(name):
+    d = load_golden(name)
+    A = golden_csr(d)
+    k = int(d["k"])
+    X0 = None if "H_ref_fn" in d else torch.from_numpy(d["X0"])
+    T = wats_hip.chebyshev_polynomials(A, k, X0)
+    assert len(T) == k + 1
+    for i, t in enumerate(T):
+        assert_parity(_np(t), d["T"][i], what=f"{name} T_{i}")
+
+
+def test_dense_adjacency_path_matches_reference():
+    """The WATS ingestion path: dense float32 torch adjacency on the device."""
+    d = load_golden("cora_rmat_k3")
+    dense = torch.tensor(golden_csr(d).toarray(), device="cuda")
+    H = wats_hip.graph_wavelet_features(dense)          # defaults k=3, s=0.8
+    assert_parity(_np(H), d["H"], what="dense H")
+
+
+@pytest.mark.parametrize("F", [1, 2, 3, 4, 5, 8, 40, 41, 64, 130, 300])
+def test_signal_widths(F):
+    """Every F-tiling / vector width against the oracle (weighted, directed,
+    self loops, isolated nodes)."""
+    g = random_graph(600, 0.02, seed=F, directed=True, weighted=True, self_loop_frac=0.05, isolated_frac=0.05)
+    A = g.to_scipy()
+    rng = np.random.default_rng(F)
+    X = rng.standard_normal((g.n, F)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=6, s=0.8, X0=X, return_all=True)
+    H, S = wats_hip.graph_wavelet_features(A, k=6, s=0.8, X0=torch.from_numpy(X), return_S=True)
+    assert_parity(_np(S), ref["S"], what=f"F={F} S")
+    assert_parity(_np(H), ref["H"], what=f"F={F} H")
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 5, 32])
+def test_orders(k):
+    g = rmat_graph(4000, 40000, seed=k)
+    A = g.to_scipy()
+    ref = O.graph_wavelet_features(A, k=k, s=0.8, return_all=True)
+    H, S = wats_hip.graph_wavelet_features(A, k=k, return_S=True)
+    assert_parity(_np(S), ref["S"], what=f"K={k} S")
+    assert_parity(_np(H), ref["H"], what=f"K={k} H")
+
+
+def test_pubmed_config_vs_oracle():
+    """BASELINE config 1: PubMed-size, K=16, F=1."""
+    g = named_graph("pubmed")
+    A = g.to_scipy()
+    ref = O.graph_wavelet_features(A, k=16, s=0.8, return_all=True)
+    H, S = wats_hip.graph_wavelet_features(A, k=16, return_S=True)
+    assert_parity(_np(S), ref["S"], what="pubmed S")
+
+
+def test_arxiv_config_vs_oracle():
+    """BASELINE config 2 (the metric's workload): ogbn-arxiv-size, K=16, F=40."""
+    g = named_graph("ogbn-arxiv")
+    A = g.to_scipy()
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((g.n, 40)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=16, s=0.8, X0=X, return_all=True)
+    H, S = wats_hip.graph_wavelet_features(A, k=16, X0=torch.from_numpy(X), return_S=True)
+    assert_parity(_np(S), ref["S"], what="arxiv S")
+    assert_parity(_np(H), ref["H"], what="arxiv H")
+
+
+def test_hub_rows_long_row_path():
+    """A star graph: one row of 20k nonzeros exercises the workgroup-per-row
+    path (and fp64 accumulation on a hub)."""
+    n = 20001
+    src = np.zeros(n - 1, np.int64)
+    dst = np.arange(1, n)
+    A = sp.coo_matrix((np.ones(2 * (n - 1), np.float32), (np.r_[src, dst], np.r_[dst, src])), shape=(n, n)).tocsr()
+    for F in (1, 40):
+        X = np.random.default_rng(F).standard_normal((n, F)).astype(np.float32)
+        ref = O.graph_wavelet_features(A, k=5, s=0.8, X0=X, return_all=True)
+        H, S = wats_hip.graph_wavelet_features(A, k=5, X0=torch.from_numpy(X), return_S=True)
+        assert_parity(_np(S), ref["S"], what=f"star F={F}")
+
+
+# ----------------------------------------------------------------- properties at full size
+@pytest.mark.parametrize("name,k", [("ogbn-arxiv", 16), ("pubmed", 32)])
+def test_eigenvector_kat_full_size(name, k):
+    """X0 = sqrt(w) -> S = X0 * sum_k (-1)^k e^{-sk} exactly (any size)."""
+    g = named_graph(name)
+    A = g.to_scipy()
+    X0, coef = O.eigen_kat_expected_S(A, k, 0.8)
+    H, S = wats_hip.graph_wavelet_features(g, k=k, X0=torch.from_numpy(X0), return_S=True)
+    assert_parity(_np(S), X0.astype(np.float64) * coef, what=f"{name} eigen KAT")
+
+
+def test_deterministic_and_reorder_invariant():
+    g = named_graph("ogbn-arxiv")
+    X = torch.randn(g.n, 8, generator=torch.Generator().manual_seed(0))
+    L = NormalizedLaplacian.from_graph(g)
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=16, X0=X, return_S=True)
+    H2, S2 = wats_hip.graph_wavelet_features(L, k=16, X0=X, return_S=True)
+    assert torch.equal(S1, S2) and torch.equal(H1, H2)
+    L0 = NormalizedLaplacian.from_graph(g, reorder=False)
+    H3, S3 = wats_hip.graph_wavelet_features(L0, k=16, X0=X, return_S=True)
+    # relabelling keeps each row's column order; only the lane split of the
+    # float64 row sums differs -> agreement far inside the 1e-5 contract
+    assert_parity(_np(S3), _np(S1).astype(np.float64), tol=1e-6, what="reorder invariance")
+
+
+def test_invalid_arguments_raise():
+    g = random_graph(50, 0.1, seed=0)
+    L = NormalizedLaplacian.from_graph(g)
+    with pytest.raises(wats_hip.WaveletError):
+        wats_hip.graph_wavelet_features(L, k=-1)
+    with pytest.raises(ValueError):
+        wats_hip.graph_wavelet_features(L, X0=torch.zeros(49, 1))
+
+
+# ----------------------------------------------------------------- drop-in
+def test_wats_dropin_on_gpu_matches_reference():
+    from models import CompatibleGCN
+    d = load_golden("wats_forward120")
+    n, nfeat = d["x"].shape
+    ncls = d["base.gc2.weight"].shape[0]
+    base = CompatibleGCN(nfeat, ncls, nhid=d["base.gc1.weight"].shape[0])
+    base.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in d.items() if k.startswith("base.")})
+    base.eval()
+    for p in base.parameters():
+        p.requires_grad = False
+    x, y = torch.from_numpy(d["x"]), torch.from_numpy(d["y"])
+    adj, val = torch.from_numpy(d["adj"]), torch.from_numpy(d["val_mask"])
+    w = wats_hip.WATS(base, x, y, adj, val, verbose=False)
+    assert w.wavelet_feats.is_cuda
+    assert_parity(_np(w.wavelet_feats), d["wavelet_feats"], what="WATS wavelet_feats")
+    w.net.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in d.items() if k.startswith("net.")})
+    w.eval()
+    with torch.no_grad():
+        out = _np(w(x, adj))
+    np.testing.assert_allclose(out, d["out"], rtol=1e-5, atol=1e-5)
