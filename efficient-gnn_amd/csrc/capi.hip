@@ -1,0 +1,198 @@
+// capi.hip -- C ABI entry points of the chain (include/wats_hip.h):
+// graph_wavelet_features (reference calibration/WATS.py:39-74), one
+// chebyshev_polynomials step (WATS.py:29-37), row-L1 normalisation
+// (WATS.py:71-72), row permutations, halo gather, profiling and tuning.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "internal.h"
+
+namespace wg {
+
+namespace {
+thread_local std::string g_err;
+thread_local std::string g_text;
+
+__global__ void gather_rows_kernel(int64_t n, int64_t F, const int32_t* __restrict__ rows, const float* __restrict__ src,
+                                   float* __restrict__ dst) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * F) return;
+  const int64_t i = idx / F;
+  const int64_t f = idx - i * F;
+  dst[idx] = src[(int64_t)rows[i] * F + f];
+}
+}  // namespace
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);
+
+}  // namespace wg
+
+using namespace wg;
+
+extern "C" {
+
+const char* wg_last_error(void) { return g_err.c_str(); }
+
+int wg_abi_version(void) { return WG_ABI_VERSION; }
+
+int wg_laplacian_get_info(wg_laplacian_t L, wg_laplacian_info* info) {
+  if (!L || !info) return fail(WG_ERR_INVALID, "wg_laplacian_get_info: NULL argument");
+  info->n_rows = L->n_rows;
+  info->n_cols = L->n_cols;
+  info->nnz_input = L->nnz_input;
+  info->nnz = L->nnz;
+  info->n_isolated = L->n_iso;
+  info->max_row_nnz = L->max_row;
+  info->n_segments = 0;
+  for (auto& kv : L->plans) info->n_segments = std::max(info->n_segments, kv.second.tab.n);
+  info->reordered = L->reordered ? 1 : 0;
+  return WG_OK;
+}
+
+int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
+  if (!L || !key) return fail(WG_ERR_INVALID, "wg_laplacian_tune: NULL argument");
+  if (!strcmp(key, "iter")) {
+    if (value < 1) return fail(WG_ERR_INVALID, "iter must be >= 1");
+    L->tune.iter = (int32_t)value;
+  } else if (!strcmp(key, "chunk_iter")) {
+    if (value < 1) return fail(WG_ERR_INVALID, "chunk_iter must be >= 1");
+    L->tune.chunk_iter = (int32_t)value;
+  } else if (!strcmp(key, "seg_mask")) {
+    L->tune.seg_mask = value;
+    return WG_OK;  // no replan
+  } else {
+    return fail(WG_ERR_INVALID, "wg_laplacian_tune: unknown key '%s'", key);
+  }
+  WG_HIP_TRY(hipDeviceSynchronize());
+  for (auto& kv : L->plans) kv.second.release();
+  L->plans.clear();
+  return WG_OK;
+}
+
+const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
+  g_text.clear();
+  if (!L || F < 1) return "";
+  const int vec = (F % 4 == 0) ? 4 : (F % 2 == 0) ? 2 : 1;
+  const int LF = (int)(std::min<int64_t>(F, 64 * vec) / vec);
+  Plan* p = nullptr;
+  if (get_plan(L, LF, vec, &p)) return "";
+  char buf[128];
+  snprintf(buf, sizeof(buf), "F=%lld VEC=%d LF=%d segments=%d blocks=%d\n", (long long)F, vec, LF, p->tab.n,
+           p->tab.total_blocks);
+  g_text = buf + p->text;
+  return g_text.c_str();
+}
+
+int wg_cheb_step(wg_laplacian_t L, int32_t k, int64_t F, const float* t_km1, const float* t_km2, float* t_k, float* S,
+                 float* H, double alpha0, double alpha_k, void* stream_) {
+  if (!L || k < 1 || F < 1 || !t_km1 || (k >= 2 && !t_km2) || (H && !S))
+    return fail(WG_ERR_INVALID, "wg_cheb_step: bad arguments (k=%d F=%lld)", k, (long long)F);
+  return launch_step(L, k, F, t_km1, t_km2, t_k, S, H, alpha0, alpha_k, as_stream(stream_));
+}
+
+int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float* src, float* dst, void* stream_) {
+  if (!L || F < 1 || (direction != 0 && direction != 1) || (L->n_rows && (!src || !dst)))
+    return fail(WG_ERR_INVALID, "wg_permute_rows: bad arguments");
+  return launch_permute(L, direction, F, src, dst, as_stream(stream_));
+}
+
+int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s, float* S, float* H,
+                        void* stream_) {
+  if (!L || F < 1 || K < 0 || (!S && !H) || (L->n_rows && !X0))
+    return fail(WG_ERR_INVALID, "wg_wavelet_features: bad arguments (F=%lld K=%d)", (long long)F, K);
+  if (L->n_cols != L->n_rows)
+    return fail(WG_ERR_INVALID, "wg_wavelet_features: sharded handle (halo columns); use wg_cheb_step");
+  hipStream_t stream = as_stream(stream_);
+  const int64_t n = L->n_rows;
+  if (n == 0) return WG_OK;
+  // workspace: T ping-pong (2) + internal S, 256-B aligned sub-buffers
+  const size_t stride = ((size_t)n * F + 63) / 64 * 64;
+  const size_t need = 3 * stride;
+  if (L->ws_floats < need) {
+    WG_HIP_TRY(hipStreamSynchronize(stream));
+    (void)hipFree(L->ws);
+    L->ws = nullptr;
+    L->ws_floats = 0;
+    WG_HIP_TRY(hipMalloc(&L->ws, need * sizeof(float)));
+    L->ws_floats = need;
+  }
+  float* b0 = L->ws;               // T_0, then T_2, T_4, ... (in place)
+  float* b1 = L->ws + stride;      // T_1, T_3, ...
+  float* sint = L->ws + 2 * stride;
+  int rc = launch_permute(L, 0, F, X0, b0, stream);
+  if (rc) return rc;
+  if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * F, hipMemcpyDeviceToDevice, stream));
+  for (int32_t k = 1; k <= K; ++k) {
+    const float* xm1 = (k & 1) ? b0 : b1;
+    const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
+    float* xk = (k == K) ? nullptr : ((k & 1) ? b1 : b0);  // T_K itself is never re-read
+    const double ak = std::exp(-s * (double)k);             // WATS.py:65
+    hipEvent_t e_stop = nullptr;
+    if (L->prof) {
+      while (L->ev.size() < L->ev_used + 2) {
+        hipEvent_t e;
+        WG_HIP_TRY(hipEventCreate(&e));
+        L->ev.push_back(e);
+      }
+      WG_HIP_TRY(hipEventRecord(L->ev[L->ev_used], stream));
+      e_stop = L->ev[L->ev_used + 1];
+      L->ev_used += 2;
+    }
+    rc = launch_step(L, k, F, xm1, xm2, xk, sint, nullptr, 1.0, ak, stream);
+    if (rc) return rc;
+    if (e_stop) WG_HIP_TRY(hipEventRecord(e_stop, stream));
+  }
+  return launch_finalize(L, F, sint, S, H, stream);
+}
+
+int wg_profile_enable(wg_laplacian_t L, int32_t enable) {
+  if (!L) return fail(WG_ERR_INVALID, "wg_profile_enable: NULL handle");
+  L->prof = enable != 0;
+  return WG_OK;
+}
+
+int wg_profile_collect(wg_laplacian_t L, double* sum_ms, int64_t* launches, double* max_ms) {
+  if (!L || !sum_ms || !launches) return fail(WG_ERR_INVALID, "wg_profile_collect: NULL argument");
+  double tot = 0.0, mx = 0.0;
+  for (size_t i = 0; i + 1 < L->ev_used; i += 2) {
+    WG_HIP_TRY(hipEventSynchronize(L->ev[i + 1]));
+    float ms = 0.0f;
+    WG_HIP_TRY(hipEventElapsedTime(&ms, L->ev[i], L->ev[i + 1]));
+    tot += ms;
+    mx = std::max(mx, (double)ms);
+  }
+  *sum_ms = tot;
+  *launches = (int64_t)(L->ev_used / 2);
+  if (max_ms) *max_ms = mx;
+  L->ev_used = 0;
+  return WG_OK;
+}
+
+int wg_row_l1_normalize(const float* S, float* H, int64_t n_rows, int64_t F, void* stream_) {
+  if (n_rows < 0 || F < 1 || (n_rows && (!S || !H))) return fail(WG_ERR_INVALID, "wg_row_l1_normalize: bad arguments");
+  if (n_rows == 0) return WG_OK;
+  return launch_l1_normalize(S, H, n_rows, F, as_stream(stream_));
+}
+
+int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, float* dst, void* stream_) {
+  if (n < 0 || F < 1 || (n && (!src || !rows || !dst))) return fail(WG_ERR_INVALID, "wg_gather_rows: bad arguments");
+  if (n == 0) return WG_OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(ceil_div(n * F, 256)), dim3(256), 0, as_stream(stream_), n, F, rows, src,
+                     dst);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+// internal.h -- shared internals of libwats_hip (not part of the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "wats_hip.h"
+
+namespace wg {
+
+int fail(int code, const char* fmt, ...);
+
+#define WG_HIP_TRY(expr)                                                                       \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return ::wg::fail(e_ == hipErrorOutOfMemory ? WG_ERR_OOM : WG_ERR_HIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                     \
+  } while (0)
+
+#define WG_LAUNCH_CHECK() WG_HIP_TRY(hipGetLastError())
+
+constexpr int kBlock = 256;   // 4 waves of 64 lanes
+constexpr int kMaxSeg = 24;
+constexpr int kBuckets = 33;  // row-length buckets: b=0: len<=1; b>0: 2^(b-1) < len <= 2^b
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+template <typename T>
+int dmalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  WG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+  return WG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Step-kernel launch plan (per signal-tile shape), see step.hip.
+// ---------------------------------------------------------------------------
+struct Seg {
+  int32_t begin;      // team mode: internal rows [begin, end); chunk mode: chunk ids
+  int32_t end;
+  int32_t blk_begin;  // first workgroup of this segment
+  int32_t ln;         // team mode: lane sub-groups cooperating on one row
+  int32_t mode;       // 0 = team (rows of similar length), 1 = chunk (workgroup per nnz chunk)
+};
+
+struct SegTable {
+  Seg s[kMaxSeg];
+  int32_t n;
+  int32_t total_blocks;
+};
+
+struct ChunkDesc {  // one workgroup's share of a long row
+  int32_t row;
+  int32_t e0, e1;   // nnz range
+  int32_t first;    // chunk id of the row's first chunk (partials + arrival counter)
+  int32_t count;    // chunks of this row
+  int32_t pad[3];
+};
+
+struct Plan {
+  SegTable tab{};
+  int32_t n_chunks = 0;
+  int32_t width = 0;            // LF * VEC doubles per partial
+  ChunkDesc* chunks = nullptr;  // device
+  double* partial = nullptr;    // device [n_chunks][width]
+  unsigned int* arrive = nullptr;  // device [n_chunks], zero between launches
+  std::string text;
+  void release();
+};
+
+struct Tuning {
+  int32_t iter = 8;         // team mode: target nonzeros per lane sub-group
+  int32_t chunk_iter = 16;  // chunk mode: nonzeros per sub-group per chunk
+  int64_t seg_mask = -1;    // timing attribution only: launch only these segments
+};
+
+}  // namespace wg
+
+struct wg_laplacian_s {
+  int device = 0;
+  int64_t n_rows = 0, n_cols = 0, nnz_input = 0, nnz = 0, n_iso = 0, max_row = 0;
+  bool reordered = true;
+  int32_t* rowptr = nullptr;  // internal order, int32
+  int32_t* col = nullptr;
+  float* val = nullptr;
+  uint8_t* iso = nullptr;     // internal order
+  int32_t* perm = nullptr;    // internal -> caller row
+  int32_t* iperm = nullptr;   // caller -> internal row
+  float* rowsum = nullptr;    // caller order, float32 (for X0)
+  unsigned int bucket[wg::kBuckets] = {0};  // rows per length bucket (internal rows sorted descending)
+  int64_t avg_len = 0;
+  wg::Tuning tune;
+  std::map<int, wg::Plan> plans;  // key: LF * 8 + VEC
+  // workspace for wg_wavelet_features
+  float* ws = nullptr;
+  size_t ws_floats = 0;
+  // live step-kernel timing (wg_profile_*)
+  bool prof = false;
+  std::vector<hipEvent_t> ev;  // pool of (start, stop) pairs
+  size_t ev_used = 0;
+
+  ~wg_laplacian_s();
+};
+
+namespace wg {
+// step.hip
+int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
+int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out);
+int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
+                float* S, float* H, double alpha0, double alpha_k, hipStream_t stream);
+int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, float* S, float* H, hipStream_t stream);
+int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);
+int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);
+}  // namespace wg

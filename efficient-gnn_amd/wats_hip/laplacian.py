@@ -194,6 +194,15 @@ class NormalizedLaplacian:
             check(_lib.load().wg_cheb_step(self.handle, int(k), F, ptr(t_km1), ptr(t_km2), ptr(out), ptr(S), ptr(H),
                                            float(alpha0), float(alpha_k), stream_handle(self.device)), "cheb_step")
 
+    def tune(self, **knobs) -> None:
+        """Step-kernel tuning knobs: iter, chunk_iter, seg_mask (see wats_hip.h)."""
+        for k, v in knobs.items():
+            check(_lib.load().wg_laplacian_tune(self.handle, k.encode(), int(v)), f"tune {k}")
+
+    def describe(self, F: int = 1) -> str:
+        """The step kernel's launch plan for an F-column signal."""
+        return _lib.load().wg_laplacian_describe(self.handle, int(F)).decode()
+
     def profile_enable(self, enable: bool = True) -> None:
         """Record HIP events around each step launch of graph_wavelet_features."""
         check(_lib.load().wg_profile_enable(self.handle, 1 if enable else 0), "profile_enable")

@@ -154,6 +154,15 @@ int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float*
 int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s,
                         float* S, float* H, void* stream);
 
+/* Tuning: key "iter" (team-mode nonzeros per lane sub-group, default 8),
+ * "chunk_iter" (chunk-mode nonzeros per sub-group, default 16), "seg_mask"
+ * (bitmask of plan segments to launch -- timing attribution only; results
+ * are wrong unless all bits are set).  Synchronous (drops cached plans). */
+int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value);
+/* Human-readable launch plan of the step kernel for an F-column signal
+ * (thread-local string, valid until the next call on this thread). */
+const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F);
+
 /* Live kernel timing for benchmarks: while enabled, wg_wavelet_features
  * records a HIP event pair on `stream` around every Chebyshev-step launch.
  * wg_profile_collect waits for the recorded events (synchronous), returns

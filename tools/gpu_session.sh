@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session: smoke, parity tests, bench, rocprofv3 kernel trace.
+# Every GPU step has its own time limit; a crash/timeout stops the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${SESSION:-s1}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+stop_if_fatal() {  # $1 = rc, $2 = step
+  local rc=$1
+  echo "[$2] rc=$rc" | tee -a "$OUT/steps.log"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "fatal rc in $2, stopping"; exit "$rc"; fi
+}
+rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+stop_if_fatal $? smoke
+if [ "${RUN_TESTS:-1}" = 1 ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider > "$OUT/gpu_tests.log" 2>&1
+  stop_if_fatal $? pytest
+fi
+if [ -n "${SWEEP:-}" ]; then
+  timeout -k 10 600 python tools/sweep.py $SWEEP > "$OUT/sweep.log" 2>&1
+  stop_if_fatal $? sweep
+fi
+timeout -k 10 400 python bench.py --steps ${STEPS:-20} --warmup 3 --out "$OUT/bench.json" > "$OUT/bench.log" 2>&1
+stop_if_fatal $? bench
+if [ "${RUN_PROF:-1}" = 1 ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- \
+      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1
+  stop_if_fatal $? rocprof
+fi
+echo done

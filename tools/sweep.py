@@ -1,0 +1,79 @@
+"""GPU tuning sweep for the step kernel (run on the GPU box).
+
+For a named config: time graph_wavelet_features' step kernels for a grid of
+(iter, chunk_iter) knobs, and attribute time per plan segment (seg_mask).
+Writes one JSON line per measurement to stdout."""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "efficient-gnn_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import wats_hip  # noqa: E402
+from wats_hip.graphgen import NAMED_CONFIGS, named_graph  # noqa: E402
+
+
+def time_chain(L, X, K, reps=10):
+    n, F = X.shape
+    S = torch.empty_like(X)
+    H = torch.empty_like(X)
+    lib = wats_hip._lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    run = lambda: wats_hip._lib.check(lib.wg_wavelet_features(L.handle, X.data_ptr(), F, K, 0.8, S.data_ptr(),
+                                                               H.data_ptr(), st))
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize()
+    L.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    p = L.profile_collect()
+    L.profile_enable(False)
+    return dict(step_us=p["sum_ms"] / max(1, p["launches"]) * 1e3, max_us=p["max_ms"] * 1e3, call_ms=wall * 1e3)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="ogbn-arxiv")
+    ap.add_argument("--F", type=int, default=None)
+    ap.add_argument("--K", type=int, default=16)
+    ap.add_argument("--iters", default="4,8,16")
+    ap.add_argument("--chunk-iters", default="8,16,32")
+    ap.add_argument("--segments", action="store_true")
+    a = ap.parse_args()
+    n, nnz, K, F = NAMED_CONFIGS[a.config]
+    F = a.F or F
+    g = named_graph(a.config)
+    L = wats_hip.NormalizedLaplacian.from_graph(g)
+    X = torch.randn(g.n, F, device="cuda") if F > 1 else L.log1p_degree()
+    bstep = 8 * L.nnz + 4 * (L.n + 1) + 20 * L.n * F
+    for it in [int(x) for x in a.iters.split(",")]:
+        for ci in [int(x) for x in a.chunk_iters.split(",")]:
+            L.tune(iter=it, chunk_iter=ci, seg_mask=-1)
+            r = time_chain(L, X, a.K)
+            r.update(config=a.config, F=F, iter=it, chunk_iter=ci, GBs=bstep / (r["step_us"] * 1e-6) / 1e9)
+            print(json.dumps(r), flush=True)
+    if a.segments:
+        it, ci = [int(x) for x in a.iters.split(",")][0], [int(x) for x in a.chunk_iters.split(",")][0]
+        L.tune(iter=it, chunk_iter=ci)
+        plan = L.describe(F)
+        print(plan, flush=True)
+        nseg = int(plan.split("segments=")[1].split()[0])
+        for i in range(nseg):
+            L.tune(seg_mask=1 << i)
+            r = time_chain(L, X, a.K)
+            r.update(segment=i)
+            print(json.dumps(r), flush=True)
+        L.tune(seg_mask=-1)
+
+
+if __name__ == "__main__":
+    main()
