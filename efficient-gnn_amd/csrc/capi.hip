@@ -23,6 +23,11 @@ __global__ void gather_rows_kernel(int64_t n, int64_t F, const int32_t* __restri
   const int64_t f = idx - i * F;
   dst[idx] = src[(int64_t)rows[i] * F + f];
 }
+__global__ void map_rows_kernel(int64_t n, const int32_t* __restrict__ map, const int32_t* __restrict__ rows,
+                                int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = map[rows[i]];
+}
 }  // namespace
 
 int fail(int code, const char* fmt, ...) {
@@ -184,6 +189,17 @@ int wg_row_l1_normalize(const float* S, float* H, int64_t n_rows, int64_t F, voi
   if (n_rows < 0 || F < 1 || (n_rows && (!S || !H))) return fail(WG_ERR_INVALID, "wg_row_l1_normalize: bad arguments");
   if (n_rows == 0) return WG_OK;
   return launch_l1_normalize(S, H, n_rows, F, as_stream(stream_));
+}
+
+int wg_laplacian_map_rows(wg_laplacian_t L, int32_t direction, const int32_t* rows, int64_t n, int32_t* out,
+                          void* stream_) {
+  if (!L || n < 0 || (direction != 0 && direction != 1) || (n && (!rows || !out)))
+    return fail(WG_ERR_INVALID, "wg_laplacian_map_rows: bad arguments");
+  if (n == 0) return WG_OK;
+  hipLaunchKernelGGL(map_rows_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream_), n,
+                     direction == 0 ? L->iperm : L->perm, rows, out);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
 }
 
 int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, float* dst, void* stream_) {

@@ -48,7 +48,7 @@ struct Seg {
   int32_t end;
   int32_t blk_begin;  // first workgroup of this segment
   int32_t ln;         // team mode: lane sub-groups cooperating on one row
-  int32_t mode;       // 0 = team (rows of similar length), 1 = chunk (workgroup per nnz chunk)
+  int32_t mode;       // 0 = team, 1 = block (workgroup per row), 2 = split (workgroup per nnz chunk)
 };
 
 struct SegTable {
@@ -57,28 +57,27 @@ struct SegTable {
   int32_t total_blocks;
 };
 
-struct ChunkDesc {  // one workgroup's share of a long row
+struct ChunkDesc {  // one workgroup's share of a split row
   int32_t row;
   int32_t e0, e1;   // nnz range
-  int32_t first;    // chunk id of the row's first chunk (partials + arrival counter)
-  int32_t count;    // chunks of this row
-  int32_t pad[3];
+  int32_t pad;
 };
 
 struct Plan {
   SegTable tab{};
   int32_t n_chunks = 0;
   int32_t width = 0;            // LF * VEC doubles per partial
-  ChunkDesc* chunks = nullptr;  // device
+  int32_t n_split = 0;          // split rows = internal rows [0, n_split)
+  ChunkDesc* chunks = nullptr;  // device [n_chunks]
   double* partial = nullptr;    // device [n_chunks][width]
-  unsigned int* arrive = nullptr;  // device [n_chunks], zero between launches
+  int2* rowchunks = nullptr;    // device [n_split] {first chunk, chunk count}
   std::string text;
   void release();
 };
 
 struct Tuning {
   int32_t iter = 8;         // team mode: target nonzeros per lane sub-group
-  int32_t chunk_iter = 16;  // chunk mode: nonzeros per sub-group per chunk
+  int32_t chunk_iter = 32;  // block/split mode: nonzeros per sub-group per workgroup pass
   int64_t seg_mask = -1;    // timing attribution only: launch only these segments
 };
 

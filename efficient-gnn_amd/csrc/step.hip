@@ -11,13 +11,15 @@
 //  * Team mode (short rows): LN sub-groups (LN a divisor of G) share one row
 //    and split its nonzeros; G/LN rows per wave.  The LN partial sums meet in
 //    a fixed shuffle order (tree for power-of-two LN).
-//  * Chunk mode (long rows): a 256-lane workgroup = 4G sub-groups processes a
-//    chunk of at most CH nonzeros of one row and reduces it through an LDS
-//    tree.  A row with several chunks publishes each chunk's float64 partial;
-//    the last workgroup to arrive (agent-scope atomic counter, release/acquire
-//    per cdna_hip_programming.md Guideline 16) sums the partials in chunk
-//    order -- deterministic regardless of arrival order -- and runs the
-//    epilogue.  No workgroup ever waits on another.
+//  * Block mode (long rows): a 256-lane workgroup = 4G sub-groups splits the
+//    row; sub-groups reduce by shuffles inside each wave, the 4 wave sums meet
+//    in LDS behind one barrier.
+//  * Split mode (hub rows longer than CH nonzeros): one workgroup per CH-nnz
+//    chunk writes a float64 partial; a small combine kernel launched right
+//    after sums each row's partials in chunk order and runs the epilogue.
+//    (An in-kernel last-arriver combine needs an agent-scope release fence
+//    per chunk -- buffer_wbl2 of the XCD L2 with the step's dirty S/T_k
+//    lines in it -- measured 1.3-2.2x slower for the whole step.)
 // Row sums accumulate in float64 (products of two float32 are exact).
 #include <algorithm>
 #include <cmath>
@@ -45,7 +47,6 @@ struct StepArgs {
   double alpha_k;
   const ChunkDesc* chunks;
   double* partial;
-  unsigned int* arrive;
   int64_t seg_mask;
 };
 
@@ -155,10 +156,33 @@ __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t
   }
 }
 
+// Sum the partial sums of n lane sub-groups (lanes base + q*LF + fs, q < n)
+// into sub-group 0, in a fixed order (tree for power-of-two n).  Must be
+// called by every lane of the wave (uniform control flow).
+template <int VEC>
+__device__ __forceinline__ void reduce_subgroups(double (&acc)[VEC], int n, int LF, int base, int fs) {
+  if (n <= 1) return;
+  if ((n & (n - 1)) == 0) {
+    for (int off = n >> 1; off >= 1; off >>= 1) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += __shfl_down(acc[j], off * LF, 64);
+    }
+  } else {
+    double tot[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) tot[j] = acc[j];
+    for (int q = 1; q < n; ++q) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) tot[j] += __shfl(acc[j], base + q * LF + fs, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = tot[j];
+  }
+}
+
 template <int VEC>
 __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, SegTable tab) {
-  __shared__ double red[kBlock * VEC];
-  __shared__ int s_last;
+  __shared__ double red[4 * 64 * VEC];
   int si = 0;
   for (int i = 1; i < tab.n; ++i)
     if ((int32_t)blockIdx.x >= tab.s[i].blk_begin) si = i;
@@ -172,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, SegTable 
   for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
 
   if (seg.mode == 0) {
-    // ---------------- team mode
+    // ---------------- team mode: LN sub-groups per row, G/LN rows per wave
     const int LN = seg.ln;
     const int TS = LF * LN;
     const int tpw = 64 / TS;
@@ -186,85 +210,75 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, SegTable 
       const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
       accumulate<VEC>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc);
     }
-    if (LN > 1) {
-      if ((LN & (LN - 1)) == 0) {
-        for (int off = LN >> 1; off >= 1; off >>= 1) {
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) acc[j] += __shfl_down(acc[j], off * LF, 64);
-        }
-      } else {
-        double tot[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) tot[j] = acc[j];
-        for (int q = 1; q < LN; ++q) {
-          const int src = team * TS + q * LF + fs;
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) tot[j] += __shfl(acc[j], src, 64);
-        }
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = tot[j];
-      }
-    }
+    reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
     if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, team * TS);
     return;
   }
 
-  // ---------------- chunk mode: one workgroup per chunk of a long row
+  // ---------------- workgroup modes: 4 waves x G sub-groups on one nnz range
+  //   mode 1: a whole row (then the epilogue)
+  //   mode 2: one chunk of a split row (then a float64 partial; finished by combine_kernel)
+  int64_t row;
+  int32_t e0, e1, cid = 0;
+  if (seg.mode == 1) {
+    row = (int64_t)seg.begin + (blockIdx.x - seg.blk_begin);
+    e0 = a.rowptr[row];
+    e1 = a.rowptr[row + 1];
+  } else {
+    cid = seg.begin + (int32_t)(blockIdx.x - seg.blk_begin);
+    const ChunkDesc d = a.chunks[cid];
+    row = d.row;
+    e0 = d.e0;
+    e1 = d.e1;
+  }
   const int G = 64 / LF;
-  const int NS = 4 * G;
   const int sg = lane / LF;
   const int fs = lane - sg * LF;
-  const int sub = wave * G + sg;
-  const int cid = seg.begin + (int)(blockIdx.x - seg.blk_begin);
-  const ChunkDesc d = a.chunks[cid];
-  const int width = LF * VEC;
-  if (sg < G) {
-    accumulate<VEC>(a, d.e0 + sub, d.e1, NS, a.xm1 + fs * VEC, acc);
-    const int base = (sub * LF + fs) * VEC;
+  if (sg < G) accumulate<VEC>(a, e0 + wave * G + sg, e1, 4 * G, a.xm1 + fs * VEC, acc);
+  reduce_subgroups<VEC>(acc, G, LF, 0, fs);
+  if (lane < LF) {
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) red[base + j] = acc[j];
+    for (int j = 0; j < VEC; ++j) red[(wave * LF + lane) * VEC + j] = acc[j];
   }
   __syncthreads();
-  int p2 = 1;
-  while (p2 < NS) p2 <<= 1;
-  for (int s = p2 >> 1; s >= 1; s >>= 1) {
-    for (int idx = threadIdx.x; idx < s * width; idx += kBlock) {
-      if (idx / width + s < NS) red[idx] += red[idx + s * width];
-    }
-    __syncthreads();
-  }
-  if (d.count > 1) {
-    // publish this chunk's partial, then count arrivals
-    if (threadIdx.x < width) a.partial[(int64_t)cid * width + threadIdx.x] = red[threadIdx.x];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned prev = __hip_atomic_fetch_add(a.arrive + d.first, 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-      const int last = (prev == (unsigned)(d.count - 1));
-      if (last) {
-        __hip_atomic_store(a.arrive + d.first, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x < width) {
-      double sum = 0.0;
-      for (int q = 0; q < d.count; ++q) sum += a.partial[(int64_t)(d.first + q) * width + threadIdx.x];
-      red[threadIdx.x] = sum;
-    }
-    __syncthreads();
-  }
   if (threadIdx.x < LF) {
+    const int t = threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] = red[threadIdx.x * VEC + j];
-    step_epilogue<VEC>(a, d.row, threadIdx.x, acc, 0);
+    for (int j = 0; j < VEC; ++j)
+      acc[j] = ((red[(0 * LF + t) * VEC + j] + red[(1 * LF + t) * VEC + j]) + red[(2 * LF + t) * VEC + j]) +
+               red[(3 * LF + t) * VEC + j];
+    if (seg.mode == 1) {
+      step_epilogue<VEC>(a, row, t, acc, 0);
+    } else {
+      double* p = a.partial + (int64_t)cid * (LF * VEC) + t * VEC;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) p[j] = acc[j];
+    }
   }
+}
+
+// Split rows: sum each row's chunk partials in chunk order, then the epilogue.
+// Sub-group of LF lanes per row.
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_split, const int2* __restrict__ rowchunks) {
+  const int lane = threadIdx.x & 63;
+  const int LF = a.LF;
+  const int G = 64 / LF;
+  const int sg = lane / LF;
+  const int fs = lane - sg * LF;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + sg;
+  if (sg >= G || row >= n_split) return;
+  const int2 rc = rowchunks[row];
+  const int width = LF * VEC;
+  double acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
+  for (int q = 0; q < rc.y; ++q) {
+    const double* p = a.partial + (int64_t)(rc.x + q) * width + fs * VEC;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] += p[j];
+  }
+  step_epilogue<VEC>(a, row, fs, acc, sg * LF);
 }
 
 // internal S -> caller-order S and H = S / (||S||_1 + 1e-8); team of LF lanes per row.
@@ -371,9 +385,18 @@ int divisor_at_least(int G, int64_t want) {
 }
 
 template <int VEC>
-int launch_step_vec(wg_laplacian_s* L, const StepArgs& a, const SegTable& tab, hipStream_t stream) {
-  hipLaunchKernelGGL(cheb_step_kernel<VEC>, dim3(tab.total_blocks), dim3(kBlock), 0, stream, a, tab);
-  WG_LAUNCH_CHECK();
+int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
+  const SegTable& tab = plan.tab;
+  if (tab.total_blocks > 0) {
+    hipLaunchKernelGGL(cheb_step_kernel<VEC>, dim3(tab.total_blocks), dim3(kBlock), 0, stream, a, tab);
+    WG_LAUNCH_CHECK();
+  }
+  if (plan.n_split > 0 && ((a.seg_mask >> tab.n) & 1)) {
+    const int G = 64 / a.LF;
+    hipLaunchKernelGGL(combine_kernel<VEC>, dim3((unsigned)ceil_div(plan.n_split, 4 * G)), dim3(kBlock), 0, stream, a,
+                       plan.n_split, plan.rowchunks);
+    WG_LAUNCH_CHECK();
+  }
   return WG_OK;
 }
 
@@ -382,10 +405,10 @@ int launch_step_vec(wg_laplacian_s* L, const StepArgs& a, const SegTable& tab, h
 void Plan::release() {
   (void)hipFree(chunks);
   (void)hipFree(partial);
-  (void)hipFree(arrive);
+  (void)hipFree(rowchunks);
   chunks = nullptr;
   partial = nullptr;
-  arrive = nullptr;
+  rowchunks = nullptr;
 }
 
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
@@ -399,7 +422,11 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
   return 1;
 }
 
-// Build (once per tile shape) the segment table and the chunk table.
+// Build (once per tile shape) the segment table and the split-row chunk table.
+//   team  rows: len <= G*iter            (LN sub-groups per row, LN | G)
+//   block rows: len <= CH = 4G*chunk_iter (one workgroup per row)
+//   split rows: longer                   (one workgroup per CH-nnz chunk + combine_kernel)
+// Classification is by power-of-two length bucket (rows are sorted by length).
 int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out) {
   const int key = LF * 8 + VEC;
   auto it = L->plans.find(key);
@@ -425,74 +452,83 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out) {
     t.total_blocks = (int32_t)ceil_div(n, 4 * tpw);
     snprintf(buf, sizeof(buf), "team rows[0,%lld) ln=%d (no reorder)\n", (long long)n, ln);
     p.text = buf;
-  } else {
-    // rows are sorted by descending length: highest bucket first
-    int64_t n_chunk_rows = 0;
-    for (int b = kBuckets - 1; b >= 0; --b) {
-      const int64_t maxlen = (b == 0) ? 1 : (1ll << b);
-      if (maxlen > team_max) n_chunk_rows += L->bucket[b];
-    }
-    int nseg = 0;
-    int32_t blk = 0;
-    if (n_chunk_rows > 0) {
-      std::vector<int32_t> rp(n_chunk_rows + 1);
-      WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n_chunk_rows + 1), hipMemcpyDeviceToHost));
-      std::vector<ChunkDesc> ch;
-      for (int64_t r = 0; r < n_chunk_rows; ++r) {
-        const int64_t len = rp[r + 1] - rp[r];
-        const int cnt = (int)std::max<int64_t>(1, ceil_div(len, CH));
-        const int first = (int)ch.size();
-        for (int q = 0; q < cnt; ++q) {
-          ChunkDesc d{};
-          d.row = (int32_t)r;
-          d.e0 = (int32_t)(rp[r] + q * CH);
-          d.e1 = (int32_t)std::min<int64_t>(rp[r + 1], rp[r] + (q + 1) * CH);
-          d.first = first;
-          d.count = cnt;
-          ch.push_back(d);
-        }
+    auto res = L->plans.emplace(key, p);
+    *out = &res.first->second;
+    return WG_OK;
+  }
+  int64_t n_split = 0, n_block = 0;
+  for (int b = kBuckets - 1; b >= 0; --b) {
+    const int64_t maxlen = (b == 0) ? 1 : (1ll << b);
+    if (maxlen > CH) n_split += L->bucket[b];
+    else if (maxlen > team_max) n_block += L->bucket[b];
+  }
+  int nseg = 0;
+  int32_t blk = 0;
+  if (n_split > 0) {
+    std::vector<int32_t> rp(n_split + 1);
+    WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n_split + 1), hipMemcpyDeviceToHost));
+    std::vector<ChunkDesc> ch;
+    std::vector<int2> rc(n_split);
+    for (int64_t r = 0; r < n_split; ++r) {
+      const int64_t len = rp[r + 1] - rp[r];
+      const int cnt = (int)std::max<int64_t>(1, ceil_div(len, CH));
+      rc[r] = make_int2((int)ch.size(), cnt);
+      for (int q = 0; q < cnt; ++q) {
+        ChunkDesc d{};
+        d.row = (int32_t)r;
+        d.e0 = (int32_t)(rp[r] + q * CH);
+        d.e1 = (int32_t)std::min<int64_t>(rp[r + 1], rp[r] + (q + 1) * CH);
+        ch.push_back(d);
       }
-      p.n_chunks = (int32_t)ch.size();
-      int rc = dmalloc(&p.chunks, ch.size());
-      if (!rc) rc = dmalloc(&p.partial, ch.size() * (size_t)p.width);
-      if (!rc) rc = dmalloc(&p.arrive, ch.size());
-      if (rc) {
-        p.release();
-        return rc;
-      }
-      WG_HIP_TRY(hipMemcpy(p.chunks, ch.data(), sizeof(ChunkDesc) * ch.size(), hipMemcpyHostToDevice));
-      WG_HIP_TRY(hipMemset(p.arrive, 0, sizeof(unsigned int) * ch.size()));
-      t.s[nseg++] = Seg{0, p.n_chunks, 0, 4 * G, 1};
-      blk = p.n_chunks;
-      snprintf(buf, sizeof(buf), "chunk rows[0,%lld) chunks=%d CH=%lld\n", (long long)n_chunk_rows, p.n_chunks,
-               (long long)CH);
-      p.text += buf;
     }
-    int32_t row = (int32_t)n_chunk_rows;
-    for (int b = kBuckets - 1; b >= 0; --b) {
-      const int32_t cnt = (int32_t)L->bucket[b];
-      const int64_t maxlen = (b == 0) ? 1 : (1ll << b);
-      if (!cnt || maxlen > team_max) continue;
-      int ln = divisor_at_least(G, ceil_div(maxlen, iter));
-      Seg* last = nseg ? &t.s[nseg - 1] : nullptr;
-      if (last && last->mode == 0 && (last->ln == ln || nseg == kMaxSeg)) {
-        if (last->ln != ln) ln = last->ln;  // out of slots: extend
-        last->end = row + cnt;
-        blk = last->blk_begin + (int32_t)ceil_div(last->end - last->begin, 4 * (G / ln));
-      } else {
-        t.s[nseg++] = Seg{row, row + cnt, blk, ln, 0};
-        blk += (int32_t)ceil_div(cnt, 4 * (G / ln));
-      }
-      row += cnt;
+    p.n_chunks = (int32_t)ch.size();
+    p.n_split = (int32_t)n_split;
+    int rc_ = dmalloc(&p.chunks, ch.size());
+    if (!rc_) rc_ = dmalloc(&p.partial, ch.size() * (size_t)p.width);
+    if (!rc_) rc_ = dmalloc(&p.rowchunks, rc.size());
+    if (rc_) {
+      p.release();
+      return rc_;
     }
-    t.n = nseg;
-    t.total_blocks = blk;
-    for (int i = 0; i < nseg; ++i) {
-      if (t.s[i].mode != 0) continue;
-      snprintf(buf, sizeof(buf), "team rows[%d,%d) ln=%d blocks=%d\n", t.s[i].begin, t.s[i].end, t.s[i].ln,
-               (i + 1 < nseg ? t.s[i + 1].blk_begin : blk) - t.s[i].blk_begin);
-      p.text += buf;
+    WG_HIP_TRY(hipMemcpy(p.chunks, ch.data(), sizeof(ChunkDesc) * ch.size(), hipMemcpyHostToDevice));
+    WG_HIP_TRY(hipMemcpy(p.rowchunks, rc.data(), sizeof(int2) * rc.size(), hipMemcpyHostToDevice));
+    t.s[nseg++] = Seg{0, p.n_chunks, 0, G, 2};
+    blk = p.n_chunks;
+    snprintf(buf, sizeof(buf), "split rows[0,%lld) chunks=%d CH=%lld (+combine)\n", (long long)n_split, p.n_chunks,
+             (long long)CH);
+    p.text += buf;
+  }
+  if (n_block > 0) {
+    t.s[nseg++] = Seg{(int32_t)n_split, (int32_t)(n_split + n_block), blk, G, 1};
+    blk += (int32_t)n_block;
+    snprintf(buf, sizeof(buf), "block rows[%lld,%lld) (workgroup per row)\n", (long long)n_split,
+             (long long)(n_split + n_block));
+    p.text += buf;
+  }
+  int32_t row = (int32_t)(n_split + n_block);
+  const int first_team = nseg;
+  for (int b = kBuckets - 1; b >= 0; --b) {
+    const int32_t cnt = (int32_t)L->bucket[b];
+    const int64_t maxlen = (b == 0) ? 1 : (1ll << b);
+    if (!cnt || maxlen > team_max) continue;
+    int ln = divisor_at_least(G, ceil_div(maxlen, iter));
+    Seg* last = nseg > first_team ? &t.s[nseg - 1] : nullptr;
+    if (last && (last->ln == ln || nseg == kMaxSeg)) {
+      if (last->ln != ln) ln = last->ln;  // out of slots: extend
+      last->end = row + cnt;
+      blk = last->blk_begin + (int32_t)ceil_div(last->end - last->begin, 4 * (G / ln));
+    } else {
+      t.s[nseg++] = Seg{row, row + cnt, blk, ln, 0};
+      blk += (int32_t)ceil_div(cnt, 4 * (G / ln));
     }
+    row += cnt;
+  }
+  t.n = nseg;
+  t.total_blocks = blk;
+  for (int i = first_team; i < nseg; ++i) {
+    snprintf(buf, sizeof(buf), "team rows[%d,%d) ln=%d blocks=%d\n", t.s[i].begin, t.s[i].end, t.s[i].ln,
+             (i + 1 < nseg ? t.s[i + 1].blk_begin : blk) - t.s[i].blk_begin);
+    p.text += buf;
   }
   auto res = L->plans.emplace(key, p);
   *out = &res.first->second;
@@ -511,7 +547,6 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     Plan* plan = nullptr;
     int rc = get_plan(L, LF, vec, &plan);
     if (rc) return rc;
-    if (plan->tab.total_blocks == 0) continue;
     StepArgs a{};
     a.rowptr = L->rowptr;
     a.col = L->col;
@@ -529,11 +564,10 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.alpha_k = alpha_k;
     a.chunks = plan->chunks;
     a.partial = plan->partial;
-    a.arrive = plan->arrive;
     a.seg_mask = L->tune.seg_mask;
-    if (vec == 4) rc = launch_step_vec<4>(L, a, plan->tab, stream);
-    else if (vec == 2) rc = launch_step_vec<2>(L, a, plan->tab, stream);
-    else rc = launch_step_vec<1>(L, a, plan->tab, stream);
+    if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
+    else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
+    else rc = launch_step_vec<1>(*plan, a, stream);
     if (rc) return rc;
   }
   if (H && !fuse_h) {

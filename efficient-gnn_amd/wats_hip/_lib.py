@@ -60,6 +60,7 @@ SIGNATURES = {
     "wg_profile_collect": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64),
                                           ctypes.POINTER(ctypes.c_double)]),
     "wg_row_l1_normalize": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "wg_laplacian_map_rows": (ctypes.c_int, [c_vp, c_i32, c_vp, c_i64, c_vp, c_vp]),
     "wg_gather_rows": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
 }
 

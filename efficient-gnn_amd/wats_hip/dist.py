@@ -1,0 +1,245 @@
+"""Row-sharded multi-GPU graph-wavelet path.
+
+One process per GPU.  A graph too large (or too slow) for one GPU is split
+into contiguous 1-D row blocks balanced by nonzeros.  Each rank owns the rows
+``[r0, r1)`` of ``L_hat`` and keeps its column space as ``[owned rows | halo
+rows]``, with the halo rows grouped by owner rank.  Row i of ``T_k`` needs
+``T_{k-1}`` at i's neighbours, plus ``T_{k-2}`` and ``S`` at row i only.  So the
+only exchange per Chebyshev step (reference ``calibration/WATS.py:35-36``) is
+the halo rows of ``T_{k-1}``.  That is one all-to-all-v, done with
+``torch.distributed.all_to_all_single``, which is RCCL over xGMI with the
+"nccl" backend.  The heat sum and the row-L1 normalisation are row-local.
+
+Setup also needs the Laplacian's column degree ``w = colsum(A) - diag(A)``
+(scipy ``_laplacian.py:467``).  It spans all shards, so it costs one
+all-reduce of float64 partial column sums.
+
+The planning functions (:func:`partition_rows`, :func:`build_halo_plan`,
+:func:`global_column_degree`) are plain numpy / torch.distributed and run on
+any backend (CPU-tested with gloo).  :class:`ShardedWavelet` runs the HIP
+kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def partition_rows(indptr: np.ndarray, world: int) -> np.ndarray:
+    """Contiguous row blocks balanced by (nnz + rows): returns ``bounds`` of
+    length world+1 with rank q owning rows [bounds[q], bounds[q+1])."""
+    indptr = np.asarray(indptr, dtype=np.int64)
+    n = len(indptr) - 1
+    weight = indptr + np.arange(n + 1)           # cumulative nnz + rows
+    total = weight[-1]
+    targets = (np.arange(1, world) * total) // world
+    cuts = np.searchsorted(weight, targets, side="left")
+    bounds = np.concatenate([[0], np.clip(cuts, 0, n), [n]]).astype(np.int64)
+    return np.maximum.accumulate(bounds)
+
+
+@dataclass
+class HaloPlan:
+    rank: int
+    world: int
+    bounds: np.ndarray
+    r0: int
+    r1: int
+    n_halo: int
+    halo_global: np.ndarray                 # global ids of halo rows (grouped by owner, ascending)
+    recv_counts: list                       # halo rows received from each peer
+    send_counts: list                       # rows sent to each peer
+    send_rows: np.ndarray                   # local (caller-order) row ids to send, grouped by peer
+    local_indices: np.ndarray               # CSR columns renumbered to [own | halo]
+    stats: dict = field(default_factory=dict)
+
+    @property
+    def n_own(self) -> int:
+        return self.r1 - self.r0
+
+    @property
+    def n_cols(self) -> int:
+        return self.n_own + self.n_halo
+
+
+def _device_for(group) -> torch.device:
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def exchange_int_lists(lists: list, group=None) -> list:
+    """All-to-all of variable-length int64 arrays: lists[q] goes to rank q;
+    returns what every rank sent to us (index = source rank)."""
+    world = dist.get_world_size(group)
+    dev = _device_for(group)
+    send_counts = torch.tensor([len(x) for x in lists], dtype=torch.int64, device=dev)
+    recv_counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    rc = recv_counts.cpu().tolist()
+    sc = send_counts.cpu().tolist()
+    send = torch.from_numpy(np.concatenate([np.asarray(x, np.int64) for x in lists]) if sum(sc) else
+                            np.zeros(0, np.int64)).to(dev)
+    recv = torch.empty(sum(rc), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc, group=group)
+    out = recv.cpu().numpy()
+    offs = np.concatenate([[0], np.cumsum(rc)])
+    return [out[offs[q]:offs[q + 1]] for q in range(world)]
+
+
+def build_halo_plan(indptr_local: np.ndarray, indices_global: np.ndarray, bounds: np.ndarray, group=None) -> HaloPlan:
+    """Renumber this rank's CSR columns to [own | halo] and agree with every
+    peer on who sends which rows (collective)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+    cols = np.asarray(indices_global, dtype=np.int64)
+    own = (cols >= r0) & (cols < r1)
+    halo_global = np.unique(cols[~own])
+    n_own = r1 - r0
+    local = np.empty(cols.shape, dtype=np.int64)
+    local[own] = cols[own] - r0
+    local[~own] = n_own + np.searchsorted(halo_global, cols[~own])
+    owner = np.searchsorted(bounds, halo_global, side="right") - 1
+    recv_lists = [halo_global[owner == q] for q in range(world)]
+    requested = exchange_int_lists(recv_lists, group)      # what each peer needs from us
+    send_rows = np.concatenate(requested).astype(np.int64) - r0 if world else np.zeros(0, np.int64)
+    assert np.all((send_rows >= 0) & (send_rows < max(n_own, 1))) or send_rows.size == 0
+    plan = HaloPlan(rank=rank, world=world, bounds=np.asarray(bounds), r0=r0, r1=r1, n_halo=int(halo_global.size),
+                    halo_global=halo_global, recv_counts=[int(len(x)) for x in recv_lists],
+                    send_counts=[int(len(x)) for x in requested], send_rows=send_rows.astype(np.int32),
+                    local_indices=local.astype(np.int32))
+    plan.stats = dict(n_own=n_own, n_halo=plan.n_halo, nnz_local=int(cols.size),
+                      nnz_remote=int((~own).sum()), send_rows=int(send_rows.size))
+    return plan
+
+
+def global_column_degree(partial_colsum: torch.Tensor, partial_diag: torch.Tensor, plan: HaloPlan,
+                         group=None) -> torch.Tensor:
+    """``w = colsum(A) - diag(A)`` for the columns [own | halo] of this rank:
+    all-reduce the float64 partial sums, then scipy's float32 subtraction."""
+    dev = _device_for(group)
+    cs = partial_colsum.to(dev, torch.float64)
+    dg = partial_diag.to(dev, torch.float64)
+    dist.all_reduce(cs, group=group)
+    dist.all_reduce(dg, group=group)
+    ids = torch.from_numpy(np.concatenate([np.arange(plan.r0, plan.r1), plan.halo_global]).astype(np.int64)).to(dev)
+    return cs[ids].to(torch.float32) - dg[ids].to(torch.float32)
+
+
+def halo_exchange(ext: torch.Tensor, plan: HaloPlan, pack, sendbuf: torch.Tensor, group=None,
+                  host_staged: bool = False) -> None:
+    """Fill the halo rows ``ext[n_own:]`` of the extended vector with the
+    owners' current values: pack the rows each peer asked for (``pack(ext,
+    sendbuf)``), then one all-to-all-v.  Collective: every rank calls it every
+    step, also with nothing to send."""
+    if plan.world == 1:
+        return
+    pack(ext, sendbuf)
+    recv = ext[plan.n_own:]
+    if not host_staged:
+        dist.all_to_all_single(recv, sendbuf, output_split_sizes=plan.recv_counts,
+                               input_split_sizes=plan.send_counts, group=group)
+    else:
+        r = torch.empty(plan.n_halo, ext.shape[1], dtype=ext.dtype)
+        dist.all_to_all_single(r, sendbuf.cpu(), output_split_sizes=plan.recv_counts,
+                               input_split_sizes=plan.send_counts, group=group)
+        recv.copy_(r.to(ext.device))
+
+
+class ShardedWavelet:
+    """One rank's shard of ``L_hat`` on its GPU, plus the halo exchange.
+
+    ``exchange="nccl"``: all_to_all_single on device buffers (RCCL/xGMI).
+    ``exchange="host"``: the same collective on host copies (gloo) -- lets
+    several ranks share one GPU in tests; never used for timing.
+    """
+
+    def __init__(self, indptr_local, indices_global, values_local, n_global: int, bounds, group=None,
+                 exchange: str = "nccl", device=None):
+        from .laplacian import NormalizedLaplacian, require_gpu
+        self.device = require_gpu(device)
+        self.group = group
+        self.exchange = exchange
+        indptr_local = np.asarray(indptr_local, np.int64)
+        self.plan = build_halo_plan(indptr_local, indices_global, bounds, group)
+        p = self.plan
+        # partial column degrees of this shard, on the GPU (float64 atomics)
+        lib = _lib.load()
+        ip = torch.from_numpy(indptr_local).to(self.device)
+        ix = torch.from_numpy(np.asarray(indices_global, np.int32)).to(self.device)
+        vals = None if values_local is None else torch.as_tensor(np.asarray(values_local, np.float32)).to(self.device)
+        colsum = torch.zeros(n_global, dtype=torch.float64, device=self.device)
+        diag = torch.zeros(n_global, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            check(lib.wg_column_degree(p.n_own, p.r0, ptr(ip), ptr(ix) if ix.numel() else None, ptr(vals),
+                                       ptr(colsum), ptr(diag), st), "column_degree")
+        w_cols = global_column_degree(colsum, diag, p, group).to(self.device)
+        del colsum, diag
+        self.L = NormalizedLaplacian(p.n_own, ip, torch.from_numpy(p.local_indices), vals, n_cols=p.n_cols,
+                                     w_cols=w_cols, device=self.device)
+        rows = torch.from_numpy(p.send_rows).to(self.device)
+        self.send_rows = torch.empty_like(rows)
+        if rows.numel():
+            with torch.cuda.device(self.device):
+                check(lib.wg_laplacian_map_rows(self.L.handle, 0, ptr(rows), rows.numel(), ptr(self.send_rows),
+                                                torch.cuda.current_stream(self.device).cuda_stream), "map_rows")
+        self._bufs = {}
+
+    # -------------------------------------------------------------- exchange
+    def _pack(self, ext: torch.Tensor, out: torch.Tensor) -> None:
+        n = int(self.send_rows.numel())
+        if n:
+            with torch.cuda.device(self.device):
+                check(_lib.load().wg_gather_rows(ptr(ext), ptr(self.send_rows), n, ext.shape[1], ptr(out),
+                                                 torch.cuda.current_stream(self.device).cuda_stream), "gather_rows")
+
+    def _halo_exchange(self, ext: torch.Tensor) -> None:
+        sendbuf = self._buf("send", int(self.send_rows.numel()), ext.shape[1])
+        halo_exchange(ext, self.plan, self._pack, sendbuf, self.group, host_staged=(self.exchange != "nccl"))
+
+    def _buf(self, name, rows, F):
+        key = (name, F)
+        b = self._bufs.get(key)
+        if b is None or b.shape[0] < rows:
+            b = torch.empty(max(rows, 1), F, dtype=torch.float32, device=self.device)
+            self._bufs[key] = b
+        return b[:rows]
+
+    # -------------------------------------------------------------- chain
+    def wavelet_features(self, X0_local: torch.Tensor, k: int = 3, s: float = 0.8):
+        """Owned rows of (H, S) for signal rows X0_local (caller order)."""
+        import math
+        p = self.plan
+        L = self.L
+        X = X0_local.to(self.device, torch.float32).reshape(p.n_own, -1).contiguous()
+        F = X.shape[1]
+        A = self._buf("A", p.n_cols, F)
+        B = self._buf("B", p.n_cols, F)
+        S = self._buf("S", p.n_own, F)
+        with torch.cuda.device(self.device):
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            if p.n_own:
+                check(_lib.load().wg_permute_rows(L.handle, 0, F, ptr(X), ptr(A), st), "permute_rows")
+        if k == 0:
+            S.copy_(A[: p.n_own])
+        bufs = (A, B)
+        for i in range(1, k + 1):
+            cur = bufs[(i - 1) % 2]
+            nxt = bufs[i % 2]
+            self._halo_exchange(cur)
+            L.step(i, cur, None if i == 1 else nxt[: p.n_own], None if i == k else nxt[: p.n_own], S=S,
+                   alpha0=1.0, alpha_k=math.exp(-s * i))
+        from .wavelet import row_l1_normalize
+        H_int = row_l1_normalize(S) if p.n_own else S.clone()
+        S_out = L.permute(S, to_internal=False) if p.n_own else S.clone()
+        H_out = L.permute(H_int, to_internal=False) if p.n_own else H_int
+        return H_out, S_out

@@ -175,6 +175,11 @@ int wg_profile_collect(wg_laplacian_t L, double* sum_ms_host, int64_t* launches_
 /* a6 standalone: H = S / (||S||_1,row + 1e-8) (calibration/WATS.py:71-72). */
 int wg_row_l1_normalize(const float* S, float* H, int64_t n_rows, int64_t F, void* stream);
 
+/* Row-id mapping between the caller's numbering and the internal one:
+ * direction 0: out[i] = internal id of caller row rows[i]; 1: the inverse. */
+int wg_laplacian_map_rows(wg_laplacian_t L, int32_t direction, const int32_t* rows, int64_t n,
+                          int32_t* out, void* stream);
+
 /* Multi-GPU halo pack: dst[i] = src[rows[i]] for i < n (row stride F). */
 int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, float* dst,
                    void* stream);
