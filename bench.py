@@ -154,7 +154,10 @@ def main():
 
     if rank == 0:
         avg_ms = prof["sum_ms"] / max(1, prof["launches"])
-        b_step = algorithmic_bytes(n, nnz, F)
+        # the step kernel processes the rows that enter the chain; purely
+        # isolated rows (closed form T_k = (-1)^k X0) are handled by finalize
+        n_active = n - int(L.info["n_closed_form"])
+        b_step = algorithmic_bytes(n_active, nnz, F)
         achieved = b_step / (avg_ms * 1e-3) / 1e9
         traffic = None
         if args.traffic_json and os.path.exists(args.traffic_json):
@@ -189,6 +192,9 @@ def main():
                 "traffic": traffic,
                 "kernel": "cheb_step_kernel",
                 "algorithmic_bytes_per_launch": b_step,
+                "rows_per_launch": n_active,
+                "closed_form_rows": n - n_active,
+                "algorithmic_bytes_all_rows": algorithmic_bytes(n, nnz, F),
                 "avg_launch_us": avg_ms * 1e3,
                 "max_launch_us": prof["max_ms"] * 1e3,
                 "launches": prof["launches"],

@@ -63,6 +63,7 @@ int wg_laplacian_get_info(wg_laplacian_t L, wg_laplacian_info* info) {
   info->n_segments = 0;
   for (auto& kv : L->plans) info->n_segments = std::max(info->n_segments, kv.second.tab.n);
   info->reordered = L->reordered ? 1 : 0;
+  info->n_closed_form = L->n_closed;
   return WG_OK;
 }
 
@@ -92,10 +93,10 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
   const int vec = (F % 4 == 0) ? 4 : (F % 2 == 0) ? 2 : 1;
   const int LF = (int)(std::min<int64_t>(F, 64 * vec) / vec);
   Plan* p = nullptr;
-  if (get_plan(L, LF, vec, &p)) return "";
+  if (get_plan(L, LF, vec, true, &p)) return "";
   char buf[128];
-  snprintf(buf, sizeof(buf), "F=%lld VEC=%d LF=%d segments=%d blocks=%d\n", (long long)F, vec, LF, p->tab.n,
-           p->tab.total_blocks);
+  snprintf(buf, sizeof(buf), "F=%lld VEC=%d LF=%d segments=%d blocks=%d active_rows=%lld closed_form_rows=%lld\n",
+           (long long)F, vec, LF, p->tab.n, p->tab.total_blocks, (long long)L->n_active, (long long)L->n_closed);
   g_text = buf + p->text;
   return g_text.c_str();
 }
@@ -139,6 +140,10 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   int rc = launch_permute(L, 0, F, X0, b0, stream);
   if (rc) return rc;
   if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * F, hipMemcpyDeviceToDevice, stream));
+  // purely isolated rows (internal rows >= n_active) never enter the chain:
+  // T_k = (-1)^k X0 exactly, so S = X0 * sum_k (-1)^k alpha_k (WATS.py:65-68)
+  double coef = 0.0;
+  for (int32_t k = 0; k <= K; ++k) coef += ((k & 1) ? -1.0 : 1.0) * std::exp(-s * (double)k);
   for (int32_t k = 1; k <= K; ++k) {
     const float* xm1 = (k & 1) ? b0 : b1;
     const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
@@ -155,11 +160,11 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
       e_stop = L->ev[L->ev_used + 1];
       L->ev_used += 2;
     }
-    rc = launch_step(L, k, F, xm1, xm2, xk, sint, nullptr, 1.0, ak, stream);
+    rc = launch_step(L, k, F, xm1, xm2, xk, sint, nullptr, 1.0, ak, stream, /*active_only=*/true);
     if (rc) return rc;
     if (e_stop) WG_HIP_TRY(hipEventRecord(e_stop, stream));
   }
-  return launch_finalize(L, F, sint, S, H, stream);
+  return launch_finalize(L, F, sint, b0, coef, S, H, stream);
 }
 
 int wg_profile_enable(wg_laplacian_t L, int32_t enable) {

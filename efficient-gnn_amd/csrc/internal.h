@@ -96,8 +96,10 @@ struct wg_laplacian_s {
   float* rowsum = nullptr;    // caller order, float32 (for X0)
   unsigned int bucket[wg::kBuckets] = {0};  // rows per length bucket (internal rows sorted descending)
   int64_t avg_len = 0;
+  int64_t n_active = 0;       // rows [0, n_active) enter the chain in wg_wavelet_features
+  int64_t n_closed = 0;       // purely isolated rows at the end: T_k = (-1)^k X0 (closed form)
   wg::Tuning tune;
-  std::map<int, wg::Plan> plans;  // key: LF * 8 + VEC
+  std::map<int, wg::Plan> plans;  // key: (LF * 8 + VEC) * 2 + active_only
   // workspace for wg_wavelet_features
   float* ws = nullptr;
   size_t ws_floats = 0;
@@ -112,10 +114,11 @@ struct wg_laplacian_s {
 namespace wg {
 // step.hip
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
-int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out);
+int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out);
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
-                float* S, float* H, double alpha0, double alpha_k, hipStream_t stream);
-int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, float* S, float* H, hipStream_t stream);
+                float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false);
+int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef,
+                    float* S, float* H, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);
 }  // namespace wg

@@ -31,7 +31,7 @@ namespace {
 __global__ __launch_bounds__(kBlock) void row_info_kernel(
     int64_t n_rows, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ values, int32_t* __restrict__ offdiag_len, double* __restrict__ rowsum,
-    float* __restrict__ diag, double* __restrict__ colsum) {
+    float* __restrict__ diag, double* __restrict__ colsum, int32_t* __restrict__ colcnt) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n_rows) return;
@@ -43,7 +43,12 @@ __global__ __launch_bounds__(kBlock) void row_info_kernel(
     const int32_t c = indices[e];
     const float v = values ? values[e] : 1.0f;
     rs += (double)v;
-    if (c == row) dg += v; else ++cnt;
+    if (c == row) {
+      dg += v;
+    } else {
+      ++cnt;
+      atomicAdd(colcnt + c, 1);
+    }
     if (colsum) atomicAdd(colsum + c, (double)v);
   }
   for (int off = 32; off >= 1; off >>= 1) {
@@ -89,6 +94,22 @@ __global__ void degree_kernel(int64_t n_cols, int64_t n_rows, const float* __res
   const bool iso = (w == 0.0f);
   sw[j] = iso ? 1.0f : sqrtf(w);
   iso_col[j] = iso ? 1 : 0;
+}
+
+// Sort key: off-diagonal length, then "needed in the chain" (0 for purely
+// isolated rows: w_i == 0, no off-diagonal entries in row i or column i --
+// T_k,i = (-1)^k X0_i in closed form and no other row gathers it).
+__global__ void sort_key_kernel(int64_t n, const int32_t* __restrict__ len, const int32_t* __restrict__ colcnt,
+                                const uint8_t* __restrict__ iso_col, int allow_closed, unsigned long long* __restrict__ key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool pure = allow_closed && iso_col[i] && len[i] == 0 && colcnt[i] == 0;
+  key[i] = ((unsigned long long)len[i] << 1) | (pure ? 0ull : 1ull);
+}
+
+__global__ void count_pure_kernel(int64_t n, const unsigned long long* __restrict__ key, unsigned int* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && key[i] == 0ull) atomicAdd(cnt, 1u);
 }
 
 __global__ void iota_kernel(int64_t n, int32_t* __restrict__ out) {
@@ -288,6 +309,13 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   uint8_t* iso_col;
   unsigned int* hist;
   int rc = 0;
+  int32_t* colcnt;
+  unsigned long long *key, *key_sorted;
+  unsigned int* npure_d;
+  if ((rc = tmp.alloc(&colcnt, n_cols)) || (rc = tmp.alloc(&key, n_rows)) || (rc = tmp.alloc(&key_sorted, n_rows)) ||
+      (rc = tmp.alloc(&npure_d, 1)))
+    return rc;
+  WG_HIP_TRY(hipMemsetAsync(colcnt, 0, sizeof(int32_t) * std::max<int64_t>(1, n_cols), stream));
   if ((rc = tmp.alloc(&len, n_rows)) || (rc = tmp.alloc(&len_sorted, n_rows)) || (rc = tmp.alloc(&ids, n_rows)) ||
       (rc = tmp.alloc(&rowsum64, n_rows)) || (rc = tmp.alloc(&diag, n_rows)) || (rc = tmp.alloc(&colsum32, n_cols)) ||
       (rc = tmp.alloc(&sw, n_cols)) || (rc = tmp.alloc(&iso_col, n_cols)) || (rc = tmp.alloc(&hist, kBuckets)))
@@ -302,7 +330,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   }
   if (n_rows > 0) {
     hipLaunchKernelGGL(row_info_kernel, dim3(ceil_div(n_rows, 4)), dim3(kBlock), 0, stream, n_rows, indptr, indices,
-                       values, len, rowsum64, diag, colsum64);
+                       values, len, rowsum64, diag, colsum64, colcnt);
     WG_LAUNCH_CHECK();
   }
   if (w_cols == nullptr && n_cols > 0) {
@@ -345,15 +373,28 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
     WG_HIP_TRY(hipStreamSynchronize(stream));
     return WG_OK;
   }
+  L->n_active = n_rows;
   // relabelling by descending off-diagonal length (stable: ties keep caller order)
   hipLaunchKernelGGL(iota_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, ids);
   WG_LAUNCH_CHECK();
   if (L->reordered) {
+    // closed-form rows only on a whole-graph handle (a shard's rows may be halo rows elsewhere)
+    const int allow_closed = (w_cols == nullptr) ? 1 : 0;
+    hipLaunchKernelGGL(sort_key_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, len, colcnt, iso_col, allow_closed,
+                       key);
+    WG_LAUNCH_CHECK();
     rc = cub_call(stream, [&](void* t, size_t& b) {
-      return hipcub::DeviceRadixSort::SortPairsDescending(t, b, len, len_sorted, ids, L->perm, (int)n_rows, 0, 32,
+      return hipcub::DeviceRadixSort::SortPairsDescending(t, b, key, key_sorted, ids, L->perm, (int)n_rows, 0, 33,
                                                           stream);
     });
     if (rc) return rc;
+    WG_HIP_TRY(hipMemsetAsync(npure_d, 0, sizeof(unsigned int), stream));
+    hipLaunchKernelGGL(count_pure_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, key, npure_d);
+    WG_LAUNCH_CHECK();
+    unsigned int npure = 0;
+    WG_HIP_TRY(hipMemcpyAsync(&npure, npure_d, sizeof(unsigned int), hipMemcpyDeviceToHost, stream));
+    WG_HIP_TRY(hipStreamSynchronize(stream));
+    L->n_active = n_rows - (int64_t)npure;
   } else {
     WG_HIP_TRY(hipMemcpyAsync(L->perm, ids, sizeof(int32_t) * n_rows, hipMemcpyDeviceToDevice, stream));
   }
@@ -399,6 +440,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   L->n_iso = niso;
   L->max_row = max_len;
   L->avg_len = L->nnz / n_rows;
+  L->n_closed = n_rows - L->n_active;
   return WG_OK;
 }
 

@@ -282,9 +282,12 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
 }
 
 // internal S -> caller-order S and H = S / (||S||_1 + 1e-8); team of LF lanes per row.
+// Rows >= closed_from are purely isolated (T_k = (-1)^k X0): S = coef * X0
+// with coef = sum_k (-1)^k alpha_k, read from the untouched T_0 rows.
 template <int VEC>
 __global__ __launch_bounds__(kBlock) void finalize_kernel(int64_t n, int64_t F, int LF, const int32_t* __restrict__ perm,
-                                                          const float* __restrict__ Sint, float* __restrict__ S,
+                                                          const float* __restrict__ Sint, const float* __restrict__ X0int,
+                                                          int64_t closed_from, double coef, float* __restrict__ S,
                                                           float* __restrict__ H) {
   const int lane = threadIdx.x & 63;
   const int G = 64 / LF;
@@ -292,44 +295,51 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(int64_t n, int64_t F, 
   const int fs = lane - sg * LF;
   const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + sg;
   const bool active = sg < G && row < n;
+  const bool closed = row >= closed_from;
   float x[VEC];
+  double s[VEC];
   double part = 0.0;
   if (active) {
-    load_vec<VEC>(Sint + row * F + fs * VEC, x);
+    load_vec<VEC>((closed ? X0int : Sint) + row * F + fs * VEC, x);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) part += fabs((double)x[j]);
+    for (int j = 0; j < VEC; ++j) {
+      s[j] = closed ? coef * (double)x[j] : (double)x[j];
+      part += fabs(s[j]);
+    }
   }
   double tot = 0.0;
   for (int q = 0; q < LF; ++q) tot += __shfl(part, sg * LF + q, 64);
   if (!active) return;
   const int64_t r = perm ? perm[row] : row;
-  double s[VEC], h[VEC];
+  double h[VEC];
   const double den = tot + 1e-8;
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) {
-    s[j] = (double)x[j];
-    h[j] = s[j] / den;
-  }
+  for (int j = 0; j < VEC; ++j) h[j] = s[j] / den;
   if (S) store_vec<VEC>(S + r * F + fs * VEC, s);
   if (H) store_vec<VEC>(H + r * F + fs * VEC, h);
 }
 
 // wide-F fallback (F > 64*VEC): wave per row.
 __global__ __launch_bounds__(kBlock) void finalize_wide_kernel(int64_t n, int64_t F, const int32_t* __restrict__ perm,
-                                                               const float* __restrict__ Sint, float* __restrict__ S,
+                                                               const float* __restrict__ Sint,
+                                                               const float* __restrict__ X0int, int64_t closed_from,
+                                                               double coef, float* __restrict__ S,
                                                                float* __restrict__ H) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n) return;
   const int64_t r = perm ? perm[row] : row;
+  const bool closed = row >= closed_from;
+  const float* src = closed ? X0int : Sint;
+  const double c = closed ? coef : 1.0;
   double part = 0.0;
-  for (int64_t f = lane; f < F; f += 64) part += fabs((double)Sint[row * F + f]);
+  for (int64_t f = lane; f < F; f += 64) part += fabs(c * (double)src[row * F + f]);
   for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off, 64);
   const double den = part + 1e-8;
   for (int64_t f = lane; f < F; f += 64) {
-    const float s = Sint[row * F + f];
-    if (S) S[r * F + f] = s;
-    if (H) H[r * F + f] = (float)((double)s / den);
+    const double s = c * (double)src[row * F + f];
+    if (S) S[r * F + f] = (float)s;
+    if (H) H[r * F + f] = (float)(s / den);
   }
 }
 
@@ -427,8 +437,9 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 //   block rows: len <= CH = 4G*chunk_iter (one workgroup per row)
 //   split rows: longer                   (one workgroup per CH-nnz chunk + combine_kernel)
 // Classification is by power-of-two length bucket (rows are sorted by length).
-int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out) {
-  const int key = LF * 8 + VEC;
+int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
+  active_only = active_only && L->reordered;
+  const int key = (LF * 8 + VEC) * 2 + (active_only ? 1 : 0);
   auto it = L->plans.find(key);
   if (it != L->plans.end()) {
     *out = &it->second;
@@ -437,7 +448,10 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out) {
   Plan p;
   p.width = LF * VEC;
   const int G = 64 / LF;
-  const int64_t n = L->n_rows;
+  const int64_t n = active_only ? L->n_active : L->n_rows;
+  unsigned int bucket[kBuckets];
+  for (int b = 0; b < kBuckets; ++b) bucket[b] = L->bucket[b];
+  bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
   const int iter = std::max(1, L->tune.iter);
   const int64_t team_max = (int64_t)G * iter;
   const int64_t CH = (int64_t)4 * G * std::max(1, L->tune.chunk_iter);
@@ -459,8 +473,8 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out) {
   int64_t n_split = 0, n_block = 0;
   for (int b = kBuckets - 1; b >= 0; --b) {
     const int64_t maxlen = (b == 0) ? 1 : (1ll << b);
-    if (maxlen > CH) n_split += L->bucket[b];
-    else if (maxlen > team_max) n_block += L->bucket[b];
+    if (maxlen > CH) n_split += bucket[b];
+    else if (maxlen > team_max) n_block += bucket[b];
   }
   int nseg = 0;
   int32_t blk = 0;
@@ -508,7 +522,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out) {
   int32_t row = (int32_t)(n_split + n_block);
   const int first_team = nseg;
   for (int b = kBuckets - 1; b >= 0; --b) {
-    const int32_t cnt = (int32_t)L->bucket[b];
+    const int32_t cnt = (int32_t)bucket[b];
     const int64_t maxlen = (b == 0) ? 1 : (1ll << b);
     if (!cnt || maxlen > team_max) continue;
     int ln = divisor_at_least(G, ceil_div(maxlen, iter));
@@ -536,7 +550,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, Plan** out) {
 }
 
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
-                float* H, double alpha0, double alpha_k, hipStream_t stream) {
+                float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only) {
   if (L->n_rows == 0) return WG_OK;
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H});
   const int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
@@ -545,7 +559,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     const int64_t fw = std::min<int64_t>(max_tile, F - f0);
     const int LF = (int)(fw / vec);
     Plan* plan = nullptr;
-    int rc = get_plan(L, LF, vec, &plan);
+    int rc = get_plan(L, LF, vec, active_only, &plan);
     if (rc) return rc;
     StepArgs a{};
     a.rowptr = L->rowptr;
@@ -577,19 +591,28 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
   return WG_OK;
 }
 
-int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, float* S, float* H, hipStream_t stream) {
+int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef, float* S,
+                    float* H, hipStream_t stream) {
+  const int64_t closed_from = X0int ? L->n_active : L->n_rows;
   const int64_t n = L->n_rows;
   if (n == 0) return WG_OK;
-  const int vec = pick_vec(F, {Sint, S, H});
+  const int vec = pick_vec(F, {Sint, X0int, S, H});
   if (F <= 64 * vec) {
     const int LF = (int)(F / vec);
     const int G = 64 / LF;
     const dim3 grid((unsigned)ceil_div(n, 4 * G));
-    if (vec == 4) hipLaunchKernelGGL(finalize_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, S, H);
-    else if (vec == 2) hipLaunchKernelGGL(finalize_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, S, H);
-    else hipLaunchKernelGGL(finalize_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, S, H);
+    if (vec == 4)
+      hipLaunchKernelGGL(finalize_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, X0int, closed_from,
+                         closed_coef, S, H);
+    else if (vec == 2)
+      hipLaunchKernelGGL(finalize_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, X0int, closed_from,
+                         closed_coef, S, H);
+    else
+      hipLaunchKernelGGL(finalize_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, X0int, closed_from,
+                         closed_coef, S, H);
   } else {
-    hipLaunchKernelGGL(finalize_wide_kernel, dim3(ceil_div(n, 4)), dim3(kBlock), 0, stream, n, F, L->perm, Sint, S, H);
+    hipLaunchKernelGGL(finalize_wide_kernel, dim3(ceil_div(n, 4)), dim3(kBlock), 0, stream, n, F, L->perm, Sint, X0int,
+                       closed_from, closed_coef, S, H);
   }
   WG_LAUNCH_CHECK();
   return WG_OK;

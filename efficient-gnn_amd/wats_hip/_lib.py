@@ -32,6 +32,7 @@ class LaplacianInfo(ctypes.Structure):
         ("max_row_nnz", c_i64),
         ("n_segments", c_i32),
         ("reordered", c_i32),
+        ("n_closed_form", c_i64),
     ]
 
     def as_dict(self) -> dict:

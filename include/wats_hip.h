@@ -54,6 +54,9 @@ typedef struct wg_laplacian_info {
   int64_t max_row_nnz;   /* longest L_hat row */
   int32_t n_segments;    /* row-length bins of the step kernel */
   int32_t reordered;     /* 1 if rows are relabelled by descending degree */
+  int64_t n_closed_form; /* purely isolated rows (w_i = 0, empty row and column):
+                            T_k = (-1)^k X0 exactly, kept out of the step kernel
+                            by wg_wavelet_features */
 } wg_laplacian_info;
 
 /* -------------------------------------------------------------------------
