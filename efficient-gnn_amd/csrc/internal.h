@@ -65,6 +65,7 @@ struct ChunkDesc {  // one workgroup's share of a split row
 
 struct Plan {
   SegTable tab{};
+  Seg* d_segs = nullptr;        // device copy of tab.s (read with scalar loads)
   int32_t n_chunks = 0;
   int32_t width = 0;            // LF * VEC doubles per partial
   int32_t n_split = 0;          // split rows = internal rows [0, n_split)
@@ -76,9 +77,11 @@ struct Plan {
 };
 
 struct Tuning {
-  int32_t iter = 8;         // team mode: target nonzeros per lane sub-group
-  int32_t chunk_iter = 32;  // block/split mode: nonzeros per sub-group per workgroup pass
-  int64_t seg_mask = -1;    // timing attribution only: launch only these segments
+  int32_t iter = 24;         // team mode: target nonzeros per lane sub-group
+  int32_t chunk_iter = 128;  // block/split mode: nonzeros per sub-group per workgroup
+  int32_t nt = 0;            // non-temporal hints: 1 = CSR col/val loads, 2 = own-row loads, 4 = stores
+  int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
+  int64_t seg_mask = -1;     // timing attribution only: launch only these segments
 };
 
 }  // namespace wg

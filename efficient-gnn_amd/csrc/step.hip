@@ -48,6 +48,7 @@ struct StepArgs {
   const ChunkDesc* chunks;
   double* partial;
   int64_t seg_mask;
+  int32_t nt;
 };
 
 template <int VEC>
@@ -60,6 +61,35 @@ __device__ __forceinline__ void load_vec(const float* p, float (&x)[VEC]) {
   } else {
     const float4 v = *reinterpret_cast<const float4*>(p);
     x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  }
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int VEC>
+__device__ __forceinline__ void load_vec_nt(const float* p, float (&x)[VEC]) {
+  if constexpr (VEC == 1) {
+    x[0] = __builtin_nontemporal_load(p);
+  } else if constexpr (VEC == 2) {
+    const f32x2 v = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(p));
+    x[0] = v.x; x[1] = v.y;
+  } else {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec_nt(float* p, const double (&x)[VEC]) {
+  if constexpr (VEC == 1) {
+    __builtin_nontemporal_store((float)x[0], p);
+  } else if constexpr (VEC == 2) {
+    f32x2 v = {(float)x[0], (float)x[1]};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(p));
+  } else {
+    f32x4 v = {(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
   }
 }
 
@@ -81,6 +111,8 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
                                               int lane0) {
   const int64_t off = row * a.ld + (int64_t)fs * VEC;
   float x[VEC];
+  const bool nt_ld = (a.nt & 2) != 0;
+  const bool nt_st = (a.nt & 4) != 0;
   if (a.iso[row]) {  // L_hat_ii = -1 (scipy setdiag(1 - iso), then "- identity")
     load_vec<VEC>(a.xm1 + off, x);
 #pragma unroll
@@ -91,11 +123,15 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
 #pragma unroll
     for (int j = 0; j < VEC; ++j) t[j] = acc[j];
   } else {
-    load_vec<VEC>(a.xm2 + off, x);
+    if (nt_ld) load_vec_nt<VEC>(a.xm2 + off, x);
+    else load_vec<VEC>(a.xm2 + off, x);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) t[j] = 2.0 * acc[j] - (double)x[j];
   }
-  if (a.xk) store_vec<VEC>(a.xk + off, t);
+  if (a.xk) {
+    if (nt_st) store_vec_nt<VEC>(a.xk + off, t);
+    else store_vec<VEC>(a.xk + off, t);
+  }
   if (a.S) {
     double s[VEC];
     if (a.k == 1) {  // S = alpha0*T_0 + alpha1*T_1, T_0 = own row of xm1
@@ -103,11 +139,13 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
 #pragma unroll
       for (int j = 0; j < VEC; ++j) s[j] = a.alpha0 * (double)x[j] + a.alpha_k * t[j];
     } else {
-      load_vec<VEC>(a.S + off, x);
+      if (nt_ld) load_vec_nt<VEC>(a.S + off, x);
+      else load_vec<VEC>(a.S + off, x);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) s[j] = (double)x[j] + a.alpha_k * t[j];
     }
-    store_vec<VEC>(a.S + off, s);
+    if (nt_st) store_vec_nt<VEC>(a.S + off, s);
+    else store_vec<VEC>(a.S + off, s);
     if (a.H) {
       double part = 0.0;
 #pragma unroll
@@ -123,10 +161,16 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
   }
 }
 
+template <bool NT, typename T>
+__device__ __forceinline__ T ldg(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 // acc += sum over e = e, e+stride, ... < e1 of val[e] * x[col[e]] (float64).
-template <int VEC>
-__device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
-                                           const float* __restrict__ xb, double (&acc)[VEC]) {
+template <int VEC, bool NT = false>
+__device__ __forceinline__ void accumulate_t(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                             const float* __restrict__ xb, double (&acc)[VEC]) {
   const int32_t* __restrict__ col = a.col;
   const float* __restrict__ val = a.val;
   const int64_t ld = a.ld;
@@ -135,8 +179,8 @@ __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t
     float v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      c[u] = col[e + u * stride];
-      v[u] = val[e + u * stride];
+      c[u] = ldg<NT>(col + e + u * stride);
+      v[u] = ldg<NT>(val + e + u * stride);
     }
     float x[4][VEC];
 #pragma unroll
@@ -147,13 +191,20 @@ __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t
       for (int j = 0; j < VEC; ++j) acc[j] = fma((double)v[u], (double)x[u][j], acc[j]);
   }
   for (; e < e1; e += stride) {
-    const int32_t c = col[e];
-    const float v = val[e];
+    const int32_t c = ldg<NT>(col + e);
+    const float v = ldg<NT>(val + e);
     float x[VEC];
     load_vec<VEC>(xb + (int64_t)c * ld, x);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] = fma((double)v, (double)x[j], acc[j]);
   }
+}
+
+template <int VEC>
+__device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                           const float* __restrict__ xb, double (&acc)[VEC]) {
+  if (a.nt & 1) accumulate_t<VEC, true>(a, e, e1, stride, xb, acc);
+  else accumulate_t<VEC, false>(a, e, e1, stride, xb, acc);
 }
 
 // Sum the partial sums of n lane sub-groups (lanes base + q*LF + fs, q < n)
@@ -181,12 +232,12 @@ __device__ __forceinline__ void reduce_subgroups(double (&acc)[VEC], int n, int 
 }
 
 template <int VEC>
-__global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, SegTable tab) {
+__global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
   __shared__ double red[4 * 64 * VEC];
   int si = 0;
-  for (int i = 1; i < tab.n; ++i)
-    if ((int32_t)blockIdx.x >= tab.s[i].blk_begin) si = i;
-  const Seg seg = tab.s[si];
+  for (int i = 1; i < nseg; ++i)
+    if ((int32_t)blockIdx.x >= segs[i].blk_begin) si = i;
+  const Seg seg = segs[si];
   if (!((a.seg_mask >> si) & 1)) return;  // timing attribution only
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -398,7 +449,8 @@ template <int VEC>
 int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const SegTable& tab = plan.tab;
   if (tab.total_blocks > 0) {
-    hipLaunchKernelGGL(cheb_step_kernel<VEC>, dim3(tab.total_blocks), dim3(kBlock), 0, stream, a, tab);
+    hipLaunchKernelGGL(cheb_step_kernel<VEC>, dim3(tab.total_blocks), dim3(kBlock), 0, stream, a,
+                       (const Seg*)plan.d_segs, tab.n);
     WG_LAUNCH_CHECK();
   }
   if (plan.n_split > 0 && ((a.seg_mask >> tab.n) & 1)) {
@@ -412,7 +464,18 @@ int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
 
 }  // namespace
 
+namespace {
+int upload_segs(Plan& p) {
+  int rc = dmalloc(&p.d_segs, kMaxSeg);
+  if (rc) return rc;
+  WG_HIP_TRY(hipMemcpy(p.d_segs, p.tab.s, sizeof(Seg) * kMaxSeg, hipMemcpyHostToDevice));
+  return WG_OK;
+}
+}  // namespace
+
 void Plan::release() {
+  (void)hipFree(d_segs);
+  d_segs = nullptr;
   (void)hipFree(chunks);
   (void)hipFree(partial);
   (void)hipFree(rowchunks);
@@ -466,6 +529,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
     t.total_blocks = (int32_t)ceil_div(n, 4 * tpw);
     snprintf(buf, sizeof(buf), "team rows[0,%lld) ln=%d (no reorder)\n", (long long)n, ln);
     p.text = buf;
+    if (int rc2 = upload_segs(p)) return rc2;
     auto res = L->plans.emplace(key, p);
     *out = &res.first->second;
     return WG_OK;
@@ -544,6 +608,10 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
              (i + 1 < nseg ? t.s[i + 1].blk_begin : blk) - t.s[i].blk_begin);
     p.text += buf;
   }
+  if (int rc2 = upload_segs(p)) {
+    p.release();
+    return rc2;
+  }
   auto res = L->plans.emplace(key, p);
   *out = &res.first->second;
   return WG_OK;
@@ -553,7 +621,8 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only) {
   if (L->n_rows == 0) return WG_OK;
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H});
-  const int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
+  int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
+  if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
   const bool fuse_h = (H != nullptr) && F <= max_tile;
   for (int64_t f0 = 0; f0 < F; f0 += max_tile) {
     const int64_t fw = std::min<int64_t>(max_tile, F - f0);
@@ -579,6 +648,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.chunks = plan->chunks;
     a.partial = plan->partial;
     a.seg_mask = L->tune.seg_mask;
+    a.nt = L->tune.nt;
     if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
     else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
     else rc = launch_step_vec<1>(*plan, a, stream);

@@ -179,3 +179,57 @@ def random_graph(n: int, p: float, seed: int = 0, directed: bool = True, weighte
             g = CSRGraph(n, A.indptr.astype(np.int64), A.indices.astype(np.int32),
                          A.data.astype(np.float32))
     return g
+
+
+def rmat_graph_device(n: int, target_nnz: int, seed: int = 0, device="cuda", max_rounds: int = 16):
+    """R-MAT graph generated on the GPU with torch ops (same recipe as
+    :func:`rmat_graph`: a=.57, b=c=.19, random vertex permutation, ids >= n
+    rejected, symmetrised, clamped to 1, no self loops, nnz within +0..5 %
+    of the target).  Deterministic for a given seed, so every rank of a
+    sharded run builds the identical graph.  Used for the Reddit / 8M R-MAT
+    sizes, where the numpy generator takes minutes.  Returns
+    (indptr int64, indices int32) device tensors.
+    (Not bit-identical to the numpy generator: a different random stream.)"""
+    import torch
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    scale = max(1, math.ceil(math.log2(max(n, 2))))
+    perm = torch.randperm(1 << scale, generator=gen, device=device)
+    a, b, c = 0.57, 0.19, 0.19
+    ab = a + b
+    c_norm = c / (1.0 - ab)
+    a_norm = a / ab
+    keys = torch.zeros(0, dtype=torch.int64, device=device)
+    m = max(16, int(target_nnz // 2 * 1.05))
+    for _ in range(max_rounds):
+        src = torch.zeros(m, dtype=torch.int64, device=device)
+        dst = torch.zeros(m, dtype=torch.int64, device=device)
+        for lvl in range(scale):
+            r1 = torch.rand(m, generator=gen, device=device)
+            r2 = torch.rand(m, generator=gen, device=device)
+            sb = r1 > ab
+            db = torch.where(sb, r2 > c_norm, r2 > a_norm)
+            src |= sb.to(torch.int64) << lvl
+            dst |= db.to(torch.int64) << lvl
+        src, dst = perm[src], perm[dst]
+        ok = (src < n) & (dst < n) & (src != dst)
+        src, dst = src[ok], dst[ok]
+        keys = torch.unique(torch.cat([keys, src * n + dst, dst * n + src]))
+        del src, dst, ok
+        if keys.numel() >= target_nnz:
+            break
+        m = max(16, int((target_nnz - keys.numel()) / 2 * 1.3) + 16)
+    if keys.numel() > int(target_nnz * 1.05):
+        rows, cols = keys // n, keys % n
+        upper = keys[rows < cols]
+        n_pairs = int(math.ceil(target_nnz * 1.02 / 2))
+        sel = torch.randperm(upper.numel(), generator=gen, device=device)[:n_pairs]
+        up = upper[sel]
+        r, cc = up // n, up % n
+        keys = torch.unique(torch.cat([r * n + cc, cc * n + r]))
+    rows = keys // n
+    cols = (keys % n).to(torch.int32)
+    counts = torch.bincount(rows, minlength=n)
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    indptr[1:] = torch.cumsum(counts, 0)
+    return indptr, cols

@@ -22,6 +22,14 @@ if [ -n "${SWEEP:-}" ]; then
   timeout -k 10 600 python tools/sweep.py $SWEEP > "$OUT/sweep.log" 2>&1
   stop_if_fatal $? sweep
 fi
+if [ -n "${SWEEP2:-}" ]; then
+  timeout -k 10 600 python tools/sweep.py $SWEEP2 > "$OUT/sweep2.log" 2>&1
+  stop_if_fatal $? sweep2
+fi
+if [ -n "${SWEEP3:-}" ]; then
+  timeout -k 10 600 python tools/sweep.py $SWEEP3 > "$OUT/sweep3.log" 2>&1
+  stop_if_fatal $? sweep3
+fi
 timeout -k 10 400 python bench.py --steps ${STEPS:-20} --warmup 3 --out "$OUT/bench.json" > "$OUT/bench.log" 2>&1
 stop_if_fatal $? bench
 if [ "${RUN_PROF:-1}" = 1 ]; then

@@ -44,32 +44,38 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="ogbn-arxiv")
     ap.add_argument("--F", type=int, default=None)
-    ap.add_argument("--K", type=int, default=16)
-    ap.add_argument("--iters", default="4,8,16")
-    ap.add_argument("--chunk-iters", default="8,16,32")
+    ap.add_argument("--K", type=int, default=None)
+    ap.add_argument("--grid", default="iter=24;chunk_iter=128",
+                    help="knob grid, e.g. 'iter=16,24;chunk_iter=64,128;nt=0,7'")
     ap.add_argument("--segments", action="store_true")
     a = ap.parse_args()
+    import itertools
     n, nnz, K, F = NAMED_CONFIGS[a.config]
     F = a.F or F
+    K = a.K or K
     g = named_graph(a.config)
     L = wats_hip.NormalizedLaplacian.from_graph(g)
     X = torch.randn(g.n, F, device="cuda") if F > 1 else L.log1p_degree()
-    bstep = 8 * L.nnz + 4 * (L.n + 1) + 20 * L.n * F
-    for it in [int(x) for x in a.iters.split(",")]:
-        for ci in [int(x) for x in a.chunk_iters.split(",")]:
-            L.tune(iter=it, chunk_iter=ci, seg_mask=-1)
-            r = time_chain(L, X, a.K)
-            r.update(config=a.config, F=F, iter=it, chunk_iter=ci, GBs=bstep / (r["step_us"] * 1e-6) / 1e9)
-            print(json.dumps(r), flush=True)
+    n_act = L.n - int(L.info["n_closed_form"])
+    bstep = 8 * L.nnz + 4 * (n_act + 1) + 20 * n_act * F
+    grid = [(kv.split("=")[0], [int(v) for v in kv.split("=")[1].split(",")]) for kv in a.grid.split(";") if kv]
+    names = [k for k, _ in grid]
+    first = None
+    for combo in itertools.product(*[v for _, v in grid]):
+        knobs = dict(zip(names, combo))
+        first = first or knobs
+        L.tune(seg_mask=-1, **knobs)
+        r = time_chain(L, X, K)
+        r.update(config=a.config, F=F, K=K, GBs=bstep / (r["step_us"] * 1e-6) / 1e9, **knobs)
+        print(json.dumps(r), flush=True)
     if a.segments:
-        it, ci = [int(x) for x in a.iters.split(",")][0], [int(x) for x in a.chunk_iters.split(",")][0]
-        L.tune(iter=it, chunk_iter=ci)
+        L.tune(**first)
         plan = L.describe(F)
         print(plan, flush=True)
         nseg = int(plan.split("segments=")[1].split()[0])
         for i in range(nseg):
             L.tune(seg_mask=1 << i)
-            r = time_chain(L, X, a.K)
+            r = time_chain(L, X, K)
             r.update(segment=i)
             print(json.dumps(r), flush=True)
         L.tune(seg_mask=-1)
