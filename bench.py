@@ -16,8 +16,9 @@ value = total edges*K processed by all ranks / max-over-ranks wall time, where
 edges = nnz of the off-diagonal L_hat (= symmetrised adjacency without loops).
 Multi-GPU (torchrun, one process per GPU): each rank runs its own
 independently generated graph of the same size -- weak scaling over
-independent graphs, no data-path collective (the row-sharded single-graph
-path with RCCL halo exchange is `--mode sharded`).
+independent graphs, no data-path collective.  `--mode sharded` instead splits
+ONE graph (e.g. --config reddit / rmat-8m) into row blocks over the ranks with a
+per-step RCCL halo exchange (strong scaling), see DESIGN.md section 7.
 
 Also printed in the same JSON line:
   roofline      -- the step kernel's algorithmic bytes (SURVEY.md 8(d):
@@ -60,6 +61,9 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--mode", default="graphs", choices=["graphs", "sharded"],
+                    help="graphs: one independent graph per rank (default); sharded: one graph row-sharded over all "
+                         "ranks with a per-step RCCL halo exchange")
     return ap.parse_args()
 
 
@@ -89,6 +93,92 @@ def cpu_baseline(g, K, F, s, X, seconds):
                        f"matvecs, {t_total:.1f} s")
 
 
+def sharded_main(args, world, rank, device):
+    """One graph (generated identically on every rank, on the GPU) split into
+    nnz-balanced row blocks; per Chebyshev step one all_to_all_single halo
+    exchange (RCCL) + the step kernel.  Strong scaling (fixed graph)."""
+    import wats_hip
+    from wats_hip.dist import ShardedWavelet, partition_rows
+    from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
+
+    n_t, nnz_t, K_def, F_def = NAMED_CONFIGS[args.config]
+    K = args.K if args.K is not None else K_def
+    F = args.F if args.F is not None else F_def
+    indptr_d, indices_d = rmat_graph_device(n_t, nnz_t, seed=args.seed, device=device)
+    indptr = indptr_d.cpu().numpy()
+    bounds = partition_rows(indptr, world)
+    r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+    lo, hi = int(indptr[r0]), int(indptr[r1])
+    cols = indices_d[lo:hi].cpu().numpy()
+    nnz_global = int(indptr[-1])
+    del indptr_d, indices_d
+    torch.cuda.empty_cache()
+    sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange="nccl", device=device)
+    if F == 1:
+        X = sw.L.log1p_degree()
+    else:
+        g = torch.Generator(device=device)
+        g.manual_seed(1 + rank)
+        X = torch.randn(r1 - r0, F, generator=g, device=device)
+    for _ in range(args.warmup):
+        sw.wavelet_features(X, k=K, s=args.s)
+    torch.cuda.synchronize(device)
+    sw.profile = True
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sw.wavelet_features(X, k=K, s=args.s)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = sw.profile_collect()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    nnz_lhat = torch.tensor([float(sw.L.nnz)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(nnz_lhat)
+    nnz_lhat = float(nnz_lhat.item())
+    if rank == 0:
+        p = sw.plan
+        n_loc = p.n_own
+        b_step = algorithmic_bytes(n_loc, sw.L.nnz, F)
+        avg_ms = prof["step_ms"]
+        line = {
+            "metric": f"Chebyshev SpMM-chain edges*K/s ({args.config}-size, K={K}, row-sharded)",
+            "value": nnz_lhat * K * args.steps / elapsed,
+            "unit": "edges*K/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{args.config}-size R-MAT (GPU generator, seed {args.seed}), one graph row-sharded "
+                                   f"over {world} ranks, halo all_to_all per step; K={K} F={F}",
+                       "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
+                       "rank0_rows": n_loc, "rank0_halo_rows": p.n_halo, "parallelism": f"rows x{world}"},
+            "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None,
+                         "traffic": None, "kernel": "cheb_step_kernel (rank 0 shard)",
+                         "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
+                         "avg_exchange_us": prof["exchange_ms"] * 1e3},
+        }
+        js = json.dumps(line)
+        print(js, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(js + "\n")
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,6 +189,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank if world > 1 else 0)
     torch.cuda.set_device(device)
+    if args.mode == "sharded":
+        sharded_main(args, world, rank, device)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     import wats_hip
     from wats_hip.graphgen import NAMED_CONFIGS, named_graph

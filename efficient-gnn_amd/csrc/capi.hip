@@ -75,6 +75,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "chunk_iter")) {
     if (value < 1) return fail(WG_ERR_INVALID, "chunk_iter must be >= 1");
     L->tune.chunk_iter = (int32_t)value;
+  } else if (!strcmp(key, "block_iter")) {
+    if (value < 1) return fail(WG_ERR_INVALID, "block_iter must be >= 1");
+    L->tune.block_iter = (int32_t)value;
   } else if (!strcmp(key, "nt")) {
     L->tune.nt = (int32_t)value;
     return WG_OK;

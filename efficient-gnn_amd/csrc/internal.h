@@ -78,8 +78,9 @@ struct Plan {
 
 struct Tuning {
   int32_t iter = 24;         // team mode: target nonzeros per lane sub-group
-  int32_t chunk_iter = 128;  // block/split mode: nonzeros per sub-group per workgroup
-  int32_t nt = 0;            // non-temporal hints: 1 = CSR col/val loads, 2 = own-row loads, 4 = stores
+  int32_t block_iter = 32;   // block mode: rows up to 4G*block_iter nonzeros get one workgroup
+  int32_t chunk_iter = 32;   // split mode: 4G*chunk_iter nonzeros per workgroup chunk
+  int32_t nt = 4;            // non-temporal hints: 4 = T_k / S stores (keeps L2 for the gathers)
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments
 };

@@ -68,19 +68,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int VEC>
-__device__ __forceinline__ void load_vec_nt(const float* p, float (&x)[VEC]) {
-  if constexpr (VEC == 1) {
-    x[0] = __builtin_nontemporal_load(p);
-  } else if constexpr (VEC == 2) {
-    const f32x2 v = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(p));
-    x[0] = v.x; x[1] = v.y;
-  } else {
-    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-  }
-}
-
-template <int VEC>
 __device__ __forceinline__ void store_vec_nt(float* p, const double (&x)[VEC]) {
   if constexpr (VEC == 1) {
     __builtin_nontemporal_store((float)x[0], p);
@@ -104,46 +91,54 @@ __device__ __forceinline__ void store_vec(float* p, const double (&x)[VEC]) {
   }
 }
 
+// Per-row epilogue operands, loaded BEFORE the row's gathers so their latency
+// overlaps the accumulation (they do not depend on it).
+template <int VEC>
+struct EpiIn {
+  float prev[VEC];  // k == 1: T_0 own row (for S); k >= 2: T_{k-2} own row
+  float sold[VEC];  // S own row (k >= 2)
+  int iso;
+};
+
+template <int VEC>
+__device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int fs, EpiIn<VEC>& in) {
+  const int64_t off = row * a.ld + (int64_t)fs * VEC;
+  in.iso = a.iso[row];
+  load_vec<VEC>((a.k == 1 ? a.xm1 : a.xm2) + off, in.prev);
+  if (a.S && a.k >= 2) load_vec<VEC>(a.S + off, in.sold);
+}
+
 // Per-row epilogue, run by the LF lanes holding the row's sums (`lane0` = wave
-// lane of the row's first column slice, for the H shuffle).
+// lane of the row's first column slice, for the H shuffle): diagonal of
+// isolated rows, recurrence, T_k store, heat sum, optional normalisation.
 template <int VEC>
 __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, int fs, double (&acc)[VEC],
-                                              int lane0) {
+                                              const EpiIn<VEC>& in, int lane0) {
   const int64_t off = row * a.ld + (int64_t)fs * VEC;
-  float x[VEC];
-  const bool nt_ld = (a.nt & 2) != 0;
   const bool nt_st = (a.nt & 4) != 0;
-  if (a.iso[row]) {  // L_hat_ii = -1 (scipy setdiag(1 - iso), then "- identity")
-    load_vec<VEC>(a.xm1 + off, x);
+  if (in.iso) {  // L_hat_ii = -1 (scipy setdiag(1 - iso), then "- identity")
+    float x[VEC];
+    if (a.k == 1) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) x[j] = in.prev[j];
+    } else {
+      load_vec<VEC>(a.xm1 + off, x);
+    }
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] -= (double)x[j];
   }
   double t[VEC];
-  if (a.k == 1) {
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) t[j] = acc[j];
-  } else {
-    if (nt_ld) load_vec_nt<VEC>(a.xm2 + off, x);
-    else load_vec<VEC>(a.xm2 + off, x);
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) t[j] = 2.0 * acc[j] - (double)x[j];
-  }
+  for (int j = 0; j < VEC; ++j) t[j] = (a.k == 1) ? acc[j] : 2.0 * acc[j] - (double)in.prev[j];
   if (a.xk) {
     if (nt_st) store_vec_nt<VEC>(a.xk + off, t);
     else store_vec<VEC>(a.xk + off, t);
   }
   if (a.S) {
     double s[VEC];
-    if (a.k == 1) {  // S = alpha0*T_0 + alpha1*T_1, T_0 = own row of xm1
-      load_vec<VEC>(a.xm1 + off, x);
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) s[j] = a.alpha0 * (double)x[j] + a.alpha_k * t[j];
-    } else {
-      if (nt_ld) load_vec_nt<VEC>(a.S + off, x);
-      else load_vec<VEC>(a.S + off, x);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) s[j] = (double)x[j] + a.alpha_k * t[j];
-    }
+    for (int j = 0; j < VEC; ++j)  // k == 1: S = alpha0*T_0 + alpha1*T_1
+      s[j] = (a.k == 1) ? a.alpha0 * (double)in.prev[j] + a.alpha_k * t[j] : (double)in.sold[j] + a.alpha_k * t[j];
     if (nt_st) store_vec_nt<VEC>(a.S + off, s);
     else store_vec<VEC>(a.S + off, s);
     if (a.H) {
@@ -161,16 +156,10 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
   }
 }
 
-template <bool NT, typename T>
-__device__ __forceinline__ T ldg(const T* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-
 // acc += sum over e = e, e+stride, ... < e1 of val[e] * x[col[e]] (float64).
-template <int VEC, bool NT = false>
-__device__ __forceinline__ void accumulate_t(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
-                                             const float* __restrict__ xb, double (&acc)[VEC]) {
+template <int VEC>
+__device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                           const float* __restrict__ xb, double (&acc)[VEC]) {
   const int32_t* __restrict__ col = a.col;
   const float* __restrict__ val = a.val;
   const int64_t ld = a.ld;
@@ -179,8 +168,8 @@ __device__ __forceinline__ void accumulate_t(const StepArgs& a, int32_t e, int32
     float v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      c[u] = ldg<NT>(col + e + u * stride);
-      v[u] = ldg<NT>(val + e + u * stride);
+      c[u] = col[e + u * stride];
+      v[u] = val[e + u * stride];
     }
     float x[4][VEC];
 #pragma unroll
@@ -191,20 +180,13 @@ __device__ __forceinline__ void accumulate_t(const StepArgs& a, int32_t e, int32
       for (int j = 0; j < VEC; ++j) acc[j] = fma((double)v[u], (double)x[u][j], acc[j]);
   }
   for (; e < e1; e += stride) {
-    const int32_t c = ldg<NT>(col + e);
-    const float v = ldg<NT>(val + e);
+    const int32_t c = col[e];
+    const float v = val[e];
     float x[VEC];
     load_vec<VEC>(xb + (int64_t)c * ld, x);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] = fma((double)v, (double)x[j], acc[j]);
   }
-}
-
-template <int VEC>
-__device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
-                                           const float* __restrict__ xb, double (&acc)[VEC]) {
-  if (a.nt & 1) accumulate_t<VEC, true>(a, e, e1, stride, xb, acc);
-  else accumulate_t<VEC, false>(a, e, e1, stride, xb, acc);
 }
 
 // Sum the partial sums of n lane sub-groups (lanes base + q*LF + fs, q < n)
@@ -257,12 +239,14 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
     const int fs = tl - ns * LF;
     const int64_t row = (int64_t)seg.begin + (int64_t)(blockIdx.x - seg.blk_begin) * (4 * tpw) + wave * tpw + team;
     const bool active = team < tpw && row < seg.end;
+    EpiIn<VEC> in;
     if (active) {
+      if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
       const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
       accumulate<VEC>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc);
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
-    if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, team * TS);
+    if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
     return;
   }
 
@@ -285,6 +269,8 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
   const int G = 64 / LF;
   const int sg = lane / LF;
   const int fs = lane - sg * LF;
+  EpiIn<VEC> in;
+  if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
   if (sg < G) accumulate<VEC>(a, e0 + wave * G + sg, e1, 4 * G, a.xm1 + fs * VEC, acc);
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
@@ -299,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
       acc[j] = ((red[(0 * LF + t) * VEC + j] + red[(1 * LF + t) * VEC + j]) + red[(2 * LF + t) * VEC + j]) +
                red[(3 * LF + t) * VEC + j];
     if (seg.mode == 1) {
-      step_epilogue<VEC>(a, row, t, acc, 0);
+      step_epilogue<VEC>(a, row, t, acc, in, 0);
     } else {
       double* p = a.partial + (int64_t)cid * (LF * VEC) + t * VEC;
 #pragma unroll
@@ -321,6 +307,8 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
   if (sg >= G || row >= n_split) return;
   const int2 rc = rowchunks[row];
   const int width = LF * VEC;
+  EpiIn<VEC> in;
+  epi_prefetch<VEC>(a, row, fs, in);
   double acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
@@ -329,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] += p[j];
   }
-  step_epilogue<VEC>(a, row, fs, acc, sg * LF);
+  step_epilogue<VEC>(a, row, fs, acc, in, sg * LF);
 }
 
 // internal S -> caller-order S and H = S / (||S||_1 + 1e-8); team of LF lanes per row.
@@ -496,9 +484,9 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 }
 
 // Build (once per tile shape) the segment table and the split-row chunk table.
-//   team  rows: len <= G*iter            (LN sub-groups per row, LN | G)
-//   block rows: len <= CH = 4G*chunk_iter (one workgroup per row)
-//   split rows: longer                   (one workgroup per CH-nnz chunk + combine_kernel)
+//   team  rows: len <= G*iter              (LN sub-groups per row, LN | G)
+//   block rows: len <= 4G*block_iter       (one workgroup per row)
+//   split rows: longer                     (one workgroup per CH = 4G*chunk_iter nnz + combine_kernel)
 // Classification is by power-of-two length bucket (rows are sorted by length).
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   active_only = active_only && L->reordered;
@@ -517,6 +505,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
   const int iter = std::max(1, L->tune.iter);
   const int64_t team_max = (int64_t)G * iter;
+  const int64_t block_max = (int64_t)4 * G * std::max(1, L->tune.block_iter);
   const int64_t CH = (int64_t)4 * G * std::max(1, L->tune.chunk_iter);
   SegTable& t = p.tab;
   char buf[256];
@@ -537,7 +526,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   int64_t n_split = 0, n_block = 0;
   for (int b = kBuckets - 1; b >= 0; --b) {
     const int64_t maxlen = (b == 0) ? 1 : (1ll << b);
-    if (maxlen > CH) n_split += bucket[b];
+    if (maxlen > block_max) n_split += bucket[b];
     else if (maxlen > team_max) n_block += bucket[b];
   }
   int nseg = 0;

@@ -49,4 +49,8 @@ if [ "${RUN_PMC:-0}" = 1 ]; then
       --out "$OUT/bench_traffic.json" > "$OUT/bench_traffic.log" 2>&1
   stop_if_fatal $? bench_traffic
 fi
+if [ -n "${EXTRA:-}" ]; then
+  timeout -k 10 900 bash -c "$EXTRA" > "$OUT/extra.log" 2>&1
+  stop_if_fatal $? extra
+fi
 echo done
