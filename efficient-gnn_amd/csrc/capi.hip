@@ -81,6 +81,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "nt")) {
     L->tune.nt = (int32_t)value;
     return WG_OK;
+  } else if (!strcmp(key, "pipe")) {
+    L->tune.pipe = value ? 1 : 0;
+    return WG_OK;
   } else if (!strcmp(key, "tile_f")) {
     L->tune.tile_f = (int32_t)std::max<int64_t>(0, value);
   } else if (!strcmp(key, "seg_mask")) {

@@ -82,6 +82,7 @@ struct Tuning {
   int32_t chunk_iter = 32;   // split mode: 4G*chunk_iter nonzeros per workgroup chunk
   int32_t nt = 4;            // non-temporal hints: 4 = T_k / S stores (keeps L2 for the gathers)
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
+  int32_t pipe = 0;          // 1 = software-pipelined index loads in the gather loop
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments
 };
 

@@ -49,6 +49,7 @@ struct StepArgs {
   double* partial;
   int64_t seg_mask;
   int32_t nt;
+  int32_t pipe;
 };
 
 template <int VEC>
@@ -157,6 +158,54 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
 }
 
 // acc += sum over e = e, e+stride, ... < e1 of val[e] * x[col[e]] (float64).
+// Software-pipelined variant: the next batch's (col, val) loads are issued
+// while the current batch's gathers are in flight, so each batch costs one
+// dependent round trip instead of two.  Out-of-range slots gather row 0 and
+// are masked out (never multiplied in).
+template <int VEC>
+__device__ __forceinline__ void accumulate_pipe(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                                const float* __restrict__ xb, double (&acc)[VEC]) {
+  const int32_t* __restrict__ col = a.col;
+  const float* __restrict__ val = a.val;
+  const int64_t ld = a.ld;
+  if (e >= e1) return;
+  int32_t c[4];
+  float v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int32_t idx = e + u * stride;
+    const bool ok = idx < e1;
+    c[u] = ok ? col[idx] : 0;
+    v[u] = ok ? val[idx] : 0.0f;
+  }
+  for (; e < e1; e += 4 * stride) {
+    float x[4][VEC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load_vec<VEC>(xb + (int64_t)c[u] * ld, x[u]);
+    int32_t cn[4];
+    float vn[4];
+    const int32_t en = e + 4 * stride;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int32_t idx = en + u * stride;
+      const bool ok = idx < e1;
+      cn[u] = ok ? col[idx] : 0;
+      vn[u] = ok ? val[idx] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = e + u * stride < e1;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] = ok ? fma((double)v[u], (double)x[u][j], acc[j]) : acc[j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = cn[u];
+      v[u] = vn[u];
+    }
+  }
+}
+
 template <int VEC>
 __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
                                            const float* __restrict__ xb, double (&acc)[VEC]) {
@@ -213,7 +262,14 @@ __device__ __forceinline__ void reduce_subgroups(double (&acc)[VEC], int n, int 
   }
 }
 
-template <int VEC>
+template <int VEC, bool PIPE>
+__device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                          const float* __restrict__ xb, double (&acc)[VEC]) {
+  if constexpr (PIPE) accumulate_pipe<VEC>(a, e, e1, stride, xb, acc);
+  else accumulate<VEC>(a, e, e1, stride, xb, acc);
+}
+
+template <int VEC, bool PIPE>
 __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
   __shared__ double red[4 * 64 * VEC];
   int si = 0;
@@ -243,7 +299,7 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
     if (active) {
       if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
       const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
-      accumulate<VEC>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc);
+      acc_range<VEC, PIPE>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc);
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
     if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
@@ -271,7 +327,7 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
   if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
-  if (sg < G) accumulate<VEC>(a, e0 + wave * G + sg, e1, 4 * G, a.xm1 + fs * VEC, acc);
+  if (sg < G) acc_range<VEC, PIPE>(a, e0 + wave * G + sg, e1, 4 * G, a.xm1 + fs * VEC, acc);
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
 #pragma unroll
@@ -437,8 +493,12 @@ template <int VEC>
 int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const SegTable& tab = plan.tab;
   if (tab.total_blocks > 0) {
-    hipLaunchKernelGGL(cheb_step_kernel<VEC>, dim3(tab.total_blocks), dim3(kBlock), 0, stream, a,
-                       (const Seg*)plan.d_segs, tab.n);
+    if (a.pipe)
+      hipLaunchKernelGGL((cheb_step_kernel<VEC, true>), dim3(tab.total_blocks), dim3(kBlock), 0, stream, a,
+                         (const Seg*)plan.d_segs, tab.n);
+    else
+      hipLaunchKernelGGL((cheb_step_kernel<VEC, false>), dim3(tab.total_blocks), dim3(kBlock), 0, stream, a,
+                         (const Seg*)plan.d_segs, tab.n);
     WG_LAUNCH_CHECK();
   }
   if (plan.n_split > 0 && ((a.seg_mask >> tab.n) & 1)) {
@@ -638,6 +698,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.partial = plan->partial;
     a.seg_mask = L->tune.seg_mask;
     a.nt = L->tune.nt;
+    a.pipe = L->tune.pipe;
     if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
     else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
     else rc = launch_step_vec<1>(*plan, a, stream);

@@ -69,6 +69,13 @@ class HaloPlan:
         return self.n_own + self.n_halo
 
 
+def _rank_world(group=None):
+    """(rank, world) of the group; an uninitialised default group is a single rank."""
+    if group is None and not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
 def _device_for(group) -> torch.device:
     backend = dist.get_backend(group)
     if backend == "nccl":
@@ -98,7 +105,7 @@ def exchange_int_lists(lists: list, group=None) -> list:
 def build_halo_plan(indptr_local: np.ndarray, indices_global: np.ndarray, bounds: np.ndarray, group=None) -> HaloPlan:
     """Renumber this rank's CSR columns to [own | halo] and agree with every
     peer on who sends which rows (collective)."""
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rank, world = _rank_world(group)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
     cols = np.asarray(indices_global, dtype=np.int64)
     own = (cols >= r0) & (cols < r1)
@@ -109,7 +116,7 @@ def build_halo_plan(indptr_local: np.ndarray, indices_global: np.ndarray, bounds
     local[~own] = n_own + np.searchsorted(halo_global, cols[~own])
     owner = np.searchsorted(bounds, halo_global, side="right") - 1
     recv_lists = [halo_global[owner == q] for q in range(world)]
-    requested = exchange_int_lists(recv_lists, group)      # what each peer needs from us
+    requested = exchange_int_lists(recv_lists, group) if world > 1 else recv_lists  # what each peer needs from us
     send_rows = np.concatenate(requested).astype(np.int64) - r0 if world else np.zeros(0, np.int64)
     assert np.all((send_rows >= 0) & (send_rows < max(n_own, 1))) or send_rows.size == 0
     plan = HaloPlan(rank=rank, world=world, bounds=np.asarray(bounds), r0=r0, r1=r1, n_halo=int(halo_global.size),
@@ -125,11 +132,13 @@ def global_column_degree(partial_colsum: torch.Tensor, partial_diag: torch.Tenso
                          group=None) -> torch.Tensor:
     """``w = colsum(A) - diag(A)`` for the columns [own | halo] of this rank:
     all-reduce the float64 partial sums, then scipy's float32 subtraction."""
-    dev = _device_for(group)
+    world = _rank_world(group)[1]
+    dev = _device_for(group) if world > 1 else partial_colsum.device
     cs = partial_colsum.to(dev, torch.float64)
     dg = partial_diag.to(dev, torch.float64)
-    dist.all_reduce(cs, group=group)
-    dist.all_reduce(dg, group=group)
+    if world > 1:
+        dist.all_reduce(cs, group=group)
+        dist.all_reduce(dg, group=group)
     ids = torch.from_numpy(np.concatenate([np.arange(plan.r0, plan.r1), plan.halo_global]).astype(np.int64)).to(dev)
     return cs[ids].to(torch.float32) - dg[ids].to(torch.float32)
 

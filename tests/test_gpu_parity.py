@@ -244,3 +244,24 @@ def test_wats_dropin_on_gpu_matches_reference():
     with torch.no_grad():
         out = _np(w(x, adj))
     np.testing.assert_allclose(out, d["out"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("knobs", [dict(pipe=1), dict(nt=0), dict(iter=2, block_iter=1, chunk_iter=1),
+                                   dict(iter=64, block_iter=256, chunk_iter=256), dict(tile_f=8),
+                                   dict(pipe=1, iter=4, block_iter=2, chunk_iter=2)])
+def test_tuning_knobs_preserve_results(knobs):
+    """Every plan shape / kernel variant the tuning knobs select computes the
+    same features (team, block and split rows, pipelined loads, F tiling)."""
+    g = named_graph("pubmed")
+    A = g.to_scipy()
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((g.n, 12)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=8, s=0.8, X0=X, return_all=True)
+    L = NormalizedLaplacian.from_graph(g)
+    H0, S0 = wats_hip.graph_wavelet_features(L, k=8, X0=torch.from_numpy(X), return_S=True)
+    L.tune(**knobs)
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=8, X0=torch.from_numpy(X), return_S=True)
+    assert_parity(_np(S1), ref["S"], what=f"{knobs} S")
+    assert_parity(_np(H1), ref["H"], what=f"{knobs} H")
+    if set(knobs) <= {"pipe", "nt"}:
+        assert torch.equal(S0, S1), "same plan must give bitwise-identical results"
