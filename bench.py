@@ -123,7 +123,7 @@ def sharded_main(args, world, rank, device):
     for _ in range(args.warmup):
         sw.wavelet_features(X, k=K, s=args.s)
     torch.cuda.synchronize(device)
-    sw.profile = True
+    sw.profile_start()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)

@@ -160,20 +160,8 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
     float* xk = (k == K) ? nullptr : ((k & 1) ? b1 : b0);  // T_K itself is never re-read
     const double ak = std::exp(-s * (double)k);             // WATS.py:65
-    hipEvent_t e_stop = nullptr;
-    if (L->prof) {
-      while (L->ev.size() < L->ev_used + 2) {
-        hipEvent_t e;
-        WG_HIP_TRY(hipEventCreate(&e));
-        L->ev.push_back(e);
-      }
-      WG_HIP_TRY(hipEventRecord(L->ev[L->ev_used], stream));
-      e_stop = L->ev[L->ev_used + 1];
-      L->ev_used += 2;
-    }
     rc = launch_step(L, k, F, xm1, xm2, xk, sint, nullptr, 1.0, ak, stream, /*active_only=*/true);
     if (rc) return rc;
-    if (e_stop) WG_HIP_TRY(hipEventRecord(e_stop, stream));
   }
   return launch_finalize(L, F, sint, b0, coef, S, H, stream);
 }

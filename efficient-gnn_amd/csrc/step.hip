@@ -666,9 +666,32 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   return WG_OK;
 }
 
+namespace {
+// Profiling: a pair of timing-only events around every step launch (both
+// kernels of a split step).  hipEventDisableSystemFence: no system-scope
+// release (cache write-back / invalidate) -- the events must not perturb the
+// kernels they time.
+int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start) {
+  if (!L->prof) return WG_OK;
+  if (start) {
+    while (L->ev.size() < L->ev_used + 2) {
+      hipEvent_t e;
+      WG_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+      L->ev.push_back(e);
+    }
+    WG_HIP_TRY(hipEventRecord(L->ev[L->ev_used], stream));
+  } else {
+    WG_HIP_TRY(hipEventRecord(L->ev[L->ev_used + 1], stream));
+    L->ev_used += 2;
+  }
+  return WG_OK;
+}
+}  // namespace
+
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only) {
   if (L->n_rows == 0) return WG_OK;
+  if (int rc = prof_mark(L, stream, true)) return rc;
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H});
   int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
   if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
@@ -708,7 +731,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(L->n_rows, 4)), dim3(kBlock), 0, stream, L->n_rows, F, S, H);
     WG_LAUNCH_CHECK();
   }
-  return WG_OK;
+  return prof_mark(L, stream, false);
 }
 
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef, float* S,

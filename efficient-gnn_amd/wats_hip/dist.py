@@ -225,14 +225,21 @@ class ShardedWavelet:
             self._bufs[key] = b
         return b[:rows]
 
+    def profile_start(self) -> None:
+        self.profile = True
+        self.L.profile_enable(True)
+
     def profile_collect(self) -> dict:
-        """Mean exchange / step-kernel time (ms) over the recorded steps; resets."""
+        """Mean halo-exchange and step-kernel time (ms) per Chebyshev step; resets."""
         torch.cuda.synchronize(self.device)
         ex = [e[0].elapsed_time(e[1]) for e in self.events]
-        st = [e[1].elapsed_time(e[2]) for e in self.events]
         self.events = []
-        n = max(1, len(st))
-        return dict(exchange_ms=sum(ex) / n, step_ms=sum(st) / n, max_step_ms=max(st or [0.0]), launches=len(st))
+        st = self.L.profile_collect()
+        self.L.profile_enable(False)
+        self.profile = False
+        n = max(1, st["launches"])
+        return dict(exchange_ms=sum(ex) / max(1, len(ex)), step_ms=st["sum_ms"] / n, max_step_ms=st["max_ms"],
+                    launches=st["launches"])
 
     # -------------------------------------------------------------- chain
     def wavelet_features(self, X0_local: torch.Tensor, k: int = 3, s: float = 0.8):
@@ -255,17 +262,15 @@ class ShardedWavelet:
         for i in range(1, k + 1):
             cur = bufs[(i - 1) % 2]
             nxt = bufs[i % 2]
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if self.profile else None
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if (self.profile and p.world > 1) else None
             if ev:
                 ev[0].record()
             self._halo_exchange(cur)
             if ev:
                 ev[1].record()
+                self.events.append(ev)
             L.step(i, cur, None if i == 1 else nxt[: p.n_own], None if i == k else nxt[: p.n_own], S=S,
                    alpha0=1.0, alpha_k=math.exp(-s * i))
-            if ev:
-                ev[2].record()
-                self.events.append(ev)
         from .wavelet import row_l1_normalize
         H_int = row_l1_normalize(S) if p.n_own else S.clone()
         S_out = L.permute(S, to_internal=False) if p.n_own else S.clone()

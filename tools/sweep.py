@@ -53,9 +53,15 @@ def main():
     n, nnz, K, F = NAMED_CONFIGS[a.config]
     F = a.F or F
     K = a.K or K
-    g = named_graph(a.config)
-    L = wats_hip.NormalizedLaplacian.from_graph(g)
-    X = torch.randn(g.n, F, device="cuda") if F > 1 else L.log1p_degree()
+    if nnz > 20_000_000:   # numpy generator too slow: same recipe on the GPU
+        from wats_hip.graphgen import rmat_graph_device
+        ip, ix = rmat_graph_device(n, nnz, seed=0)
+        L = wats_hip.NormalizedLaplacian(n, ip, ix)
+        del ip, ix
+    else:
+        g = named_graph(a.config)
+        L = wats_hip.NormalizedLaplacian.from_graph(g)
+    X = torch.randn(L.n, F, device="cuda") if F > 1 else L.log1p_degree()
     n_act = L.n - int(L.info["n_closed_form"])
     bstep = 8 * L.nnz + 4 * (n_act + 1) + 20 * n_act * F
     grid = [(kv.split("=")[0], [int(v) for v in kv.split("=")[1].split(",")]) for kv in a.grid.split(";") if kv]
