@@ -157,7 +157,6 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
   }
 }
 
-// acc += sum over e = e, e+stride, ... < e1 of val[e] * x[col[e]] (float64).
 // Software-pipelined variant: the next batch's (col, val) loads are issued
 // while the current batch's gathers are in flight, so each batch costs one
 // dependent round trip instead of two.  Out-of-range slots gather row 0 and
@@ -206,12 +205,24 @@ __device__ __forceinline__ void accumulate_pipe(const StepArgs& a, int32_t e, in
   }
 }
 
+// acc += sum over e = e, e+stride, ... < e1 of val[e] * x[col[e]].
+// Default: float64 FMAs (a float32 x float32 product is exact in float64).
+// -DWG_LANE_F32 (experimental build): each lane's short sequence (<= a few
+// dozen terms) in float32, added to the float64 accumulator at the end.
 template <int VEC>
 __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
                                            const float* __restrict__ xb, double (&acc)[VEC]) {
   const int32_t* __restrict__ col = a.col;
   const float* __restrict__ val = a.val;
   const int64_t ld = a.ld;
+#ifdef WG_LANE_F32
+  float part[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) part[j] = 0.0f;
+#define WG_FMA(j, vv, xx) part[j] = fmaf((vv), (xx), part[j])
+#else
+#define WG_FMA(j, vv, xx) acc[j] = fma((double)(vv), (double)(xx), acc[j])
+#endif
   for (; e + 3 * stride < e1; e += 4 * stride) {
     int32_t c[4];
     float v[4];
@@ -226,7 +237,7 @@ __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] = fma((double)v[u], (double)x[u][j], acc[j]);
+      for (int j = 0; j < VEC; ++j) WG_FMA(j, v[u], x[u][j]);
   }
   for (; e < e1; e += stride) {
     const int32_t c = col[e];
@@ -234,8 +245,13 @@ __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t
     float x[VEC];
     load_vec<VEC>(xb + (int64_t)c * ld, x);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] = fma((double)v, (double)x[j], acc[j]);
+    for (int j = 0; j < VEC; ++j) WG_FMA(j, v, x[j]);
   }
+#undef WG_FMA
+#ifdef WG_LANE_F32
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] += (double)part[j];
+#endif
 }
 
 // Sum the partial sums of n lane sub-groups (lanes base + q*LF + fs, q < n)

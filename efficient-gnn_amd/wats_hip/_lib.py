@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwats_hip.so")
+# WATS_HIP_LIB selects an experimental build (csrc/Makefile VARIANT=...) for A/B timing.
+LIB_PATH = os.environ.get("WATS_HIP_LIB") or os.path.join(_HERE, "libwats_hip.so")
 
 WG_FLAG_NONE = 0
 WG_FLAG_NO_REORDER = 1
