@@ -81,6 +81,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "nt")) {
     L->tune.nt = (int32_t)value;
     return WG_OK;
+  } else if (!strcmp(key, "waves")) {
+    if (value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "waves must be 4, 8 or 16");
+    L->tune.waves = (int32_t)value;
   } else if (!strcmp(key, "pipe")) {
     L->tune.pipe = value ? 1 : 0;
     return WG_OK;

@@ -68,6 +68,7 @@ struct Plan {
   Seg* d_segs = nullptr;        // device copy of tab.s (read with scalar loads)
   int32_t n_chunks = 0;
   int32_t width = 0;            // LF * VEC doubles per partial
+  int32_t nw = 4;               // waves per workgroup of the step kernel
   int32_t n_split = 0;          // split rows = internal rows [0, n_split)
   ChunkDesc* chunks = nullptr;  // device [n_chunks]
   double* partial = nullptr;    // device [n_chunks][width]
@@ -83,6 +84,7 @@ struct Tuning {
   int32_t nt = 4;            // non-temporal hints: 4 = T_k / S stores (keeps L2 for the gathers)
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
   int32_t pipe = 0;          // 1 = software-pipelined index loads in the gather loop
+  int32_t waves = 4;         // waves per step-kernel workgroup: 4, 8 or 16
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments
 };
 

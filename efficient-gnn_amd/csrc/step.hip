@@ -285,9 +285,9 @@ __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t 
   else accumulate<VEC>(a, e, e1, stride, xb, acc);
 }
 
-template <int VEC, bool PIPE>
-__global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
-  __shared__ double red[4 * 64 * VEC];
+template <int VEC, bool PIPE, int NW>
+__global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
+  __shared__ double red[NW * 64 * VEC];
   int si = 0;
   for (int i = 1; i < nseg; ++i)
     if ((int32_t)blockIdx.x >= segs[i].blk_begin) si = i;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
     const int tl = lane - team * TS;
     const int ns = tl / LF;
     const int fs = tl - ns * LF;
-    const int64_t row = (int64_t)seg.begin + (int64_t)(blockIdx.x - seg.blk_begin) * (4 * tpw) + wave * tpw + team;
+    const int64_t row = (int64_t)seg.begin + (int64_t)(blockIdx.x - seg.blk_begin) * (NW * tpw) + wave * tpw + team;
     const bool active = team < tpw && row < seg.end;
     EpiIn<VEC> in;
     if (active) {
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
   if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
-  if (sg < G) acc_range<VEC, PIPE>(a, e0 + wave * G + sg, e1, 4 * G, a.xm1 + fs * VEC, acc);
+  if (sg < G) acc_range<VEC, PIPE>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc);
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
 #pragma unroll
@@ -353,9 +353,12 @@ __global__ __launch_bounds__(kBlock) void cheb_step_kernel(StepArgs a, const Seg
   if (threadIdx.x < LF) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < VEC; ++j)
-      acc[j] = ((red[(0 * LF + t) * VEC + j] + red[(1 * LF + t) * VEC + j]) + red[(2 * LF + t) * VEC + j]) +
-               red[(3 * LF + t) * VEC + j];
+    for (int j = 0; j < VEC; ++j) acc[j] = red[t * VEC + j];
+#pragma unroll 1
+    for (int w = 1; w < NW; ++w) {  // fixed wave order
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += red[(w * LF + t) * VEC + j];
+    }
     if (seg.mode == 1) {
       step_epilogue<VEC>(a, row, t, acc, in, 0);
     } else {
@@ -505,16 +508,24 @@ int divisor_at_least(int G, int64_t want) {
   return G;
 }
 
+template <int VEC, int NW>
+void launch_main(const Plan& plan, const StepArgs& a, hipStream_t stream) {
+  const dim3 grid(plan.tab.total_blocks), block(NW * 64);
+  if (a.pipe)
+    hipLaunchKernelGGL((cheb_step_kernel<VEC, true, NW>), grid, block, 0, stream, a, (const Seg*)plan.d_segs,
+                       plan.tab.n);
+  else
+    hipLaunchKernelGGL((cheb_step_kernel<VEC, false, NW>), grid, block, 0, stream, a, (const Seg*)plan.d_segs,
+                       plan.tab.n);
+}
+
 template <int VEC>
 int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const SegTable& tab = plan.tab;
   if (tab.total_blocks > 0) {
-    if (a.pipe)
-      hipLaunchKernelGGL((cheb_step_kernel<VEC, true>), dim3(tab.total_blocks), dim3(kBlock), 0, stream, a,
-                         (const Seg*)plan.d_segs, tab.n);
-    else
-      hipLaunchKernelGGL((cheb_step_kernel<VEC, false>), dim3(tab.total_blocks), dim3(kBlock), 0, stream, a,
-                         (const Seg*)plan.d_segs, tab.n);
+    if (plan.nw == 16) launch_main<VEC, 16>(plan, a, stream);
+    else if (plan.nw == 8) launch_main<VEC, 8>(plan, a, stream);
+    else launch_main<VEC, 4>(plan, a, stream);
     WG_LAUNCH_CHECK();
   }
   if (plan.n_split > 0 && ((a.seg_mask >> tab.n) & 1)) {
@@ -566,7 +577,8 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // Classification is by power-of-two length bucket (rows are sorted by length).
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   active_only = active_only && L->reordered;
-  const int key = (LF * 8 + VEC) * 2 + (active_only ? 1 : 0);
+  const int NW = (L->tune.waves == 16 || L->tune.waves == 8) ? L->tune.waves : 4;
+  const int key = ((LF * 8 + VEC) * 2 + (active_only ? 1 : 0)) * 32 + NW;
   auto it = L->plans.find(key);
   if (it != L->plans.end()) {
     *out = &it->second;
@@ -574,6 +586,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   }
   Plan p;
   p.width = LF * VEC;
+  p.nw = NW;
   const int G = 64 / LF;
   const int64_t n = active_only ? L->n_active : L->n_rows;
   unsigned int bucket[kBuckets];
@@ -581,8 +594,8 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
   const int iter = std::max(1, L->tune.iter);
   const int64_t team_max = (int64_t)G * iter;
-  const int64_t block_max = (int64_t)4 * G * std::max(1, L->tune.block_iter);
-  const int64_t CH = (int64_t)4 * G * std::max(1, L->tune.chunk_iter);
+  const int64_t block_max = (int64_t)NW * G * std::max(1, L->tune.block_iter);
+  const int64_t CH = (int64_t)NW * G * std::max(1, L->tune.chunk_iter);
   SegTable& t = p.tab;
   char buf[256];
   if (!L->reordered) {
@@ -591,7 +604,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
     const int tpw = G / ln;
     t.s[0] = Seg{0, (int32_t)n, 0, ln, 0};
     t.n = n > 0 ? 1 : 0;
-    t.total_blocks = (int32_t)ceil_div(n, 4 * tpw);
+    t.total_blocks = (int32_t)ceil_div(n, NW * tpw);
     snprintf(buf, sizeof(buf), "team rows[0,%lld) ln=%d (no reorder)\n", (long long)n, ln);
     p.text = buf;
     if (int rc2 = upload_segs(p)) return rc2;
@@ -659,10 +672,10 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
     if (last && (last->ln == ln || nseg == kMaxSeg)) {
       if (last->ln != ln) ln = last->ln;  // out of slots: extend
       last->end = row + cnt;
-      blk = last->blk_begin + (int32_t)ceil_div(last->end - last->begin, 4 * (G / ln));
+      blk = last->blk_begin + (int32_t)ceil_div(last->end - last->begin, NW * (G / ln));
     } else {
       t.s[nseg++] = Seg{row, row + cnt, blk, ln, 0};
-      blk += (int32_t)ceil_div(cnt, 4 * (G / ln));
+      blk += (int32_t)ceil_div(cnt, NW * (G / ln));
     }
     row += cnt;
   }

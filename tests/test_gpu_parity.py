@@ -248,7 +248,8 @@ def test_wats_dropin_on_gpu_matches_reference():
 
 @pytest.mark.parametrize("knobs", [dict(pipe=1), dict(nt=0), dict(iter=2, block_iter=1, chunk_iter=1),
                                    dict(iter=64, block_iter=256, chunk_iter=256), dict(tile_f=8),
-                                   dict(pipe=1, iter=4, block_iter=2, chunk_iter=2)])
+                                   dict(pipe=1, iter=4, block_iter=2, chunk_iter=2),
+                                   dict(waves=16, block_iter=4, chunk_iter=2), dict(waves=8, iter=4, block_iter=8)])
 def test_tuning_knobs_preserve_results(knobs):
     """Every plan shape / kernel variant the tuning knobs select computes the
     same features (team, block and split rows, pipelined loads, F tiling)."""
