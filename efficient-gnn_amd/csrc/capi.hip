@@ -84,6 +84,8 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "waves")) {
     if (value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "waves must be 4, 8 or 16");
     L->tune.waves = (int32_t)value;
+  } else if (!strcmp(key, "hot")) {
+    L->tune.hot = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 40000));
   } else if (!strcmp(key, "pipe")) {
     L->tune.pipe = value ? 1 : 0;
     return WG_OK;

@@ -69,6 +69,7 @@ struct Plan {
   int32_t n_chunks = 0;
   int32_t width = 0;            // LF * VEC doubles per partial
   int32_t nw = 4;               // waves per workgroup of the step kernel
+  int32_t hot = 0;              // F == 1: columns [0, hot) of T_{k-1} staged in LDS (0 = off)
   int32_t n_split = 0;          // split rows = internal rows [0, n_split)
   ChunkDesc* chunks = nullptr;  // device [n_chunks]
   double* partial = nullptr;    // device [n_chunks][width]
@@ -85,6 +86,7 @@ struct Tuning {
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
   int32_t pipe = 0;          // 1 = software-pipelined index loads in the gather loop
   int32_t waves = 4;         // waves per step-kernel workgroup: 4, 8 or 16
+  int32_t hot = 0;           // F == 1: LDS hot-column cache size (columns), 0 = off
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments
 };
 

@@ -278,19 +278,72 @@ __device__ __forceinline__ void reduce_subgroups(double (&acc)[VEC], int n, int 
   }
 }
 
-template <int VEC, bool PIPE>
+// Dynamic LDS of cheb_step_hot_kernel: the hot-column cache.
+extern __shared__ float g_hot_lds[];
+
+// Two separate loads (LDS / global) behind a branch.  Written as a ternary,
+// clang merges them into one flat load of a selected generic pointer, which
+// both loses the LDS fast path and (ROCm 7.2) miscompiles the LDS-to-flat
+// cast ("V_CMP_NE_U32 src_shared_base" illegal instruction).
+__device__ __forceinline__ float hot_or_global(const float* hot, const float* __restrict__ xb, int32_t c, int32_t H,
+                                               int64_t ld) {
+  float x;
+  if (c < H) {
+    x = hot[c];
+    asm volatile("" ::: "memory");
+  } else {
+    x = xb[(int64_t)c * ld];
+    asm volatile("" ::: "memory");
+  }
+  return x;
+}
+
+// F == 1 with an LDS hot-column cache: columns [0, H) of T_{k-1} (the
+// highest-degree rows after relabelling, which receive most gathers) are read
+// from LDS, the rest from global memory.
+__device__ __forceinline__ void accumulate_hot1(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                                const float* __restrict__ xb, int32_t H, double (&acc)[1]) {
+  const float* hot = g_hot_lds;
+  const int32_t* __restrict__ col = a.col;
+  const float* __restrict__ val = a.val;
+  const int64_t ld = a.ld;
+  for (; e + 3 * stride < e1; e += 4 * stride) {
+    int32_t c[4];
+    float v[4], x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = col[e + u * stride];
+      v[u] = val[e + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = hot_or_global(hot, xb, c[u], H, ld);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[0] = fma((double)v[u], (double)x[u], acc[0]);
+  }
+  for (; e < e1; e += stride) {
+    const int32_t c = col[e];
+    const float x = hot_or_global(hot, xb, c, H, ld);
+    acc[0] = fma((double)val[e], (double)x, acc[0]);
+  }
+}
+
+template <int VEC, bool PIPE, bool HOT>
 __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
-                                          const float* __restrict__ xb, double (&acc)[VEC]) {
-  if constexpr (PIPE) accumulate_pipe<VEC>(a, e, e1, stride, xb, acc);
+                                          const float* __restrict__ xb, double (&acc)[VEC], int32_t H) {
+  if constexpr (HOT && VEC == 1) accumulate_hot1(a, e, e1, stride, xb, H, acc);
+  else if constexpr (PIPE) accumulate_pipe<VEC>(a, e, e1, stride, xb, acc);
   else accumulate<VEC>(a, e, e1, stride, xb, acc);
 }
 
-template <int VEC, bool PIPE, int NW>
-__global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
+// One work unit of the plan (a group of team rows, a block row or a split
+// chunk) processed by one workgroup of NW waves.
+template <int VEC, bool PIPE, int NW, bool HOT>
+__device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restrict__ segs, int nseg, int32_t unit,
+                                          int32_t H) {
   __shared__ double red[NW * 64 * VEC];
   int si = 0;
   for (int i = 1; i < nseg; ++i)
-    if ((int32_t)blockIdx.x >= segs[i].blk_begin) si = i;
+    if (unit >= segs[i].blk_begin) si = i;
   const Seg seg = segs[si];
   if (!((a.seg_mask >> si) & 1)) return;  // timing attribution only
   const int lane = threadIdx.x & 63;
@@ -309,13 +362,13 @@ __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Se
     const int tl = lane - team * TS;
     const int ns = tl / LF;
     const int fs = tl - ns * LF;
-    const int64_t row = (int64_t)seg.begin + (int64_t)(blockIdx.x - seg.blk_begin) * (NW * tpw) + wave * tpw + team;
+    const int64_t row = (int64_t)seg.begin + (int64_t)(unit - seg.blk_begin) * (NW * tpw) + wave * tpw + team;
     const bool active = team < tpw && row < seg.end;
     EpiIn<VEC> in;
     if (active) {
       if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
       const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
-      acc_range<VEC, PIPE>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc);
+      acc_range<VEC, PIPE, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H);
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
     if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
@@ -328,11 +381,11 @@ __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Se
   int64_t row;
   int32_t e0, e1, cid = 0;
   if (seg.mode == 1) {
-    row = (int64_t)seg.begin + (blockIdx.x - seg.blk_begin);
+    row = (int64_t)seg.begin + (unit - seg.blk_begin);
     e0 = a.rowptr[row];
     e1 = a.rowptr[row + 1];
   } else {
-    cid = seg.begin + (int32_t)(blockIdx.x - seg.blk_begin);
+    cid = seg.begin + (int32_t)(unit - seg.blk_begin);
     const ChunkDesc d = a.chunks[cid];
     row = d.row;
     e0 = d.e0;
@@ -343,7 +396,7 @@ __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Se
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
   if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
-  if (sg < G) acc_range<VEC, PIPE>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc);
+  if (sg < G) acc_range<VEC, PIPE, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H);
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
 #pragma unroll
@@ -366,6 +419,24 @@ __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Se
 #pragma unroll
       for (int j = 0; j < VEC; ++j) p[j] = acc[j];
     }
+  }
+}
+
+template <int VEC, bool PIPE, int NW>
+__global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
+  unit_body<VEC, PIPE, NW, false>(a, segs, nseg, (int32_t)blockIdx.x, 0);
+}
+
+// Persistent F == 1 variant: one workgroup per CU stages T_{k-1}[0, H) in LDS
+// once, then walks the plan's work units round-robin.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void cheb_step_hot_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg,
+                                                                int32_t total_units, int32_t H) {
+  for (int32_t i = threadIdx.x; i < H; i += NW * 64) g_hot_lds[i] = a.xm1[(int64_t)i * a.ld];
+  __syncthreads();
+  for (int32_t unit = blockIdx.x; unit < total_units; unit += gridDim.x) {
+    unit_body<1, false, NW, true>(a, segs, nseg, unit, H);
+    __syncthreads();  // the block-mode LDS partials are reused by the next unit
   }
 }
 
@@ -519,10 +590,35 @@ void launch_main(const Plan& plan, const StepArgs& a, hipStream_t stream) {
                        plan.tab.n);
 }
 
+template <int NW>
+int launch_hot(const Plan& plan, const StepArgs& a, hipStream_t stream) {
+  static int n_cu = 0;
+  static bool attr_set = false;
+  if (!n_cu) {
+    int dev = 0;
+    WG_HIP_TRY(hipGetDevice(&dev));
+    WG_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const size_t lds = (size_t)plan.hot * sizeof(float);
+  if (!attr_set) {
+    WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_step_hot_kernel<NW>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - NW * 64 * 8));
+    attr_set = true;
+  }
+  const int grid = std::min<int>(plan.tab.total_blocks, n_cu);
+  hipLaunchKernelGGL(cheb_step_hot_kernel<NW>, dim3(grid), dim3(NW * 64), lds, stream, a, (const Seg*)plan.d_segs,
+                     plan.tab.n, plan.tab.total_blocks, plan.hot);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
 template <int VEC>
 int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const SegTable& tab = plan.tab;
-  if (tab.total_blocks > 0) {
+  if (VEC == 1 && plan.hot > 0 && tab.total_blocks > 0) {
+    int rc = plan.nw == 16 ? launch_hot<16>(plan, a, stream) : launch_hot<4>(plan, a, stream);
+    if (rc) return rc;
+  } else if (tab.total_blocks > 0) {
     if (plan.nw == 16) launch_main<VEC, 16>(plan, a, stream);
     else if (plan.nw == 8) launch_main<VEC, 8>(plan, a, stream);
     else launch_main<VEC, 4>(plan, a, stream);
@@ -578,7 +674,7 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   active_only = active_only && L->reordered;
   const int NW = (L->tune.waves == 16 || L->tune.waves == 8) ? L->tune.waves : 4;
-  const int key = ((LF * 8 + VEC) * 2 + (active_only ? 1 : 0)) * 32 + NW;
+  const int key = ((LF * 8 + VEC) * 2 + (active_only ? 1 : 0)) * 32 + NW + (L->tune.hot > 0 ? (1 << 28) : 0);
   auto it = L->plans.find(key);
   if (it != L->plans.end()) {
     *out = &it->second;
@@ -587,6 +683,8 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   Plan p;
   p.width = LF * VEC;
   p.nw = NW;
+  if (LF == 1 && VEC == 1 && L->tune.hot > 0)
+    p.hot = (int32_t)std::min<int64_t>({(int64_t)L->tune.hot, L->n_cols, (int64_t)((160 * 1024 - NW * 64 * 8) / 4)});
   const int G = 64 / LF;
   const int64_t n = active_only ? L->n_active : L->n_rows;
   unsigned int bucket[kBuckets];

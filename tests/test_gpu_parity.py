@@ -251,12 +251,23 @@ def test_wats_dropin_on_gpu_matches_reference():
                                    dict(pipe=1, iter=4, block_iter=2, chunk_iter=2),
                                    dict(waves=16, block_iter=4, chunk_iter=2), dict(waves=8, iter=4, block_iter=8)])
 def test_tuning_knobs_preserve_results(knobs):
+    _check_knobs(knobs, F=12)
+
+
+@pytest.mark.parametrize("knobs", [dict(hot=4096), dict(hot=1000, waves=16), dict(hot=32768, waves=4, iter=2, block_iter=1,
+                                                                                  chunk_iter=1)])
+def test_hot_column_cache_f1(knobs):
+    """F == 1 persistent kernel with the LDS hot-column cache."""
+    _check_knobs(knobs, F=1)
+
+
+def _check_knobs(knobs, F):
     """Every plan shape / kernel variant the tuning knobs select computes the
     same features (team, block and split rows, pipelined loads, F tiling)."""
     g = named_graph("pubmed")
     A = g.to_scipy()
     rng = np.random.default_rng(3)
-    X = rng.standard_normal((g.n, 12)).astype(np.float32)
+    X = rng.standard_normal((g.n, F)).astype(np.float32)
     ref = O.graph_wavelet_features(A, k=8, s=0.8, X0=X, return_all=True)
     L = NormalizedLaplacian.from_graph(g)
     H0, S0 = wats_hip.graph_wavelet_features(L, k=8, X0=torch.from_numpy(X), return_S=True)
