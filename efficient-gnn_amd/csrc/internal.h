@@ -79,9 +79,10 @@ struct Plan {
 };
 
 struct Tuning {
-  int32_t iter = 24;         // team mode: target nonzeros per lane sub-group
-  int32_t block_iter = 32;   // block mode: rows up to 4G*block_iter nonzeros get one workgroup
-  int32_t chunk_iter = 32;   // split mode: 4G*chunk_iter nonzeros per workgroup chunk
+  // 0 = shape-dependent default (see default_knobs in step.hip)
+  int32_t iter = 0;          // team mode: target nonzeros per lane sub-group
+  int32_t block_iter = 0;    // block mode: rows up to NW*G*block_iter nonzeros get one workgroup
+  int32_t chunk_iter = 0;    // split mode: NW*G*chunk_iter nonzeros per workgroup chunk
   int32_t nt = 4;            // non-temporal hints: 4 = T_k / S stores (keeps L2 for the gathers)
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
   int32_t pipe = 0;          // 1 = software-pipelined index loads in the gather loop

@@ -666,6 +666,16 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
   return 1;
 }
 
+// Defaults measured on MI355X (profiles/r01 sweeps): wide signals (G = 64/LF
+// small, e.g. F = 40 -> G = 6) want long per-sub-group runs; F = 1 (G = 64)
+// shorter ones.
+void default_knobs(const Tuning& t, int G, int* iter, int* block_iter, int* chunk_iter) {
+  const bool wide = G <= 16;
+  *iter = t.iter > 0 ? t.iter : (wide ? 24 : 16);
+  *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 128 : 32);
+  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? 32 : 16);
+}
+
 // Build (once per tile shape) the segment table and the split-row chunk table.
 //   team  rows: len <= G*iter              (LN sub-groups per row, LN | G)
 //   block rows: len <= 4G*block_iter       (one workgroup per row)
@@ -690,10 +700,11 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   unsigned int bucket[kBuckets];
   for (int b = 0; b < kBuckets; ++b) bucket[b] = L->bucket[b];
   bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
-  const int iter = std::max(1, L->tune.iter);
+  int iter, block_iter, chunk_iter;
+  default_knobs(L->tune, G, &iter, &block_iter, &chunk_iter);
   const int64_t team_max = (int64_t)G * iter;
-  const int64_t block_max = (int64_t)NW * G * std::max(1, L->tune.block_iter);
-  const int64_t CH = (int64_t)NW * G * std::max(1, L->tune.chunk_iter);
+  const int64_t block_max = (int64_t)NW * G * block_iter;
+  const int64_t CH = (int64_t)NW * G * chunk_iter;
   SegTable& t = p.tab;
   char buf[256];
   if (!L->reordered) {

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${SESSION:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+rocprofv3 -L 2>&1 | grep -E "^[A-Za-z]" | cut -c1-120 > "$OUT/counters.txt" || true
 CONFIG=${CONFIG:-reddit}
 GRID=${GRID:-iter=16;block_iter=8;chunk_iter=16}
 i=0
@@ -16,10 +16,11 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_RE
            "TA_BUSY_avr TA_TA_BUSY_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$PWD/$OUT/pmc_${CONFIG}_$i" -o run -- \
-      python3 tools/sweep.py --config $CONFIG --grid "$GRID" > "$OUT/pmc_${CONFIG}_$i.log" 2>&1
+      python3 tools/sweep.py --config $CONFIG --grid "$GRID" --K 4 --reps 2 > "$OUT/pmc_${CONFIG}_$i.log" 2>&1
   rc=$?
   echo "[$grp] rc=$rc" | tee -a "$OUT/steps.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc $rc"; exit $rc; fi
+  python3 tools/pmc_traffic.py "$OUT/pmc_${CONFIG}_$i" --out "$OUT/pmc_${CONFIG}_$i.json" > /dev/null 2>&1 || true
+  rm -rf "$OUT/pmc_${CONFIG}_$i"
 done
-python3 tools/pmc_traffic.py "$OUT"/pmc_${CONFIG}_* --out "$OUT/pmc_${CONFIG}.json" > /dev/null 2>&1 || true
 echo done

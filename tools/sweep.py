@@ -18,7 +18,11 @@ import wats_hip  # noqa: E402
 from wats_hip.graphgen import NAMED_CONFIGS, named_graph  # noqa: E402
 
 
-def time_chain(L, X, K, reps=10):
+REPS = 10
+
+
+def time_chain(L, X, K, reps=None):
+    reps = reps or REPS
     n, F = X.shape
     S = torch.empty_like(X)
     H = torch.empty_like(X)
@@ -26,7 +30,7 @@ def time_chain(L, X, K, reps=10):
     st = torch.cuda.current_stream().cuda_stream
     run = lambda: wats_hip._lib.check(lib.wg_wavelet_features(L.handle, X.data_ptr(), F, K, 0.8, S.data_ptr(),
                                                                H.data_ptr(), st))
-    for _ in range(2):
+    for _ in range(1 if reps <= 2 else 2):
         run()
     torch.cuda.synchronize()
     L.profile_enable(True)
@@ -48,7 +52,10 @@ def main():
     ap.add_argument("--grid", default="iter=24;chunk_iter=128",
                     help="knob grid, e.g. 'iter=16,24;chunk_iter=64,128;nt=0,7'")
     ap.add_argument("--segments", action="store_true")
+    ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
+    global REPS
+    REPS = a.reps
     import itertools
     n, nnz, K, F = NAMED_CONFIGS[a.config]
     F = a.F or F
