@@ -184,11 +184,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank if world > 1 else 0)
+    # WATS_BENCH_DEVICE pins every rank to one device (multi-rank tests on a 1-GPU box)
+    dev_idx = int(os.environ.get("WATS_BENCH_DEVICE", local_rank if world > 1 else 0))
+    device = torch.device("cuda", dev_idx)
     torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
     if args.mode == "sharded":
         sharded_main(args, world, rank, device)
         if world > 1:
