@@ -49,7 +49,7 @@ struct StepArgs {
   double* partial;
   int64_t seg_mask;
   int32_t nt;
-  int32_t pipe;
+  int32_t bcast;
 };
 
 template <int VEC>
@@ -153,54 +153,6 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
 #pragma unroll
       for (int j = 0; j < VEC; ++j) h[j] = s[j] / den;
       store_vec<VEC>(a.H + off, h);
-    }
-  }
-}
-
-// Software-pipelined variant: the next batch's (col, val) loads are issued
-// while the current batch's gathers are in flight, so each batch costs one
-// dependent round trip instead of two.  Out-of-range slots gather row 0 and
-// are masked out (never multiplied in).
-template <int VEC>
-__device__ __forceinline__ void accumulate_pipe(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
-                                                const float* __restrict__ xb, double (&acc)[VEC]) {
-  const int32_t* __restrict__ col = a.col;
-  const float* __restrict__ val = a.val;
-  const int64_t ld = a.ld;
-  if (e >= e1) return;
-  int32_t c[4];
-  float v[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int32_t idx = e + u * stride;
-    const bool ok = idx < e1;
-    c[u] = ok ? col[idx] : 0;
-    v[u] = ok ? val[idx] : 0.0f;
-  }
-  for (; e < e1; e += 4 * stride) {
-    float x[4][VEC];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) load_vec<VEC>(xb + (int64_t)c[u] * ld, x[u]);
-    int32_t cn[4];
-    float vn[4];
-    const int32_t en = e + 4 * stride;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int32_t idx = en + u * stride;
-      const bool ok = idx < e1;
-      cn[u] = ok ? col[idx] : 0;
-      vn[u] = ok ? val[idx] : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const bool ok = e + u * stride < e1;
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] = ok ? fma((double)v[u], (double)x[u][j], acc[j]) : acc[j];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      c[u] = cn[u];
-      v[u] = vn[u];
     }
   }
 }
@@ -327,17 +279,71 @@ __device__ __forceinline__ void accumulate_hot1(const StepArgs& a, int32_t e, in
   }
 }
 
-template <int VEC, bool PIPE, bool HOT>
+// Sub-group cooperative index loads (LF > 1).  The LF lanes of a sub-group
+// walk the same nonzero sequence e, e+stride, ...; instead of every lane
+// issuing a dword load of the same col/val entry (10 identical addresses per
+// sub-group at F=40: the texture-address unit was ~70 % busy, PMC s11), lane
+// fs loads element t0+fs and the sub-group shares the LF (col, val) pairs
+// through ds_bpermute, which runs on the LDS pipe.  Same elements, same
+// order as accumulate() -> bitwise-identical sums.  U = gathers in flight.
+template <int VEC, int U>
+__device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                                 const float* __restrict__ xb, double (&acc)[VEC], int fs,
+                                                 int base) {
+  const int LF = a.LF;
+  const int64_t ld = a.ld;
+  if (e >= e1) return;
+  const int32_t n = (e1 - e + stride - 1) / stride;
+  for (int32_t t0 = 0; t0 < n; t0 += LF) {
+    const int32_t tt = t0 + fs;
+    int32_t myc = 0;
+    float myv = 0.0f;
+    if (tt < n) {
+      const int32_t idx = e + tt * stride;
+      myc = a.col[idx];
+      myv = a.val[idx];
+    }
+    const int cnt = min(LF, n - t0);
+    for (int j = 0; j < cnt; j += U) {
+      int32_t c[U];
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int src = base + min(j + u, LF - 1);  // stays inside the sub-group
+        c[u] = __shfl(myc, src, 64);
+        v[u] = __shfl(myv, src, 64);
+      }
+      float x[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_vec<VEC>(xb + (int64_t)c[u] * ld, x[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (j + u < cnt) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) acc[q] = fma((double)v[u], (double)x[u][q], acc[q]);
+        }
+      }
+    }
+  }
+}
+
+template <int VEC, bool BCAST, bool HOT>
 __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
-                                          const float* __restrict__ xb, double (&acc)[VEC], int32_t H) {
-  if constexpr (HOT && VEC == 1) accumulate_hot1(a, e, e1, stride, xb, H, acc);
-  else if constexpr (PIPE) accumulate_pipe<VEC>(a, e, e1, stride, xb, acc);
-  else accumulate<VEC>(a, e, e1, stride, xb, acc);
+                                          const float* __restrict__ xb, double (&acc)[VEC], int32_t H, int fs,
+                                          int base) {
+  if constexpr (HOT && VEC == 1) {
+    accumulate_hot1(a, e, e1, stride, xb, H, acc);
+  } else if constexpr (BCAST) {
+    if (a.LF % 5 == 0) accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
+    else accumulate_bcast<VEC, 4>(a, e, e1, stride, xb, acc, fs, base);
+  } else {
+    accumulate<VEC>(a, e, e1, stride, xb, acc);
+  }
 }
 
 // One work unit of the plan (a group of team rows, a block row or a split
 // chunk) processed by one workgroup of NW waves.
-template <int VEC, bool PIPE, int NW, bool HOT>
+template <int VEC, bool BCAST, int NW, bool HOT>
 __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restrict__ segs, int nseg, int32_t unit,
                                           int32_t H) {
   __shared__ double red[NW * 64 * VEC];
@@ -368,7 +374,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     if (active) {
       if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
       const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
-      acc_range<VEC, PIPE, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H);
+      acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
     if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
@@ -396,7 +402,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
   if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
-  if (sg < G) acc_range<VEC, PIPE, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H);
+  if (sg < G) acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
 #pragma unroll
@@ -422,9 +428,9 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
   }
 }
 
-template <int VEC, bool PIPE, int NW>
+template <int VEC, bool BCAST, int NW>
 __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
-  unit_body<VEC, PIPE, NW, false>(a, segs, nseg, (int32_t)blockIdx.x, 0);
+  unit_body<VEC, BCAST, NW, false>(a, segs, nseg, (int32_t)blockIdx.x, 0);
 }
 
 // Persistent F == 1 variant: one workgroup per CU stages T_{k-1}[0, H) in LDS
@@ -582,7 +588,7 @@ int divisor_at_least(int G, int64_t want) {
 template <int VEC, int NW>
 void launch_main(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const dim3 grid(plan.tab.total_blocks), block(NW * 64);
-  if (a.pipe)
+  if (a.bcast && a.LF > 1)
     hipLaunchKernelGGL((cheb_step_kernel<VEC, true, NW>), grid, block, 0, stream, a, (const Seg*)plan.d_segs,
                        plan.tab.n);
   else
@@ -859,7 +865,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.partial = plan->partial;
     a.seg_mask = L->tune.seg_mask;
     a.nt = L->tune.nt;
-    a.pipe = L->tune.pipe;
+    a.bcast = L->tune.bcast;
     if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
     else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
     else rc = launch_step_vec<1>(*plan, a, stream);

@@ -246,9 +246,9 @@ def test_wats_dropin_on_gpu_matches_reference():
     np.testing.assert_allclose(out, d["out"], rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("knobs", [dict(pipe=1), dict(nt=0), dict(iter=2, block_iter=1, chunk_iter=1),
+@pytest.mark.parametrize("knobs", [dict(bcast=0), dict(nt=0), dict(iter=2, block_iter=1, chunk_iter=1),
                                    dict(iter=64, block_iter=256, chunk_iter=256), dict(tile_f=8),
-                                   dict(pipe=1, iter=4, block_iter=2, chunk_iter=2),
+                                   dict(bcast=0, iter=4, block_iter=2, chunk_iter=2),
                                    dict(waves=16, block_iter=4, chunk_iter=2), dict(waves=8, iter=4, block_iter=8)])
 def test_tuning_knobs_preserve_results(knobs):
     _check_knobs(knobs, F=12)
@@ -275,5 +275,5 @@ def _check_knobs(knobs, F):
     H1, S1 = wats_hip.graph_wavelet_features(L, k=8, X0=torch.from_numpy(X), return_S=True)
     assert_parity(_np(S1), ref["S"], what=f"{knobs} S")
     assert_parity(_np(H1), ref["H"], what=f"{knobs} H")
-    if set(knobs) <= {"pipe", "nt"}:
+    if set(knobs) <= {"bcast", "nt"}:
         assert torch.equal(S0, S1), "same plan must give bitwise-identical results"
