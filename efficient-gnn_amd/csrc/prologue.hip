@@ -412,7 +412,10 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   WG_HIP_TRY(hipMemcpyAsync(&total, L->rowptr + n_rows, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
   WG_HIP_TRY(hipStreamSynchronize(stream));
   L->nnz = total;
-  if ((rc = dmalloc(&L->col, L->nnz)) || (rc = dmalloc(&L->val, L->nnz))) return rc;
+  // +4 padding: the F == 1 vectorised index loads read whole aligned 4-groups
+  if ((rc = dmalloc(&L->col, L->nnz + 4)) || (rc = dmalloc(&L->val, L->nnz + 4))) return rc;
+  WG_HIP_TRY(hipMemsetAsync(L->col + L->nnz, 0, 4 * sizeof(int32_t), stream));
+  WG_HIP_TRY(hipMemsetAsync(L->val + L->nnz, 0, 4 * sizeof(float), stream));
   hipLaunchKernelGGL(fill_lhat_kernel, dim3(ceil_div(n_rows, 4)), dim3(kBlock), 0, stream, n_rows, L->perm, L->iperm,
                      indptr, indices, values, sw, L->rowptr, L->col, L->val);
   WG_LAUNCH_CHECK();

@@ -50,6 +50,7 @@ struct StepArgs {
   int64_t seg_mask;
   int32_t nt;
   int32_t bcast;
+  int32_t vidx;
 };
 
 template <int VEC>
@@ -327,6 +328,34 @@ __device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, i
   }
 }
 
+// F == 1: each lane takes 4 consecutive nonzeros with one 16-B int4 / float4
+// load of col / val (4x fewer index instructions through the texture-address
+// unit).  Chunks are 4-aligned in the CSR (arrays padded by 4 entries), lane
+// ns of the row's team takes chunks ns, ns+stride, ...; elements outside
+// [e0, e1) are masked.  Different summation split than accumulate().
+__device__ __forceinline__ void accumulate_vidx1(const StepArgs& a, int32_t e0, int32_t e1, int32_t ns,
+                                                 int32_t stride, const float* __restrict__ xb, double (&acc)[1]) {
+  const int64_t ld = a.ld;
+  const int32_t eb = e0 & ~3;
+  for (int32_t q = eb + 4 * ns; q < e1; q += 4 * stride) {
+    const int4 c = *reinterpret_cast<const int4*>(a.col + q);
+    const float4 v = *reinterpret_cast<const float4*>(a.val + q);
+    const int32_t cc[4] = {c.x, c.y, c.z, c.w};
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = (q + u >= e0) && (q + u < e1);
+      x[u] = ok ? xb[(int64_t)cc[u] * ld] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = (q + u >= e0) && (q + u < e1);
+      if (ok) acc[0] = fma((double)vv[u], (double)x[u], acc[0]);
+    }
+  }
+}
+
 template <int VEC, bool BCAST, bool HOT>
 __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
                                           const float* __restrict__ xb, double (&acc)[VEC], int32_t H, int fs,
@@ -374,7 +403,12 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     if (active) {
       if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
       const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
-      acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+      if constexpr (VEC == 1 && !HOT) {
+        if (a.vidx && LF == 1) accumulate_vidx1(a, e0, e1, ns, LN, a.xm1, acc);
+        else acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+      } else {
+        acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+      }
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
     if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
@@ -402,7 +436,17 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
   if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
-  if (sg < G) acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+  if constexpr (VEC == 1 && !HOT) {
+    if (a.vidx && LF == 1) {
+      // chunk-aligned ranges: for split chunks e0 is a multiple of CH (>= 4) from the row start, so
+      // neighbouring chunks never both take an aligned 4-group (masking keeps the bounds exact anyway)
+      accumulate_vidx1(a, e0, e1, wave * G + sg, NW * G, a.xm1, acc);
+    } else if (sg < G) {
+      acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+    }
+  } else if (sg < G) {
+    acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+  }
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
 #pragma unroll
@@ -866,6 +910,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.seg_mask = L->tune.seg_mask;
     a.nt = L->tune.nt;
     a.bcast = L->tune.bcast;
+    a.vidx = L->tune.vidx;
     if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
     else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
     else rc = launch_step_vec<1>(*plan, a, stream);

@@ -254,7 +254,7 @@ def test_tuning_knobs_preserve_results(knobs):
     _check_knobs(knobs, F=12)
 
 
-@pytest.mark.parametrize("knobs", [dict(hot=4096), dict(hot=1000, waves=16), dict(hot=32768, waves=4, iter=2, block_iter=1,
+@pytest.mark.parametrize("knobs", [dict(vidx=1), dict(vidx=1, iter=2, block_iter=1, chunk_iter=1), dict(hot=4096), dict(hot=1000, waves=16), dict(hot=32768, waves=4, iter=2, block_iter=1,
                                                                                   chunk_iter=1)])
 def test_hot_column_cache_f1(knobs):
     """F == 1 persistent kernel with the LDS hot-column cache."""
