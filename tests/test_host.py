@@ -125,3 +125,24 @@ def test_accuracy_matches_reference_semantics():
     assert abs(wats_hip.accuracy(out, lab) - 2 / 3) < 1e-7
     with pytest.raises(ValueError):
         wats_hip.accuracy(out.numpy(), lab)
+
+
+@pytest.mark.parametrize("logits", [True, False])
+def test_ece_matches_reference_restatement(logits):
+    """wats_hip.metrics (torch, any device) vs the numpy restatement of
+    utils/ece.py:8-89 (oracle/ece_oracle.py; parity unpinned vs the reference
+    import, which needs seaborn)."""
+    from oracle import ece_oracle as E
+    from wats_hip import metrics as M
+    rng = np.random.default_rng(0)
+    n, c = 700, 7
+    out = rng.standard_normal((n, c)).astype(np.float32) * 3
+    if not logits:
+        out = np.exp(out) / np.exp(out).sum(1, keepdims=True)
+        out[:5, 0] = 0.0          # exact zeros fall in no bin (np.digitize quirk)
+    y = rng.integers(0, c, n)
+    ref = E.calculate_average_ece(out, y, c, logits=logits)
+    got = M.calculate_average_ece(torch.from_numpy(out), torch.from_numpy(y), c, logits=logits)
+    assert abs(got - ref) < 1e-6
+    for k in range(c):
+        assert abs(M.calculate_ece(out, y, k, logits=logits) - E.calculate_ece(out, y, k, logits=logits)) < 1e-6
