@@ -90,7 +90,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.vidx = value ? 1 : 0;
     return WG_OK;
   } else if (!strcmp(key, "bcast")) {
-    L->tune.bcast = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 2));
+    L->tune.bcast = value ? 1 : 0;
     return WG_OK;
   } else if (!strcmp(key, "tile_f")) {
     L->tune.tile_f = (int32_t)std::max<int64_t>(0, value);

@@ -365,8 +365,7 @@ __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t 
   if constexpr (HOT && VEC == 1) {
     accumulate_hot1(a, e, e1, stride, xb, H, acc);
   } else if constexpr (BCAST) {
-    if (a.bcast == 2 && a.LF == 10) accumulate_bcast<VEC, 10>(a, e, e1, stride, xb, acc, fs, base);
-    else if (a.LF % 5 == 0) accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
+    if (a.LF % 5 == 0) accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
     else accumulate_bcast<VEC, 4>(a, e, e1, stride, xb, acc, fs, base);
   } else {
     accumulate<VEC>(a, e, e1, stride, xb, acc);
