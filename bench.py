@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--sharded-extra", default="reddit",
+                    help="also measure this config row-sharded over all ranks (RCCL halo exchange) and attach it "
+                         "as the 'sharded' object of the line; 'none' to skip")
+    ap.add_argument("--sharded-steps", type=int, default=5)
     ap.add_argument("--mode", default="graphs", choices=["graphs", "sharded"],
                     help="graphs: one independent graph per rank (default); sharded: one graph row-sharded over all "
                          "ranks with a per-step RCCL halo exchange")
@@ -93,18 +97,18 @@ def cpu_baseline(g, K, F, s, X, seconds):
                        f"matvecs, {t_total:.1f} s")
 
 
-def sharded_main(args, world, rank, device):
+def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device):
     """One graph (generated identically on every rank, on the GPU) split into
     nnz-balanced row blocks; per Chebyshev step one all_to_all_single halo
-    exchange (RCCL) + the step kernel.  Strong scaling (fixed graph)."""
-    import wats_hip
+    exchange (RCCL) + the step kernel.  Strong scaling (fixed graph).
+    Returns the result dict (meaningful on rank 0)."""
     from wats_hip.dist import ShardedWavelet, partition_rows
     from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
 
-    n_t, nnz_t, K_def, F_def = NAMED_CONFIGS[args.config]
-    K = args.K if args.K is not None else K_def
-    F = args.F if args.F is not None else F_def
-    indptr_d, indices_d = rmat_graph_device(n_t, nnz_t, seed=args.seed, device=device)
+    n_t, nnz_t, K_def, F_def = NAMED_CONFIGS[config]
+    K = K if K is not None else K_def
+    F = F if F is not None else F_def
+    indptr_d, indices_d = rmat_graph_device(n_t, nnz_t, seed=seed, device=device)
     indptr = indptr_d.cpu().numpy()
     bounds = partition_rows(indptr, world)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
@@ -120,16 +124,16 @@ def sharded_main(args, world, rank, device):
         g = torch.Generator(device=device)
         g.manual_seed(1 + rank)
         X = torch.randn(r1 - r0, F, generator=g, device=device)
-    for _ in range(args.warmup):
-        sw.wavelet_features(X, k=K, s=args.s)
+    for _ in range(warmup):
+        sw.wavelet_features(X, k=K, s=s_heat)
     torch.cuda.synchronize(device)
     sw.profile_start()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sw.wavelet_features(X, k=K, s=args.s)
+    for _ in range(steps):
+        sw.wavelet_features(X, k=K, s=s_heat)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -143,35 +147,38 @@ def sharded_main(args, world, rank, device):
     if world > 1:
         dist.all_reduce(nnz_lhat)
     nnz_lhat = float(nnz_lhat.item())
+    p = sw.plan
+    b_step = algorithmic_bytes(p.n_own, sw.L.nnz, F)
+    avg_ms = prof["step_ms"]
+    return {
+        "metric": f"Chebyshev SpMM-chain edges*K/s ({config}-size, K={K}, row-sharded)",
+        "value": nnz_lhat * K * steps / elapsed,
+        "unit": "edges*K/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"{config}-size R-MAT (GPU generator, seed {seed}), one graph row-sharded over "
+                               f"{world} ranks, halo all_to_all_single (RCCL) per Chebyshev step; K={K} F={F}",
+                   "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
+                   "rank0_rows": p.n_own, "rank0_halo_rows": p.n_halo, "parallelism": f"rows x{world}"},
+        "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None,
+                     "traffic": None, "kernel": "cheb_step_kernel (rank 0 shard)",
+                     "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
+                     "avg_exchange_us": prof["exchange_ms"] * 1e3},
+    }
+
+
+def sharded_main(args, world, rank, device):
+    line = run_sharded(args.config, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device)
     if rank == 0:
-        p = sw.plan
-        n_loc = p.n_own
-        b_step = algorithmic_bytes(n_loc, sw.L.nnz, F)
-        avg_ms = prof["step_ms"]
-        line = {
-            "metric": f"Chebyshev SpMM-chain edges*K/s ({args.config}-size, K={K}, row-sharded)",
-            "value": nnz_lhat * K * args.steps / elapsed,
-            "unit": "edges*K/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic",
-            "config": {"workload": f"{args.config}-size R-MAT (GPU generator, seed {args.seed}), one graph row-sharded "
-                                   f"over {world} ranks, halo all_to_all per step; K={K} F={F}",
-                       "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
-                       "rank0_rows": n_loc, "rank0_halo_rows": p.n_halo, "parallelism": f"rows x{world}"},
-            "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None,
-                         "traffic": None, "kernel": "cheb_step_kernel (rank 0 shard)",
-                         "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
-                         "avg_exchange_us": prof["exchange_ms"] * 1e3},
-        }
         js = json.dumps(line)
         print(js, flush=True)
         if args.out:
@@ -248,6 +255,19 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
         edges_k = float(e.item())
 
+    sharded = None
+    if args.sharded_extra and args.sharded_extra != "none":
+        # BASELINE configs 3-4: one big graph row-sharded over all ranks with the
+        # per-step RCCL halo exchange.  Measured after the main line's timing;
+        # a Python-level failure is reported in the line instead of losing it.
+        try:
+            del S, H
+            torch.cuda.empty_cache()
+            sharded = run_sharded(args.sharded_extra, None, None, args.sharded_steps, 1, args.seed, args.s, world,
+                                  rank, device)
+        except Exception as exc:  # noqa: BLE001
+            sharded = {"error": f"{type(exc).__name__}: {exc}"}
+
     if rank == 0:
         avg_ms = prof["sum_ms"] / max(1, prof["launches"])
         # the step kernel processes the rows that enter the chain; purely
@@ -297,6 +317,8 @@ def main():
             },
             "chain_ms": prof["sum_ms"] / args.steps,
         }
+        if sharded is not None:
+            line["sharded"] = sharded
         if world == 1 and not args.no_cpu_baseline:
             if X_host is None:
                 X_host = L.log1p_degree().cpu().numpy()

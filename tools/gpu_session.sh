@@ -34,18 +34,18 @@ timeout -k 10 400 python bench.py --steps ${STEPS:-20} --warmup 3 --out "$OUT/be
 stop_if_fatal $? bench
 if [ "${RUN_PROF:-1}" = 1 ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- \
-      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1
+      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sharded-extra none > "$OUT/prof.log" 2>&1
   stop_if_fatal $? rocprof
 fi
 if [ "${RUN_PMC:-0}" = 1 ]; then
   for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
     tag=$(echo $ctr | cut -d' ' -f1)
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc_$tag" -o run -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$tag.log" 2>&1
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --sharded-extra none > "$OUT/pmc_$tag.log" 2>&1
     stop_if_fatal $? "pmc $tag"
   done
   python tools/pmc_traffic.py "$OUT"/pmc_* --out "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
-  timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --traffic-json "$OUT/traffic.json" \
+  timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --sharded-extra none --traffic-json "$OUT/traffic.json" \
       --out "$OUT/bench_traffic.json" > "$OUT/bench_traffic.log" 2>&1
   stop_if_fatal $? bench_traffic
 fi
