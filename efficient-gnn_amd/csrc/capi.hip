@@ -97,12 +97,29 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "seg_mask")) {
     L->tune.seg_mask = value;
     return WG_OK;  // no replan
+  } else if (!strcmp(key, "lds")) {
+    if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "lds must be 0, 1 or 2");
+    L->tune.lds = (int32_t)value;
+  } else if (!strcmp(key, "lds_cb")) {
+    if (value < 32 || value > 40704) return fail(WG_ERR_INVALID, "lds_cb must be in [32, 40704]");
+    L->tune.lds_cb = (int32_t)value;
+  } else if (!strcmp(key, "lds_iter")) {
+    if (value < 1) return fail(WG_ERR_INVALID, "lds_iter must be >= 1");
+    L->tune.lds_iter = (int32_t)value;
+  } else if (!strcmp(key, "lds_wg")) {
+    L->tune.lds_wg = (int32_t)std::max<int64_t>(0, value);
+  } else if (!strcmp(key, "lds_depth")) {
+    L->tune.lds_depth = (int32_t)value;
+    return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "lds_maxnb")) {
+    L->tune.lds_maxnb = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 64));
   } else {
     return fail(WG_ERR_INVALID, "wg_laplacian_tune: unknown key '%s'", key);
   }
   WG_HIP_TRY(hipDeviceSynchronize());
   for (auto& kv : L->plans) kv.second.release();
   L->plans.clear();
+  release_lds1(L);
   return WG_OK;
 }
 
@@ -117,6 +134,10 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
   snprintf(buf, sizeof(buf), "F=%lld VEC=%d LF=%d segments=%d blocks=%d active_rows=%lld closed_form_rows=%lld\n",
            (long long)F, vec, LF, p->tab.n, p->tab.total_blocks, (long long)L->n_active, (long long)L->n_closed);
   g_text = buf + p->text;
+  if (F == 1) {
+    Lds1Plan* lp = nullptr;
+    if (!get_lds1_plan(L, true, &lp) && lp) g_text += lp->text;
+  }
   return g_text.c_str();
 }
 
@@ -142,9 +163,16 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   hipStream_t stream = as_stream(stream_);
   const int64_t n = L->n_rows;
   if (n == 0) return WG_OK;
-  // workspace: T ping-pong (2) + internal S, 256-B aligned sub-buffers
+  // F == 1 on an unweighted graph: the column-blocked LDS kernel (lds1.hip)
+  Lds1Plan* lp = nullptr;
+  if (F == 1 && K >= 1) {
+    int rc0 = get_lds1_plan(L, /*active_only=*/true, &lp);
+    if (rc0) return rc0;
+  }
+  // workspace: T ping-pong (2) + internal S [+ u ping-pong, padded to whole column blocks], 256-B aligned
   const size_t stride = ((size_t)n * F + 63) / 64 * 64;
-  const size_t need = 3 * stride;
+  const size_t ustride = lp ? ((size_t)lp->lchunks * lp->nb * 32 + 63) / 64 * 64 : 0;
+  const size_t need = 3 * stride + 2 * ustride;
   if (L->ws_floats < need) {
     WG_HIP_TRY(hipStreamSynchronize(stream));
     (void)hipFree(L->ws);
@@ -163,6 +191,20 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   // T_k = (-1)^k X0 exactly, so S = X0 * sum_k (-1)^k alpha_k (WATS.py:65-68)
   double coef = 0.0;
   for (int32_t k = 0; k <= K; ++k) coef += ((k & 1) ? -1.0 : 1.0) * std::exp(-s * (double)k);
+  if (lp) {
+    float* u[2] = {L->ws + 3 * stride, L->ws + 3 * stride + ustride};  // u_{k-1} = T_{k-1} * dinv
+    rc = launch_scale_dinv(L, lp->n, b0, u[0], stream);
+    if (rc) return rc;
+    for (int32_t k = 1; k <= K; ++k) {
+      const float* xm1 = (k & 1) ? b0 : b1;
+      const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
+      float* xk = (k == K) ? nullptr : ((k & 1) ? b1 : b0);
+      rc = launch_lds1_step(L, lp, k, u[(k - 1) & 1], xm1, xm2, xk, (k == K) ? nullptr : u[k & 1], sint, 1.0,
+                            std::exp(-s * (double)k), stream);
+      if (rc) return rc;
+    }
+    return launch_finalize(L, F, sint, b0, coef, S, H, stream);
+  }
   for (int32_t k = 1; k <= K; ++k) {
     const float* xm1 = (k & 1) ? b0 : b1;
     const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);

@@ -78,6 +78,36 @@ struct Plan {
   void release();
 };
 
+// F == 1 column-blocked plan (lds1.hip): columns are dealt to NB blocks in
+// 32-column chunks (chunk c -> block c % NB); each workgroup stages one
+// block of the gather vector u = T_{k-1} * dinv in LDS and walks the entries
+// of that block, stored block-major with 16-bit local column ids.
+struct Lds1Plan {
+  int32_t n = 0;              // rows
+  int32_t n_cols = 0;         // column space
+  int32_t nb = 0;             // column blocks
+  int32_t lchunks = 0;        // 32-column chunks per block (LDS floats = 32 * lchunks)
+  int32_t n_wg = 0;           // workgroups of the main kernel
+  int32_t n_groups = 0;
+  int64_t nnz = 0;
+  int32_t* brp = nullptr;     // device [nb * n + 1]: block b row r = [brp[b*n+r], brp[b*n+r+1])
+  uint16_t* bcol = nullptr;   // device [nnz + 8]: local column ids
+  int2* groups = nullptr;     // device: {first row, rows | lanes-per-row << 16}
+  int4* wgs = nullptr;        // device [n_wg]: {block, first group, end group, 0}
+  float* part = nullptr;      // device: teams [nb * n] block partial sums (nb > 1); windows [n_pairs]
+  // mode 2 (windows): (row, block) segments padded to 8-id chunks, bit 15 of a
+  // segment's first id flags its start; one wave streams a contiguous chunk range
+  int32_t mode = 1;           // 1 = row teams, 2 = chunk windows
+  int64_t n_chunks = 0;
+  int32_t n_pairs = 0;        // non-empty (row, block) segments
+  uint4* chunk = nullptr;     // device [n_chunks]
+  int32_t* pos = nullptr;     // device [nb * n]: segment id of (block, row), -1 if empty
+  int4* wdesc = nullptr;      // device [n_wg * 16]: {first chunk, end chunk, first segment, 0}
+  int32_t* wblock = nullptr;  // device [n_wg]: column block of each workgroup
+  std::string text;
+  void release();
+};
+
 struct Tuning {
   // 0 = shape-dependent default (see default_knobs in step.hip)
   int32_t iter = 0;          // team mode: target nonzeros per lane sub-group
@@ -90,6 +120,12 @@ struct Tuning {
   int32_t waves = 4;         // waves per step-kernel workgroup: 4, 8 or 16
   int32_t hot = 0;           // F == 1: LDS hot-column cache size (columns), 0 = off
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments
+  int32_t lds = 2;           // F == 1, unit weights: column-blocked LDS kernel (0 = off, 1 = row teams, 2 = chunk windows)
+  int32_t lds_cb = 32768;    // LDS floats per column block (multiple of 32, <= 40960)
+  int32_t lds_iter = 8;      // target entries per lane per row team
+  int32_t lds_wg = 0;        // workgroups of the LDS kernel (0 = auto)
+  int32_t lds_maxnb = 16;    // largest block count the LDS kernel takes (else the gather kernel)
+  int32_t lds_depth = 4;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
 };
 
 }  // namespace wg
@@ -111,6 +147,12 @@ struct wg_laplacian_s {
   int64_t n_closed = 0;       // purely isolated rows at the end: T_k = (-1)^k X0 (closed form)
   wg::Tuning tune;
   std::map<int, wg::Plan> plans;  // key: (LF * 8 + VEC) * 2 + active_only
+  // unweighted graph (every off-diagonal a_ij == 1): L_hat_ij = -dinv_i dinv_j
+  // up to scipy's float32 rounding, so the F == 1 LDS kernel reads no values
+  bool unit = false;
+  double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
+  wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
+  bool lds1_failed[2] = {false, false};        // not applicable (too many blocks): use the gather kernel
   // workspace for wg_wavelet_features
   float* ws = nullptr;
   size_t ws_floats = 0;
@@ -132,4 +174,15 @@ int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float
                     float* S, float* H, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);
+int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start);
+// lds1.hip
+int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out);  // *out = nullptr: not applicable
+void release_lds1(wg_laplacian_s* L);
+// u = x * dinv (float32), rows [0, n)
+int launch_scale_dinv(wg_laplacian_s* L, int64_t n, const float* x, float* u, hipStream_t stream);
+// one Chebyshev step, F == 1: gathers u_km1 (n_cols, padded to 32), own rows of t_km1 (iso), t_km2, writes t_k,
+// u_k = t_k * dinv (nullable), S
+int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_km1, const float* t_km1,
+                     const float* t_km2, float* t_k, float* u_k, float* S, double alpha0, double alpha_k,
+                     hipStream_t stream);
 }  // namespace wg

@@ -1,0 +1,697 @@
+// lds1.hip -- the F == 1 Chebyshev step for unweighted graphs, with the
+// gather vector staged in LDS (reference calibration/WATS.py:32-36: the
+// recurrence; :65-68: the heat sum, fused into the epilogue).
+//
+// Why: at F == 1 every nonzero is one random 4-byte gather.  The gather kernel
+// (step.hip) issues it as a global load, and the texture-address unit then
+// spends about one cycle per distinct cache line: on the Reddit-size graph it
+// was 90 % busy and the step ran at 17 % of the HBM roofline (profiles/r01
+// s7, s11).  A random ds_read_b32 costs a few LDS cycles instead.
+//
+// Operator.  For an unweighted graph (every off-diagonal a_ij == 1) scipy's
+// value is L_hat_ij = -fl(fl(1 / sw_i) / sw_j) (_laplacian.py:472-474), i.e.
+// -dinv_i * dinv_j up to float32 rounding.  So
+//     (L_hat x)_i = -dinv_i * sum_j u_j  (- x_i if row i is isolated),
+//     u_j = fl32(x_j * dinv_j),
+// and the entry stream carries column ids only: no values.  The difference
+// from the scipy-rounded values is a few float32 ulps per term, far inside
+// the 1e-5 contract (tests/test_gpu_parity.py).
+//
+// Layout.  Columns are dealt to NB blocks in 32-column chunks (chunk c ->
+// block c % NB), which spreads the high-degree columns (relabelled to the
+// front) evenly over the blocks.  Block b's entries are stored block-major,
+// rows in internal order, with 16-bit local column ids
+//     local(c) = (c / 32 / NB) * 32 + c % 32,
+// 2 bytes per nonzero instead of 8 (int32 index + float32 value).
+//
+// Kernel.  One 1024-thread workgroup per CU holds one block of u in LDS
+// (<= 160 KiB) and walks a contiguous range of "row groups" of that block:
+// 64 / LN consecutive rows, LN lanes per row (LN a power of two sized to the
+// rows' lengths).  Waves take groups from an LDS counter.  Sums are float64
+// in a fixed order, so results do not depend on the schedule.  With NB == 1
+// the epilogue runs in place; otherwise every (block, row) writes a float32
+// partial and combine_lds1_kernel adds the NB partials in block order and runs
+// the epilogue.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "internal.h"
+
+namespace wg {
+namespace {
+
+constexpr int kLdsThreads = 1024;
+
+struct Lds1Args {
+  const int32_t* brp;
+  const uint16_t* bcol;
+  const int2* groups;
+  const int4* wgs;
+  const float* u_in;   // u_{k-1}, n_cols (padded to a multiple of 32)
+  const float* xm1;    // T_{k-1} own rows (isolated rows' diagonal; T_0 when k == 1)
+  const float* xm2;    // T_{k-2} (k >= 2)
+  float* xk;           // T_k (nullable)
+  float* u_out;        // u_k = T_k * dinv (nullable)
+  float* S;            // heat sum (nullable)
+  float* part;         // block partials (nb > 1)
+  const double* dinv;
+  const uint8_t* iso;
+  int32_t n;
+  int32_t nb;
+  int32_t lchunks;
+  int32_t k;
+  double alpha0;
+  double alpha_k;
+};
+
+// T_k,i = 2 (L_hat T_{k-1})_i - T_{k-2,i}  (k == 1: T_1 = L_hat T_0), S, u_k.
+__device__ __forceinline__ void lds1_epilogue(const Lds1Args& a, int32_t row, double acc) {
+  const double di = a.dinv[row];
+  double off = -di * acc;
+  const float xo = a.xm1[row];
+  if (a.iso[row]) off -= (double)xo;  // L_hat_ii = -1
+  double t;
+  if (a.k == 1) {
+    t = off;
+  } else {
+    t = 2.0 * off - (double)a.xm2[row];
+  }
+  if (a.xk) __builtin_nontemporal_store((float)t, a.xk + row);
+  if (a.u_out) a.u_out[row] = (float)(t * di);
+  if (a.S) {
+    const double s = (a.k == 1) ? a.alpha0 * (double)xo + a.alpha_k * t : (double)a.S[row] + a.alpha_k * t;
+    __builtin_nontemporal_store((float)s, a.S + row);
+  }
+}
+
+extern __shared__ float g_u_lds[];
+
+template <bool DIRECT>
+__global__ __launch_bounds__(kLdsThreads) void cheb_lds1_kernel(Lds1Args a) {
+  __shared__ int s_next;
+  const int4 d = a.wgs[blockIdx.x];
+  const int b = d.x;
+  // stage block b of u: local chunk lc <- global chunk lc * nb + b (128 B each)
+  {
+    const int n4 = a.lchunks * 8;
+    const float4* src = reinterpret_cast<const float4*>(a.u_in);
+    float4* dst = reinterpret_cast<float4*>(g_u_lds);
+    for (int i = threadIdx.x; i < n4; i += kLdsThreads) {
+      const int64_t g4 = ((int64_t)(i >> 3) * a.nb + b) * 8 + (i & 7);
+      dst[i] = src[g4];
+    }
+  }
+  if (threadIdx.x == 0) s_next = d.y;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const float* __restrict__ u = g_u_lds;
+  const uint16_t* __restrict__ bcol = a.bcol;
+  const int32_t* __restrict__ rp = a.brp + (int64_t)b * a.n;
+  for (;;) {
+    int g = 0;
+    if (lane == 0) g = atomicAdd(&s_next, 1);
+    g = __builtin_amdgcn_readfirstlane(__shfl(g, 0, 64));
+    if (g >= d.z) break;
+    const int2 gd = a.groups[g];
+    const int nrows = gd.y & 0xffff;
+    const int ln = gd.y >> 16;        // power of two, <= 64
+    const int sh = __ffs(ln) - 1;
+    const int team = lane >> sh;
+    const int q = lane & (ln - 1);
+    const int32_t row = gd.x + team;
+    const bool act = team < nrows;
+    double acc = 0.0;
+    if (act) {
+      const int32_t e1 = rp[row + 1];
+      int32_t e = rp[row] + q;
+      for (; e + 3 * ln < e1; e += 4 * ln) {
+        const uint16_t c0 = bcol[e], c1 = bcol[e + ln], c2 = bcol[e + 2 * ln], c3 = bcol[e + 3 * ln];
+        const float x0 = u[c0], x1 = u[c1], x2 = u[c2], x3 = u[c3];
+        acc += (double)x0;
+        acc += (double)x1;
+        acc += (double)x2;
+        acc += (double)x3;
+      }
+      for (; e < e1; e += ln) acc += (double)u[bcol[e]];
+    }
+    for (int o = ln >> 1; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (act && q == 0) {
+      if constexpr (DIRECT) lds1_epilogue(a, row, acc);
+      else a.part[(int64_t)b * a.n + row] = (float)acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void combine_lds1_kernel(Lds1Args a) {
+  const int32_t row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= a.n) return;
+  double acc = 0.0;
+  for (int b = 0; b < a.nb; ++b) acc += (double)a.part[(int64_t)b * a.n + row];  // fixed block order
+  lds1_epilogue(a, row, acc);
+}
+
+__global__ void scale_dinv_kernel(int64_t n, const float* __restrict__ x, const double* __restrict__ dinv,
+                                  float* __restrict__ u) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) u[i] = (float)((double)x[i] * dinv[i]);
+}
+
+// block entry counts: cnt[b * n + r] = entries of row r in block b
+__global__ __launch_bounds__(256) void lds1_count_kernel(int32_t n, int32_t nb, const int32_t* __restrict__ rowptr,
+                                                        const int32_t* __restrict__ col, int32_t* __restrict__ cnt) {
+  const int32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  for (int32_t e = rowptr[r] + lane; e < rowptr[r + 1]; e += 64) {
+    const int32_t b = (col[e] >> 5) % nb;
+    atomicAdd(cnt + (int64_t)b * n + r, 1);
+  }
+}
+
+// block-major entries with local column ids, each (row, block) in CSR order
+__global__ __launch_bounds__(256) void lds1_fill_kernel(int32_t n, int32_t nb, const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ col, const int32_t* __restrict__ brp,
+                                                       uint16_t* __restrict__ bcol) {
+  const int32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  int32_t mypos = lane < nb ? brp[(int64_t)lane * n + r] : 0;  // lane b: next slot of block b
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int32_t e0 = rowptr[r], e1 = rowptr[r + 1];
+  for (int32_t base = e0; base < e1; base += 64) {
+    const int32_t e = base + lane;
+    int32_t c = 0, blk = -1;
+    if (e < e1) {
+      c = col[e];
+      blk = (c >> 5) % nb;
+    }
+    for (int bb = 0; bb < nb; ++bb) {
+      const unsigned long long m = __ballot(blk == bb);
+      if (!m) continue;
+      const int32_t pos = __shfl(mypos, bb, 64);
+      if (blk == bb) bcol[pos + __popcll(m & lt)] = (uint16_t)((((c >> 5) / nb) << 5) | (c & 31));
+      if (lane == bb) mypos += __popcll(m);
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// mode 2: chunk windows.  Every non-empty (row, block) segment is padded to a
+// whole number of 8-id chunks (16 B; pad ids point at a zero LDS slot), and
+// bit 15 of the first id of a segment flags its start.  A wave streams a
+// contiguous chunk range, 64 chunks (512 ids, one 16-B load per lane) per
+// window with the next two windows in flight; a lane sums its chunk's 8
+// values, and a segmented inclusive scan over the wave (fixed shuffle order)
+// gives each segment's sum, carried across windows in registers.  Each
+// segment's sum goes to part[segment]; combine_lds2_kernel adds each row's
+// segments in block order and runs the epilogue.
+struct Lds2Args {
+  const uint4* chunk;
+  const int4* wdesc;
+  const int32_t* wblock;
+  const int32_t* pos;
+  Lds1Args e;  // epilogue operands (+ u_in, part, nb, lchunks, n)
+};
+
+__device__ __forceinline__ uint4 load_chunk(const uint4* __restrict__ ch, int32_t c, int32_t c1, uint32_t zz) {
+  return (c < c1) ? ch[c] : make_uint4(zz, zz, zz, zz);
+}
+
+// One step of the segmented inclusive scan through DPP (VALU only, no LDS):
+// add the value of the lane CTRL selects when it belongs to the same segment.
+// Lanes without a source keep `old` (0.0 / an impossible segment id).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void seg_scan_step(double& s, int32_t pid) {
+  const int lo = __double2loint(s), hi = __double2hiint(s);
+  const int tlo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xf, false);
+  const int thi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROWMASK, 0xf, false);
+  const int tp = __builtin_amdgcn_update_dpp(INT32_MIN, pid, CTRL, ROWMASK, 0xf, false);
+  if (tp == pid) s += __hiloint2double(thi, tlo);
+}
+
+// One window: lane sums its chunk's 8 values; segmented inclusive scan over
+// the wave (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31 across
+// rows: a fixed order); segment sums to part[], the open one carried in
+// (cur, carry).
+__device__ __forceinline__ void lds2_window(const uint4 q, const float* __restrict__ u, float* __restrict__ part,
+                                            int lane, int32_t first, int32_t& cur, double& carry) {
+  const bool flag = (q.x & 0x8000u) != 0u;
+  double s = (double)u[q.x & 0x7fffu];
+  s += (double)u[q.x >> 16];
+  s += (double)u[q.y & 0xffffu];
+  s += (double)u[q.y >> 16];
+  s += (double)u[q.z & 0xffffu];
+  s += (double)u[q.z >> 16];
+  s += (double)u[q.w & 0xffffu];
+  s += (double)u[q.w >> 16];
+  const unsigned long long F = __ballot(flag);
+  // segment id: cur + number of segment starts at lanes <= lane
+  const int32_t pid = cur + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u)) +
+                      (flag ? 1 : 0);
+  seg_scan_step<0x111, 0xf>(s, pid);  // row_shr:1
+  seg_scan_step<0x112, 0xf>(s, pid);  // row_shr:2
+  seg_scan_step<0x114, 0xf>(s, pid);  // row_shr:4
+  seg_scan_step<0x118, 0xf>(s, pid);  // row_shr:8
+  seg_scan_step<0x142, 0xa>(s, pid);  // row_bcast:15 -> rows 1, 3
+  seg_scan_step<0x143, 0xc>(s, pid);  // row_bcast:31 -> rows 2, 3
+  if (pid == cur) s += carry;                                            // continued from the last window
+  if ((F & 1ull) && lane == 0 && cur >= first) part[cur] = (float)carry;  // it ended at the boundary
+  // a segment ends at lane l < 63 when lane l + 1 starts one
+  if (lane < 63 && ((F >> (lane + 1)) & 1ull)) part[pid] = (float)s;
+  cur += (int32_t)__popcll(F);
+  const int lo = __builtin_amdgcn_readlane(__double2loint(s), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(s), 63);
+  carry = __hiloint2double(hi, lo);
+}
+
+// D windows in flight per wave: the loop is unrolled by D so each window's
+// registers are reloaded in place (no copy that would wait on a pending load).
+template <int D>
+__global__ __launch_bounds__(kLdsThreads) void cheb_lds2_kernel(Lds2Args A) {
+  const Lds1Args& a = A.e;
+  const int b = A.wblock[blockIdx.x];
+  const int zslot = a.lchunks * 32;  // zero slot for pad ids
+  {
+    const int n4 = a.lchunks * 8;
+    const float4* src = reinterpret_cast<const float4*>(a.u_in);
+    float4* dst = reinterpret_cast<float4*>(g_u_lds);
+    for (int i = threadIdx.x; i < n4; i += kLdsThreads) {
+      const int64_t g4 = ((int64_t)(i >> 3) * a.nb + b) * 8 + (i & 7);
+      dst[i] = src[g4];
+    }
+    if (threadIdx.x == 0) g_u_lds[zslot] = 0.0f;
+  }
+  const int lane = threadIdx.x & 63;
+  const int4 wd = A.wdesc[blockIdx.x * (kLdsThreads / 64) + (threadIdx.x >> 6)];
+  const int32_t c0 = wd.x, c1 = wd.y;
+  const uint4* __restrict__ ch = A.chunk;
+  const uint32_t zz = (uint32_t)zslot | ((uint32_t)zslot << 16);
+  uint4 q[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) q[i] = load_chunk(ch, c0 + 64 * i + lane, c1, zz);  // overlaps the LDS fill
+  __syncthreads();
+  const float* __restrict__ u = g_u_lds;
+  float* __restrict__ part = a.part;
+  int32_t cur = wd.z - 1;  // segment open at the window start (none yet)
+  double carry = 0.0;
+  for (int32_t cw = c0; cw < c1; cw += 64 * D) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int32_t w0 = cw + 64 * i;
+      if (w0 < c1) {
+        const uint4 cq = q[i];
+        q[i] = load_chunk(ch, w0 + 64 * D + lane, c1, zz);
+        lds2_window(cq, u, part, lane, wd.z, cur, carry);
+      }
+    }
+  }
+  if (lane == 0 && cur >= wd.z) part[cur] = (float)carry;
+}
+
+__global__ __launch_bounds__(256) void combine_lds2_kernel(Lds2Args A) {
+  const Lds1Args& a = A.e;
+  const int32_t row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= a.n) return;
+  double acc = 0.0;
+  for (int b = 0; b < a.nb; ++b) {  // fixed block order
+    const int32_t p = A.pos[(int64_t)b * a.n + row];
+    if (p >= 0) acc += (double)a.part[p];
+  }
+  lds1_epilogue(a, row, acc);
+}
+
+// segment fill: wave per row; lane b owns the row's segment of block b
+// (start chunk cpt[b * n + r]); ids keep CSR order, pad ids -> zero slot,
+// bit 15 on the segment's first id
+__global__ __launch_bounds__(256) void lds2_fill_kernel(int32_t n, int32_t nb, int32_t zslot,
+                                                       const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ col, const int32_t* __restrict__ cpt,
+                                                       const int32_t* __restrict__ cnt, uint16_t* __restrict__ ids) {
+  const int32_t r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  const int64_t start = lane < nb ? (int64_t)cpt[(int64_t)lane * n + r] * 8 : 0;
+  int64_t mypos = start;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int32_t e0 = rowptr[r], e1 = rowptr[r + 1];
+  for (int32_t base = e0; base < e1; base += 64) {
+    const int32_t e = base + lane;
+    int32_t c = 0, blk = -1;
+    if (e < e1) {
+      c = col[e];
+      blk = (c >> 5) % nb;
+    }
+    for (int bb = 0; bb < nb; ++bb) {
+      const unsigned long long m = __ballot(blk == bb);
+      if (!m) continue;
+      const int64_t p0 = __shfl(mypos, bb, 64);
+      const int64_t s0 = __shfl(start, bb, 64);
+      if (blk == bb) {
+        const int64_t dst = p0 + __popcll(m & lt);
+        uint32_t id = (uint32_t)((((c >> 5) / nb) << 5) | (c & 31));
+        if (dst == s0) id |= 0x8000u;
+        ids[dst] = (uint16_t)id;
+      }
+      if (lane == bb) mypos += __popcll(m);
+    }
+  }
+  if (lane < nb) {
+    const int32_t k = cnt[(int64_t)lane * n + r];
+    for (int64_t q = start + k; q < start + ((int64_t)k + 7) / 8 * 8; ++q) ids[q] = (uint16_t)zslot;
+  }
+}
+
+int n_cus(int dev) {
+  static int cached[64] = {0};
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+
+
+// mode 2 plan: segment chunk offsets, segment ids, chunk array, wave ranges.
+// `cnt` = entries per (block, row) (block-major), p->brp holds the same on the device.
+int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cnt) {
+  const int64_t n = p->n, nb = p->nb;
+  p->mode = 2;
+  std::vector<int32_t> cpt(nb * n), pos(nb * n);
+  std::vector<int64_t> seg_chunk;  // first chunk of each segment (+ end sentinel)
+  std::vector<int64_t> bseg(nb + 1);
+  int64_t chunks = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    bseg[b] = (int64_t)seg_chunk.size();
+    for (int64_t r = 0; r < n; ++r) {
+      const int64_t i = b * n + r;
+      const int64_t k = cnt[i];
+      cpt[i] = (int32_t)chunks;
+      if (k > 0) {
+        pos[i] = (int32_t)seg_chunk.size();
+        seg_chunk.push_back(chunks);
+        chunks += (k + 7) / 8;
+      } else {
+        pos[i] = -1;
+      }
+    }
+  }
+  bseg[nb] = (int64_t)seg_chunk.size();
+  seg_chunk.push_back(chunks);
+  if (chunks >= INT32_MAX / 2) return fail(WG_ERR_UNSUPPORTED, "lds2 plan: too many chunks (%lld)", (long long)chunks);
+  p->n_chunks = chunks;
+  p->n_pairs = (int32_t)(seg_chunk.size() - 1);
+  // waves: workgroups split evenly over the blocks, each block's segments cut
+  // into 16 * (its workgroups) contiguous ranges of equal cost (chunks + 1 per segment)
+  constexpr int kW = kLdsThreads / 64;
+  int n_wg = L->tune.lds_wg > 0 ? L->tune.lds_wg : n_cus(L->device);
+  n_wg = (int)std::max<int64_t>(nb, std::min<int64_t>(n_wg, ceil_div(chunks + p->n_pairs, 256)));
+  std::vector<int4> wd;
+  std::vector<int32_t> wb;
+  for (int64_t b = 0; b < nb; ++b) {
+    const int m = (int)(n_wg / nb + (b < n_wg % nb ? 1 : 0));
+    const int64_t s0 = bseg[b], s1 = bseg[b + 1];
+    const int64_t tot = (seg_chunk[s1] - seg_chunk[s0]) + (s1 - s0);
+    int64_t sg = s0;
+    for (int w = 0; w < m * kW; ++w) {
+      const int64_t target = tot * (w + 1) / (m * kW);
+      const int64_t g0 = sg;
+      while (sg < s1 && ((seg_chunk[sg + 1] - seg_chunk[s0]) + (sg + 1 - s0) <= target || w == m * kW - 1)) ++sg;
+      wd.push_back(make_int4((int)seg_chunk[g0], (int)seg_chunk[sg], (int)g0, 0));
+      if (w % kW == 0) wb.push_back((int32_t)b);
+    }
+  }
+  p->n_wg = (int32_t)wb.size();
+  int rc = 0;
+  int32_t* cpt_d = nullptr;
+  if ((rc = dmalloc(&p->chunk, (size_t)chunks + 1)) || (rc = dmalloc(&p->pos, (size_t)(nb * n))) ||
+      (rc = dmalloc(&p->wdesc, wd.size())) || (rc = dmalloc(&p->wblock, wb.size())) ||
+      (rc = dmalloc(&p->part, (size_t)std::max<int32_t>(1, p->n_pairs))) || (rc = dmalloc(&cpt_d, (size_t)(nb * n))))
+    return rc;
+  auto done = [&](int code) {
+    (void)hipFree(cpt_d);
+    return code;
+  };
+  if (hipMemcpy(cpt_d, cpt.data(), sizeof(int32_t) * nb * n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p->pos, pos.data(), sizeof(int32_t) * nb * n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p->wdesc, wd.data(), sizeof(int4) * wd.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p->wblock, wb.data(), sizeof(int32_t) * wb.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return done(fail(WG_ERR_HIP, "lds2 plan: upload failed"));
+  hipLaunchKernelGGL(lds2_fill_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, 0, (int32_t)n, (int32_t)nb,
+                     p->lchunks * 32, L->rowptr, L->col, cpt_d, p->brp, reinterpret_cast<uint16_t*>(p->chunk));
+  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return done(fail(WG_ERR_HIP, "lds2 plan: fill failed"));
+  done(0);
+  char buf[256];
+  snprintf(buf, sizeof(buf),
+           "lds1: windows rows=%lld cols=%d nnz=%lld blocks=%lld lds_floats=%d segments=%d chunks=%lld "
+           "(pad %.1f%%) workgroups=%d (+combine)\n",
+           (long long)n, p->n_cols, (long long)p->nnz, (long long)nb, p->lchunks * 32, p->n_pairs, (long long)chunks,
+           p->nnz ? 100.0 * (8.0 * chunks - p->nnz) / p->nnz : 0.0, p->n_wg);
+  p->text = buf;
+  return WG_OK;
+}
+}  // namespace
+
+void Lds1Plan::release() {
+  for (void* p : {(void*)brp, (void*)bcol, (void*)groups, (void*)wgs, (void*)part, (void*)chunk, (void*)pos,
+                  (void*)wdesc, (void*)wblock})
+    (void)hipFree(p);
+  chunk = nullptr;
+  pos = nullptr;
+  wdesc = nullptr;
+  wblock = nullptr;
+  brp = nullptr;
+  bcol = nullptr;
+  groups = nullptr;
+  wgs = nullptr;
+  part = nullptr;
+}
+
+void release_lds1(wg_laplacian_s* L) {
+  for (int i = 0; i < 2; ++i) {
+    if (L->lds1[i]) {
+      L->lds1[i]->release();
+      delete L->lds1[i];
+      L->lds1[i] = nullptr;
+    }
+    L->lds1_failed[i] = false;
+  }
+}
+
+int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
+  *out = nullptr;
+  active_only = active_only && L->reordered;
+  const int slot = active_only ? 1 : 0;
+  if (L->lds1[slot]) {
+    *out = L->lds1[slot];
+    return WG_OK;
+  }
+  if (!L->unit || !L->dinv || L->tune.lds == 0 || L->lds1_failed[slot]) return WG_OK;
+  const int64_t n = active_only ? L->n_active : L->n_rows;
+  const int64_t n_cols = active_only ? L->n_active : L->n_cols;
+  // + static LDS <= 160 KiB; windows: 15-bit local ids and a zero slot at 32 * lchunks
+  const int cb = std::max(32, std::min(L->tune.lds == 2 ? 32736 : 40704, L->tune.lds_cb / 32 * 32));
+  const int64_t nchunks = ceil_div(std::max<int64_t>(n_cols, 1), 32);
+  const int64_t nb = ceil_div(nchunks, cb / 32);
+  if (n == 0 || nb > std::min(L->tune.lds_maxnb, 64)) {
+    L->lds1_failed[slot] = true;
+    return WG_OK;
+  }
+  auto* p = new Lds1Plan();
+  p->n = (int32_t)n;
+  p->n_cols = (int32_t)n_cols;
+  p->nb = (int32_t)nb;
+  p->lchunks = (int32_t)ceil_div(nchunks, nb);
+  int rc = WG_OK;
+  auto bail = [&](int code) {
+    p->release();
+    delete p;
+    return code;
+  };
+  int32_t nnz = 0;
+  WG_HIP_TRY(hipMemcpy(&nnz, L->rowptr + n, sizeof(int32_t), hipMemcpyDeviceToHost));
+  p->nnz = nnz;
+  const int64_t ncnt = nb * n + 1;
+  if ((rc = dmalloc(&p->brp, ncnt))) return bail(rc);
+  WG_HIP_TRY(hipMemset(p->brp, 0, sizeof(int32_t) * ncnt));
+  const dim3 rgrid((unsigned)ceil_div(n, 4));
+  hipLaunchKernelGGL(lds1_count_kernel, rgrid, dim3(256), 0, 0, (int32_t)n, (int32_t)nb, L->rowptr, L->col, p->brp);
+  WG_LAUNCH_CHECK();
+  // exclusive scan on the host (the plan is built once per graph; brp is small)
+  std::vector<int32_t> h(ncnt);
+  WG_HIP_TRY(hipMemcpy(h.data(), p->brp, sizeof(int32_t) * ncnt, hipMemcpyDeviceToHost));
+  if (L->tune.lds == 2) {
+    rc = build_windows(L, p, h);
+    if (rc) return bail(rc);
+    L->lds1[slot] = p;
+    *out = p;
+    return WG_OK;
+  }
+  if ((rc = dmalloc(&p->bcol, (size_t)nnz + 8))) return bail(rc);
+  WG_HIP_TRY(hipMemset(p->bcol, 0, sizeof(uint16_t) * ((size_t)nnz + 8)));
+  {
+    int64_t run = 0;
+    for (int64_t i = 0; i < ncnt; ++i) {
+      const int64_t c = h[i];
+      h[i] = (int32_t)run;
+      run += c;
+    }
+    if (run != nnz) return bail(fail(WG_ERR_HIP, "lds1 plan: entry count %lld != nnz %d", (long long)run, nnz));
+  }
+  WG_HIP_TRY(hipMemcpy(p->brp, h.data(), sizeof(int32_t) * ncnt, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(lds1_fill_kernel, rgrid, dim3(256), 0, 0, (int32_t)n, (int32_t)nb, L->rowptr, L->col, p->brp,
+                     p->bcol);
+  WG_LAUNCH_CHECK();
+
+  // row groups per block: 64/LN consecutive rows, LN lanes per row
+  const int iter = std::max(1, L->tune.lds_iter);
+  std::vector<int2> groups;
+  std::vector<int64_t> gcost;  // entries + per-row overhead, for the workgroup split
+  std::vector<int64_t> bfirst(nb + 1);
+  for (int64_t b = 0; b < nb; ++b) {
+    bfirst[b] = (int64_t)groups.size();
+    const int32_t* r = h.data() + b * n;
+    auto len = [&](int64_t i) { return (int64_t)(r[i + 1] - r[i]); };
+    int64_t i = 0;
+    while (i < n) {
+      int ln = 1;
+      while (ln < 64 && (int64_t)ln * iter < len(i)) ln <<= 1;
+      int rows = (int)std::min<int64_t>(64 / ln, n - i);
+      // a longer row further in the group widens the team (rows are only roughly sorted per block)
+      for (;;) {
+        int64_t mx = 0;
+        for (int j = 0; j < rows; ++j) mx = std::max(mx, len(i + j));
+        if (ln >= 64 || mx <= 2 * (int64_t)ln * iter) break;
+        ln <<= 1;
+        rows = (int)std::min<int64_t>(64 / ln, n - i);
+      }
+      int64_t c = 16;
+      for (int j = 0; j < rows; ++j) c += len(i + j) + 2;
+      groups.push_back(make_int2((int32_t)i, rows | (ln << 16)));
+      gcost.push_back(c);
+      i += rows;
+    }
+  }
+  bfirst[nb] = (int64_t)groups.size();
+  p->n_groups = (int32_t)groups.size();
+  // workgroups: about one per CU, split evenly over the blocks, each block's
+  // groups cut into equal-cost contiguous ranges
+  int n_wg = L->tune.lds_wg > 0 ? L->tune.lds_wg : n_cus(L->device);
+  n_wg = (int)std::max<int64_t>(nb, std::min<int64_t>(n_wg, ceil_div(nnz + 2 * n, 4096)));
+  std::vector<int4> wgs;
+  for (int64_t b = 0; b < nb; ++b) {
+    const int m = (int)(n_wg / nb + (b < n_wg % nb ? 1 : 0));
+    int64_t tot = 0;
+    for (int64_t g = bfirst[b]; g < bfirst[b + 1]; ++g) tot += gcost[g];
+    int64_t g = bfirst[b], acc = 0;
+    for (int w = 0; w < m; ++w) {
+      const int64_t target = tot * (w + 1) / m;
+      const int64_t g0 = g;
+      while (g < bfirst[b + 1] && (acc + gcost[g] <= target || w == m - 1)) acc += gcost[g++];
+      if (g > g0 || w == m - 1) wgs.push_back(make_int4((int)b, (int)g0, (int)g, 0));
+    }
+  }
+  p->n_wg = (int32_t)wgs.size();
+  if ((rc = dmalloc(&p->groups, groups.size())) || (rc = dmalloc(&p->wgs, wgs.size())) ||
+      (rc = dmalloc(&p->part, nb > 1 ? (size_t)(nb * n) : 1)))
+    return bail(rc);
+  WG_HIP_TRY(hipMemcpy(p->groups, groups.data(), sizeof(int2) * std::max<size_t>(1, groups.size()),
+                       hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipMemcpy(p->wgs, wgs.data(), sizeof(int4) * std::max<size_t>(1, wgs.size()), hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipDeviceSynchronize());
+  char buf[256];
+  snprintf(buf, sizeof(buf), "lds1: rows=%lld cols=%lld nnz=%d blocks=%lld lds_floats=%d groups=%d workgroups=%d%s\n",
+           (long long)n, (long long)n_cols, nnz, (long long)nb, p->lchunks * 32, p->n_groups, p->n_wg,
+           nb > 1 ? " (+combine)" : "");
+  p->text = buf;
+  L->lds1[slot] = p;
+  *out = p;
+  return WG_OK;
+}
+
+int launch_scale_dinv(wg_laplacian_s* L, int64_t n, const float* x, float* u, hipStream_t stream) {
+  if (n <= 0) return WG_OK;
+  hipLaunchKernelGGL(scale_dinv_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, n, x, L->dinv, u);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
+int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_km1, const float* t_km1,
+                     const float* t_km2, float* t_k, float* u_k, float* S, double alpha0, double alpha_k,
+                     hipStream_t stream) {
+  if (p->n == 0) return WG_OK;
+  if (int rc = prof_mark(L, stream, true)) return rc;
+  static bool attr_set[2] = {false, false};
+  const size_t lds = (size_t)p->lchunks * 32 * sizeof(float);
+  Lds1Args a{};
+  a.brp = p->brp;
+  a.bcol = p->bcol;
+  a.groups = p->groups;
+  a.wgs = p->wgs;
+  a.u_in = u_km1;
+  a.xm1 = t_km1;
+  a.xm2 = t_km2;
+  a.xk = t_k;
+  a.u_out = u_k;
+  a.S = S;
+  a.part = p->part;
+  a.dinv = L->dinv;
+  a.iso = L->iso;
+  a.n = p->n;
+  a.nb = p->nb;
+  a.lchunks = p->lchunks;
+  a.k = k;
+  a.alpha0 = alpha0;
+  a.alpha_k = alpha_k;
+  if (p->mode == 2) {
+    const int depth = L->tune.lds_depth >= 8 ? 8 : L->tune.lds_depth >= 4 ? 4 : 2;
+    const void* fn2 = depth == 8   ? (const void*)cheb_lds2_kernel<8>
+                      : depth == 4 ? (const void*)cheb_lds2_kernel<4>
+                                   : (const void*)cheb_lds2_kernel<2>;
+    static bool attr2[3] = {false, false, false};
+    const int ai = depth == 8 ? 2 : depth == 4 ? 1 : 0;
+    if (!attr2[ai]) {
+      WG_HIP_TRY(hipFuncSetAttribute(fn2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
+      attr2[ai] = true;
+    }
+    Lds2Args A{};
+    A.chunk = p->chunk;
+    A.wdesc = p->wdesc;
+    A.wblock = p->wblock;
+    A.pos = p->pos;
+    A.e = a;
+    if (depth == 8)
+      hipLaunchKernelGGL(cheb_lds2_kernel<8>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);
+    else if (depth == 4)
+      hipLaunchKernelGGL(cheb_lds2_kernel<4>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);
+    else
+      hipLaunchKernelGGL(cheb_lds2_kernel<2>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);
+    WG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(combine_lds2_kernel, dim3((unsigned)ceil_div(p->n, 256)), dim3(256), 0, stream, A);
+    WG_LAUNCH_CHECK();
+    return prof_mark(L, stream, false);
+  }
+  const bool direct = p->nb == 1;
+  const void* fn = direct ? (const void*)cheb_lds1_kernel<true> : (const void*)cheb_lds1_kernel<false>;
+  if (!attr_set[direct]) {
+    WG_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
+    attr_set[direct] = true;
+  }
+  if (direct)
+    hipLaunchKernelGGL(cheb_lds1_kernel<true>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
+  else
+    hipLaunchKernelGGL(cheb_lds1_kernel<false>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
+  WG_LAUNCH_CHECK();
+  if (!direct) {
+    hipLaunchKernelGGL(combine_lds1_kernel, dim3((unsigned)ceil_div(p->n, 256)), dim3(256), 0, stream, a);
+    WG_LAUNCH_CHECK();
+  }
+  return prof_mark(L, stream, false);
+}
+
+}  // namespace wg

@@ -31,7 +31,7 @@ namespace {
 __global__ __launch_bounds__(kBlock) void row_info_kernel(
     int64_t n_rows, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ values, int32_t* __restrict__ offdiag_len, double* __restrict__ rowsum,
-    float* __restrict__ diag, double* __restrict__ colsum, int32_t* __restrict__ colcnt) {
+    float* __restrict__ diag, double* __restrict__ colsum, int32_t* __restrict__ colcnt, int32_t* __restrict__ nonunit) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n_rows) return;
@@ -48,6 +48,7 @@ __global__ __launch_bounds__(kBlock) void row_info_kernel(
     } else {
       ++cnt;
       atomicAdd(colcnt + c, 1);
+      if (v != 1.0f) *nonunit = 1;  // weighted off-diagonal entry
     }
     if (colsum) atomicAdd(colsum + c, (double)v);
   }
@@ -94,6 +95,15 @@ __global__ void degree_kernel(int64_t n_cols, int64_t n_rows, const float* __res
   const bool iso = (w == 0.0f);
   sw[j] = iso ? 1.0f : sqrtf(w);
   iso_col[j] = iso ? 1 : 0;
+}
+
+// dinv in the internal column order: 1 / sw (float64), sw as scipy's float32
+__global__ void dinv_kernel(int64_t n_cols, int64_t n_rows, const int32_t* __restrict__ perm, const float* __restrict__ sw,
+                            double* __restrict__ dinv) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_cols) return;
+  const int64_t src = (j < n_rows) ? perm[j] : j;
+  dinv[j] = 1.0 / (double)sw[src];
 }
 
 // Sort key: off-diagonal length, then "needed in the chain" (0 for purely
@@ -312,16 +322,18 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   int32_t* colcnt;
   unsigned long long *key, *key_sorted;
   unsigned int* npure_d;
+  int32_t* nonunit_d;
   if ((rc = tmp.alloc(&colcnt, n_cols)) || (rc = tmp.alloc(&key, n_rows)) || (rc = tmp.alloc(&key_sorted, n_rows)) ||
-      (rc = tmp.alloc(&npure_d, 1)))
+      (rc = tmp.alloc(&npure_d, 1)) || (rc = tmp.alloc(&nonunit_d, 1)))
     return rc;
+  WG_HIP_TRY(hipMemsetAsync(nonunit_d, 0, sizeof(int32_t), stream));
   WG_HIP_TRY(hipMemsetAsync(colcnt, 0, sizeof(int32_t) * std::max<int64_t>(1, n_cols), stream));
   if ((rc = tmp.alloc(&len, n_rows)) || (rc = tmp.alloc(&len_sorted, n_rows)) || (rc = tmp.alloc(&ids, n_rows)) ||
       (rc = tmp.alloc(&rowsum64, n_rows)) || (rc = tmp.alloc(&diag, n_rows)) || (rc = tmp.alloc(&colsum32, n_cols)) ||
       (rc = tmp.alloc(&sw, n_cols)) || (rc = tmp.alloc(&iso_col, n_cols)) || (rc = tmp.alloc(&hist, kBuckets)))
     return rc;
   if ((rc = dmalloc(&L->rowptr, n_rows + 1)) || (rc = dmalloc(&L->iso, n_rows)) || (rc = dmalloc(&L->perm, n_rows)) ||
-      (rc = dmalloc(&L->iperm, n_rows)) || (rc = dmalloc(&L->rowsum, n_rows)))
+      (rc = dmalloc(&L->iperm, n_rows)) || (rc = dmalloc(&L->rowsum, n_rows)) || (rc = dmalloc(&L->dinv, n_cols)))
     return rc;
   const bool unweighted_colsum = (w_cols == nullptr) && (values == nullptr);
   if (unweighted_colsum) {
@@ -330,7 +342,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   }
   if (n_rows > 0) {
     hipLaunchKernelGGL(row_info_kernel, dim3(ceil_div(n_rows, 4)), dim3(kBlock), 0, stream, n_rows, indptr, indices,
-                       values, len, rowsum64, diag, colsum64, colcnt);
+                       values, len, rowsum64, diag, colsum64, colcnt, nonunit_d);
     WG_LAUNCH_CHECK();
   }
   if (w_cols == nullptr && n_cols > 0) {
@@ -400,6 +412,8 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   }
   hipLaunchKernelGGL(invert_perm_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, L->perm, L->iperm);
   WG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dinv_kernel, dim3(nb_cols), dim3(256), 0, stream, n_cols, n_rows, L->perm, sw, L->dinv);
+  WG_LAUNCH_CHECK();
   hipLaunchKernelGGL(gather_len_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, L->perm, len, len_sorted, iso_col,
                      L->iso);
   WG_LAUNCH_CHECK();
@@ -438,6 +452,9 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
     WG_HIP_TRY(hipStreamSynchronize(stream));
     max_len = *std::max_element(lh.begin(), lh.end());
   }
+  int32_t nonunit = 0;
+  WG_HIP_TRY(hipMemcpy(&nonunit, nonunit_d, sizeof(int32_t), hipMemcpyDeviceToHost));
+  L->unit = (nonunit == 0);
   int64_t niso = 0;
   for (auto v : isoh) niso += v;
   L->n_iso = niso;
@@ -455,8 +472,9 @@ using namespace wg;
 wg_laplacian_s::~wg_laplacian_s() {
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   for (auto& kv : plans) kv.second.release();
+  wg::release_lds1(this);
   for (void* p : {(void*)rowptr, (void*)col, (void*)val, (void*)iso, (void*)perm, (void*)iperm, (void*)rowsum,
-                  (void*)ws})
+                  (void*)ws, (void*)dinv})
     (void)hipFree(p);
 }
 

@@ -856,7 +856,6 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   return WG_OK;
 }
 
-namespace {
 // Profiling: a pair of timing-only events around every step launch (both
 // kernels of a split step).  hipEventDisableSystemFence: no system-scope
 // release (cache write-back / invalidate) -- the events must not perturb the
@@ -876,7 +875,6 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start) {
   }
   return WG_OK;
 }
-}  // namespace
 
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only) {

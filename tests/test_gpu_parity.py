@@ -277,3 +277,74 @@ def _check_knobs(knobs, F):
     assert_parity(_np(H1), ref["H"], what=f"{knobs} H")
     if set(knobs) <= {"bcast", "nt"}:
         assert torch.equal(S0, S1), "same plan must give bitwise-identical results"
+
+
+# ----------------------------------------------------------------- F == 1 column-blocked LDS kernel
+@pytest.mark.parametrize("knobs", [dict(lds=0), dict(lds=1), dict(lds=1, lds_cb=2048), dict(lds=1, lds_cb=1024, lds_iter=2),
+                                   dict(lds=1, lds_cb=4096, lds_iter=64, lds_wg=7),
+                                   dict(lds=1, lds_cb=512, lds_maxnb=64), dict(lds=1, lds_cb=40704, lds_wg=1),
+                                   dict(lds=2, lds_cb=2048), dict(lds=2, lds_cb=512, lds_maxnb=64),
+                                   dict(lds=2, lds_wg=3), dict(lds=2, lds_cb=4096, lds_wg=1000),
+                                   dict(lds=2, lds_depth=2), dict(lds=2, lds_depth=8, lds_cb=1024)])
+def test_lds1_plans_f1(knobs):
+    """The LDS kernel (one and many column blocks, every team width, any
+    workgroup split) and the gather kernel it replaces agree with the oracle."""
+    _check_knobs(knobs, F=1)
+
+
+def test_lds1_is_the_f1_path_and_deterministic():
+    g = named_graph("pubmed")
+    L = NormalizedLaplacian.from_graph(g)
+    assert "lds1:" in L.describe(1)
+    L.tune(lds=1, lds_cb=2048)
+    assert "(+combine)" in L.describe(1)
+    X = L.log1p_degree()
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=16, X0=X, return_S=True)
+    H2, S2 = wats_hip.graph_wavelet_features(L, k=16, X0=X, return_S=True)
+    assert torch.equal(S1, S2) and torch.equal(H1, H2)
+    L.tune(lds=2, lds_cb=2048)
+    assert "windows" in L.describe(1)
+    X = L.log1p_degree()
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=16, X0=X, return_S=True)
+    H2, S2 = wats_hip.graph_wavelet_features(L, k=16, X0=X, return_S=True)
+    assert torch.equal(S1, S2) and torch.equal(H1, H2)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_lds1_directed_isolated_selfloops(seed):
+    """Unweighted directed graph with self loops and isolated nodes (L_hat_ii = -1
+    rows that still have off-diagonal entries) through the LDS kernel."""
+    g = random_graph(3000, 0.004, seed=seed, directed=True, weighted=False, self_loop_frac=0.05, isolated_frac=0.05)
+    A = g.to_scipy()
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(lds_cb=512 if seed else 32768)
+    assert "lds1:" in L.describe(1)
+    X = np.random.default_rng(seed).standard_normal((g.n, 1)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=7, s=0.8, X0=X, return_all=True)
+    H, S = wats_hip.graph_wavelet_features(L, k=7, X0=torch.from_numpy(X), return_S=True)
+    assert_parity(_np(S), ref["S"], what="lds1 directed S")
+    # H = S / (|S| + 1e-8) at F = 1 is ill-conditioned where |S| ~ 1e-8..1e-4 (a random
+    # signal cancels there; float32 storage alone gives ~3e-5 on such rows): compare H
+    # where |S| is not tiny, and check H is exactly the normalisation of the S we return
+    Sg, Hg = _np(S).astype(np.float64), _np(H).astype(np.float64)
+    ok = np.abs(ref["S"]) > 1e-3 * np.abs(ref["S"]).max()
+    assert np.abs(Hg[ok] - ref["H"][ok]).max() <= 1e-5
+    np.testing.assert_allclose(Hg, (Sg / (np.abs(Sg) + 1e-8)).astype(np.float32), rtol=1e-6, atol=1e-7)
+
+
+def test_lds1_not_taken_for_weighted_graphs():
+    g = random_graph(500, 0.02, seed=3, directed=False, weighted=True)
+    L = NormalizedLaplacian.from_graph(g)
+    assert "lds1:" not in L.describe(1)
+
+
+def test_lds1_arxiv_f1_vs_oracle():
+    """ogbn-arxiv-size at F = 1 (the reference signal) through the LDS kernel (3 blocks)."""
+    g = named_graph("ogbn-arxiv")
+    A = g.to_scipy()
+    L = NormalizedLaplacian.from_graph(g)
+    assert "lds1:" in L.describe(1)
+    ref = O.graph_wavelet_features(A, k=16, s=0.8, return_all=True)
+    H, S = wats_hip.graph_wavelet_features(L, k=16, return_S=True)
+    assert_parity(_np(S), ref["S"], what="arxiv F=1 S")
+    assert_parity(_np(H), ref["H"], what="arxiv F=1 H")
