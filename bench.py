@@ -77,6 +77,21 @@ def algorithmic_bytes(n: int, nnz: int, F: int) -> int:
     return 8 * nnz + 4 * (n + 1) + 20 * n * F
 
 
+def lds_algorithmic_bytes(info: dict) -> int:
+    """Bytes one step of the F == 1 column-blocked LDS kernel must move
+    (its entries carry 16-bit column ids and no values):
+    ids 2 B/nnz; float32 block partials written + read (8 B per non-empty
+    (row, block) segment); segment map 4 B per (block, row); per row: T_{k-1}
+    (isolated diagonal), T_{k-2}, T_k, u_k = T_k*dinv (4 B each), S read+write
+    (8 B), dinv (8 B, float64), iso (1 B); the gathered u read once (4 B/column;
+    the per-workgroup LDS fills are L2 hits).  Chunk padding is excluded here
+    (it is real traffic, visible in the PMC `traffic`)."""
+    n, nb, nnz, segs, cols = info["rows"], info["blocks"], info["nnz"], info["segments"], info["cols"]
+    if info["mode"] == 2:
+        return 2 * nnz + 8 * segs + 4 * nb * n + 33 * n + 4 * cols
+    return 2 * nnz + 4 * (nb * n + 1) + (8 * nb * n if nb > 1 else 0) + 33 * n + 4 * cols
+
+
 def cpu_baseline(g, K, F, s, X, seconds):
     from oracle import wats_oracle as O
     A = g.to_scipy()
@@ -148,7 +163,11 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device):
         dist.all_reduce(nnz_lhat)
     nnz_lhat = float(nnz_lhat.item())
     p = sw.plan
-    b_step = algorithmic_bytes(p.n_own, sw.L.nnz, F)
+    b_8d = algorithmic_bytes(p.n_own, sw.L.nnz, F)
+    lds_info = sw.L.lds_plan_info(active_only=False) if (F == 1 and sw.u_len() > 0) else None
+    b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
+    kernel = ("cheb_lds2_kernel + combine_lds2_kernel" if lds_info and lds_info["mode"] == 2 else
+              "cheb_lds1_kernel" if lds_info else "cheb_step_kernel") + " (rank 0 shard)"
     avg_ms = prof["step_ms"]
     return {
         "metric": f"Chebyshev SpMM-chain edges*K/s ({config}-size, K={K}, row-sharded)",
@@ -170,9 +189,13 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device):
         "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None,
-                     "traffic": None, "kernel": "cheb_step_kernel (rank 0 shard)",
+                     "traffic": None, "kernel": kernel,
                      "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
-                     "avg_exchange_us": prof["exchange_ms"] * 1e3},
+                     "avg_exchange_us": prof["exchange_ms"] * 1e3,
+                     "byte_model": "lds (16-bit ids, no values; DESIGN.md 4.4)" if lds_info else "SURVEY 8(d)",
+                     "lds_plan": lds_info,
+                     "nominal_8d_bytes": b_8d,
+                     "nominal_8d_frac": (b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None},
     }
 
 
@@ -273,7 +296,9 @@ def main():
         # the step kernel processes the rows that enter the chain; purely
         # isolated rows (closed form T_k = (-1)^k X0) are handled by finalize
         n_active = n - int(L.info["n_closed_form"])
-        b_step = algorithmic_bytes(n_active, nnz, F)
+        b_8d = algorithmic_bytes(n_active, nnz, F)
+        lds_info = L.lds_plan_info(active_only=True) if F == 1 else None
+        b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
         achieved = b_step / (avg_ms * 1e-3) / 1e9
         traffic = None
         if args.traffic_json and os.path.exists(args.traffic_json):
@@ -306,11 +331,14 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "cheb_step_kernel",
+                "kernel": ("cheb_lds2_kernel + combine_lds2_kernel" if lds_info and lds_info["mode"] == 2 else
+                           "cheb_lds1_kernel" if lds_info else "cheb_step_kernel"),
+                "byte_model": "lds (16-bit ids, no values; DESIGN.md 4.4)" if lds_info else "SURVEY 8(d)",
                 "algorithmic_bytes_per_launch": b_step,
                 "rows_per_launch": n_active,
                 "closed_form_rows": n - n_active,
                 "algorithmic_bytes_all_rows": algorithmic_bytes(n, nnz, F),
+                "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "avg_launch_us": avg_ms * 1e3,
                 "max_launch_us": prof["max_ms"] * 1e3,
                 "launches": prof["launches"],

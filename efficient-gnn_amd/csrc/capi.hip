@@ -108,6 +108,10 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.lds_iter = (int32_t)value;
   } else if (!strcmp(key, "lds_wg")) {
     L->tune.lds_wg = (int32_t)std::max<int64_t>(0, value);
+  } else if (!strcmp(key, "lds_k")) {
+    if (value != 1 && value != 2 && value != 4) return fail(WG_ERR_INVALID, "lds_k must be 1, 2 or 4");
+    L->tune.lds_k = (int32_t)value;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "lds_depth")) {
     L->tune.lds_depth = (int32_t)value;
     return WG_OK;  // launch-time choice
@@ -146,6 +150,48 @@ int wg_cheb_step(wg_laplacian_t L, int32_t k, int64_t F, const float* t_km1, con
   if (!L || k < 1 || F < 1 || !t_km1 || (k >= 2 && !t_km2) || (H && !S))
     return fail(WG_ERR_INVALID, "wg_cheb_step: bad arguments (k=%d F=%lld)", k, (long long)F);
   return launch_step(L, k, F, t_km1, t_km2, t_k, S, H, alpha0, alpha_k, as_stream(stream_));
+}
+
+int wg_cheb_u_len(wg_laplacian_t L, int64_t* len) {
+  if (!L || !len) return fail(WG_ERR_INVALID, "wg_cheb_u_len: NULL argument");
+  *len = 0;
+  Lds1Plan* lp = nullptr;
+  if (int rc = get_lds1_plan(L, /*active_only=*/false, &lp)) return rc;
+  if (lp) *len = (int64_t)lp->lchunks * lp->nb * 32;
+  return WG_OK;
+}
+
+int wg_lds_plan_info(wg_laplacian_t L, int32_t active_only, int64_t* out) {
+  if (!L || !out) return fail(WG_ERR_INVALID, "wg_lds_plan_info: NULL argument");
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+  Lds1Plan* lp = nullptr;
+  if (int rc = get_lds1_plan(L, active_only != 0, &lp)) return rc;
+  if (!lp) return WG_OK;
+  out[0] = lp->mode;
+  out[1] = lp->nb;
+  out[2] = lp->n;
+  out[3] = lp->n_cols;
+  out[4] = lp->nnz;
+  out[5] = lp->mode == 2 ? lp->n_pairs : (lp->nb > 1 ? (int64_t)lp->nb * lp->n : 0);
+  out[6] = lp->n_chunks;
+  out[7] = lp->n_wg;
+  return WG_OK;
+}
+
+int wg_scale_dinv(wg_laplacian_t L, const float* x, float* u, void* stream_) {
+  if (!L || (L->n_rows && (!x || !u))) return fail(WG_ERR_INVALID, "wg_scale_dinv: bad arguments");
+  return launch_scale_dinv(L, L->n_rows, x, u, as_stream(stream_));
+}
+
+int wg_cheb_step_u(wg_laplacian_t L, int32_t k, const float* u_km1, const float* t_km1, const float* t_km2,
+                   float* t_k, float* u_k, float* S, double alpha0, double alpha_k, void* stream_) {
+  if (!L || k < 1 || (L->n_rows && (!u_km1 || !t_km1)) || (k >= 2 && L->n_rows && !t_km2))
+    return fail(WG_ERR_INVALID, "wg_cheb_step_u: bad arguments (k=%d)", k);
+  Lds1Plan* lp = nullptr;
+  if (int rc = get_lds1_plan(L, /*active_only=*/false, &lp)) return rc;
+  if (!lp) return fail(WG_ERR_UNSUPPORTED, "wg_cheb_step_u: the LDS kernel does not apply to this handle");
+  return launch_lds1_step(L, lp, k, u_km1, t_km1, k >= 2 ? t_km2 : nullptr, t_k, u_k, S, alpha0, alpha_k,
+                          as_stream(stream_));
 }
 
 int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float* src, float* dst, void* stream_) {

@@ -125,7 +125,8 @@ struct Tuning {
   int32_t lds_iter = 8;      // target entries per lane per row team
   int32_t lds_wg = 0;        // workgroups of the LDS kernel (0 = auto)
   int32_t lds_maxnb = 16;    // largest block count the LDS kernel takes (else the gather kernel)
-  int32_t lds_depth = 4;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
+  int32_t lds_depth = 2;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
+  int32_t lds_k = 4;         // windows: chunks per lane (1 = cheb_lds2_kernel, 2 / 4 = cheb_lds3_kernel)
 };
 
 }  // namespace wg

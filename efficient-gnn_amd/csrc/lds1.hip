@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <utility>
 
 #include "internal.h"
 
@@ -212,11 +213,20 @@ struct Lds2Args {
   const int4* wdesc;
   const int32_t* wblock;
   const int32_t* pos;
+  int32_t n_part;  // segments (part[] length)
   Lds1Args e;  // epilogue operands (+ u_in, part, nb, lchunks, n)
 };
 
-__device__ __forceinline__ uint4 load_chunk(const uint4* __restrict__ ch, int32_t c, int32_t c1, uint32_t zz) {
-  return (c < c1) ? ch[c] : make_uint4(zz, zz, zz, zz);
+// Prefetch: an unconditional load from a clamped index (`last` is a valid
+// chunk).  Chunks past the wave's range are replaced by pad ids where they are
+// consumed (mask_chunk), not here: touching a loaded value right after the
+// load (or loading inside a branch) makes the waitcnt pass drain every
+// in-flight load, which serialises the prefetch.
+__device__ __forceinline__ uint4 load_chunk(const uint4* __restrict__ ch, int32_t c, int32_t last) {
+  return ch[min(c, last)];
+}
+__device__ __forceinline__ uint4 mask_chunk(const uint4 v, bool ok, uint32_t zz) {
+  return make_uint4(ok ? v.x : zz, ok ? v.y : zz, ok ? v.z : zz, ok ? v.w : zz);
 }
 
 // One step of the segmented inclusive scan through DPP (VALU only, no LDS):
@@ -231,13 +241,22 @@ __device__ __forceinline__ void seg_scan_step(double& s, int32_t pid) {
   if (tp == pid) s += __hiloint2double(thi, tlo);
 }
 
-// One window: lane sums its chunk's 8 values; segmented inclusive scan over
-// the wave (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31 across
-// rows: a fixed order); segment sums to part[], the open one carried in
-// (cur, carry).
-__device__ __forceinline__ void lds2_window(const uint4 q, const float* __restrict__ u, float* __restrict__ part,
-                                            int lane, int32_t first, int32_t& cur, double& carry) {
+// Window scan (independent of the carry, so two windows' scans interleave):
+// the lane's chunk sum of its 8 values, then a segmented inclusive scan over
+// the wave -- row_shr 1/2/4/8 inside 16-lane rows, row_bcast 15 / 31 across
+// rows, a fixed order.  lpid = segment starts at lanes <= lane (0: the
+// segment open at the window start).
+struct WinScan {
+  double s;
+  unsigned long long F;
+  int32_t lpid;
+};
+__device__ __forceinline__ WinScan lds2_scan(const uint4 q, const float* __restrict__ u) {
+  WinScan w;
   const bool flag = (q.x & 0x8000u) != 0u;
+#ifdef WG_EXP_NOLDS  // timing-only experiment: no LDS reads (wrong results)
+  double s = (double)(q.x & 0x7fffu) + (double)(q.y & 0xffffu) + (double)(q.z & 0xffffu) + (double)(q.w >> 16);
+#else
   double s = (double)u[q.x & 0x7fffu];
   s += (double)u[q.x >> 16];
   s += (double)u[q.y & 0xffffu];
@@ -246,29 +265,52 @@ __device__ __forceinline__ void lds2_window(const uint4 q, const float* __restri
   s += (double)u[q.z >> 16];
   s += (double)u[q.w & 0xffffu];
   s += (double)u[q.w >> 16];
-  const unsigned long long F = __ballot(flag);
-  // segment id: cur + number of segment starts at lanes <= lane
-  const int32_t pid = cur + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u)) +
-                      (flag ? 1 : 0);
-  seg_scan_step<0x111, 0xf>(s, pid);  // row_shr:1
-  seg_scan_step<0x112, 0xf>(s, pid);  // row_shr:2
-  seg_scan_step<0x114, 0xf>(s, pid);  // row_shr:4
-  seg_scan_step<0x118, 0xf>(s, pid);  // row_shr:8
-  seg_scan_step<0x142, 0xa>(s, pid);  // row_bcast:15 -> rows 1, 3
-  seg_scan_step<0x143, 0xc>(s, pid);  // row_bcast:31 -> rows 2, 3
-  if (pid == cur) s += carry;                                            // continued from the last window
-  if ((F & 1ull) && lane == 0 && cur >= first) part[cur] = (float)carry;  // it ended at the boundary
+#endif
+  w.F = __ballot(flag);
+#ifdef WG_EXP_NOSCAN  // timing-only experiment: no segmented scan (wrong results)
+  w.lpid = 0;
+  w.s = s;
+  return w;
+#endif
+  w.lpid = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(w.F >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)w.F, 0u)) +
+           (flag ? 1 : 0);
+  seg_scan_step<0x111, 0xf>(s, w.lpid);  // row_shr:1
+  seg_scan_step<0x112, 0xf>(s, w.lpid);  // row_shr:2
+  seg_scan_step<0x114, 0xf>(s, w.lpid);  // row_shr:4
+  seg_scan_step<0x118, 0xf>(s, w.lpid);  // row_shr:8
+  seg_scan_step<0x142, 0xa>(s, w.lpid);  // row_bcast:15 -> rows 1, 3
+  seg_scan_step<0x143, 0xc>(s, w.lpid);  // row_bcast:31 -> rows 2, 3
+  w.s = s;
+  return w;
+}
+
+// Window finish: segment sums to part[], the open one carried in (cur, carry).
+// Branch-free: both stores are buffer stores every lane issues (the b32
+// builtin takes integer data: store the float's bits), with an out-of-range
+// offset (dropped by the hardware) where nothing is due, so the waitcnt pass
+// sees the same memory-op count on every path.
+__device__ __forceinline__ void lds2_finish(WinScan w, __amdgpu_buffer_rsrc_t part, int lane, int32_t first,
+                                            int32_t& cur, double& carry) {
+  constexpr uint32_t kDrop = 0x80000000u;
+  const int32_t pid = cur + w.lpid;
+  double s = w.s;
+  if (w.lpid == 0) s += carry;  // continued from the last window
+  // the open segment ended at the window boundary: lane 0 flushes the carry
+  const bool flush = (w.F & 1ull) && lane == 0 && cur >= first;
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)carry), part, flush ? (uint32_t)cur * 4u : kDrop, 0, 0);
   // a segment ends at lane l < 63 when lane l + 1 starts one
-  if (lane < 63 && ((F >> (lane + 1)) & 1ull)) part[pid] = (float)s;
-  cur += (int32_t)__popcll(F);
+  const bool end = lane < 63 && ((w.F >> (lane + 1)) & 1ull);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)s), part, end ? (uint32_t)pid * 4u : kDrop, 0, 0);
+  cur += (int32_t)__popcll(w.F);
   const int lo = __builtin_amdgcn_readlane(__double2loint(s), 63);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(s), 63);
   carry = __hiloint2double(hi, lo);
 }
 
-// D windows in flight per wave: the loop is unrolled by D so each window's
-// registers are reloaded in place (no copy that would wait on a pending load).
+// D (even) windows in flight per wave, processed in pairs: both loads of the
+// next pair are issued first, then the two scans (independent), then the two
+// finishes.  The loop is unrolled so each window's registers are reloaded in
+// place (no copy that would wait on a pending load).
 template <int D>
 __global__ __launch_bounds__(kLdsThreads) void cheb_lds2_kernel(Lds2Args A) {
   const Lds1Args& a = A.e;
@@ -289,36 +331,199 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_lds2_kernel(Lds2Args A) {
   const int32_t c0 = wd.x, c1 = wd.y;
   const uint4* __restrict__ ch = A.chunk;
   const uint32_t zz = (uint32_t)zslot | ((uint32_t)zslot << 16);
+  const int32_t last = max(c1 - 1, 0);
+  const __amdgpu_buffer_rsrc_t part =
+      __builtin_amdgcn_make_buffer_rsrc(a.part, 0, A.n_part * 4, 0x00020000);  // raw buffer, gfx9 dword 3
   uint4 q[D];
 #pragma unroll
-  for (int i = 0; i < D; ++i) q[i] = load_chunk(ch, c0 + 64 * i + lane, c1, zz);  // overlaps the LDS fill
+  for (int i = 0; i < D; ++i) {  // overlaps the LDS fill
+    q[i] = load_chunk(ch, c0 + 64 * i + lane, last);
+    // the loop issues (load, store, store) per window; two dropped stores here give the
+    // loop header the same in-flight pattern on entry, so its wait keeps D windows in flight
+    __builtin_amdgcn_raw_buffer_store_b32(0u, part, 0x80000000u, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(0u, part, 0x80000000u, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   __syncthreads();
   const float* __restrict__ u = g_u_lds;
-  float* __restrict__ part = a.part;
   int32_t cur = wd.z - 1;  // segment open at the window start (none yet)
   double carry = 0.0;
+  // whole groups of D windows; windows past c1 are all pad ids (no flags, no stores)
   for (int32_t cw = c0; cw < c1; cw += 64 * D) {
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-      const int32_t w0 = cw + 64 * i;
-      if (w0 < c1) {
-        const uint4 cq = q[i];
-        q[i] = load_chunk(ch, w0 + 64 * D + lane, c1, zz);
-        lds2_window(cq, u, part, lane, wd.z, cur, carry);
-      }
+    for (int i = 0; i < D; i += 2) {
+      const int32_t w0 = cw + 64 * i, w1 = w0 + 64;
+      const uint4 qa = mask_chunk(q[i], w0 + lane < c1, zz);
+      const uint4 qb = mask_chunk(q[i + 1], w1 + lane < c1, zz);
+      q[i] = load_chunk(ch, w0 + 64 * D + lane, last);
+      q[i + 1] = load_chunk(ch, w1 + 64 * D + lane, last);
+      __builtin_amdgcn_sched_barrier(0);  // issue the prefetches here, not after the windows
+      const WinScan sa = lds2_scan(qa, u);
+      const WinScan sb = lds2_scan(qb, u);
+      lds2_finish(sa, part, lane, wd.z, cur, carry);
+      lds2_finish(sb, part, lane, wd.z, cur, carry);
     }
   }
-  if (lane == 0 && cur >= wd.z) part[cur] = (float)carry;
+  if (lane == 0 && cur >= wd.z) a.part[cur] = (float)carry;
+}
+
+// ---------------------------------------------------------------------------
+// K chunks per lane (K = 2, 4): a window is 64*K consecutive chunks, lane l
+// holding chunks K*l .. K*l+K-1 in sequence order.  Segments that start and
+// end inside a lane are summed sequentially and stored by that lane; one
+// segmented scan over the lanes' tail sums per window (K times fewer scans
+// per id than cheb_lds2_kernel).  Lane l's scan segment starts at the highest
+// lane <= l holding a segment start (seg0); a scan step adds its source lane
+// when the source is >= seg0.  Same fixed order on every run.
+__device__ __forceinline__ double chunk_sum(const uint4 q, const float* __restrict__ u) {
+  double s = (double)u[q.x & 0x7fffu];
+  s += (double)u[q.x >> 16];
+  s += (double)u[q.y & 0xffffu];
+  s += (double)u[q.y >> 16];
+  s += (double)u[q.z & 0xffffu];
+  s += (double)u[q.z >> 16];
+  s += (double)u[q.w & 0xffffu];
+  s += (double)u[q.w >> 16];
+  return s;
+}
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void seg_scan_step_src(double& s, int src, int seg0) {
+  const int tlo = __builtin_amdgcn_update_dpp(0, __double2loint(s), CTRL, ROWMASK, 0xf, false);
+  const int thi = __builtin_amdgcn_update_dpp(0, __double2hiint(s), CTRL, ROWMASK, 0xf, false);
+  if (src >= seg0) s += __hiloint2double(thi, tlo);  // lanes without a source read 0.0
+}
+
+template <int K>
+__device__ __forceinline__ void lds3_window(const uint4 (&q)[K], const float* __restrict__ u,
+                                            __amdgpu_buffer_rsrc_t part, int lane, int32_t first, int32_t& cur,
+                                            double& carry) {
+  constexpr uint32_t kDrop = 0x80000000u;
+  double sc[K];
+  bool f[K];
+  int32_t before = 0;  // segment starts in lanes < lane
+  int32_t total = 0;   // segment starts in the window
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    f[j] = (q[j].x & 0x8000u) != 0u;
+    sc[j] = chunk_sum(q[j], u);
+    const unsigned long long B = __ballot(f[j]);
+    before += (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(B >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)B, 0u));
+    total += (int32_t)__popcll(B);
+  }
+  const int32_t open = cur + before;  // segment open before this lane's first chunk
+  // lane-local: head (chunks before the first start), segments inside the lane, tail
+  double run = 0.0, head = 0.0;
+  int nf = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {  // branch-free: a (possibly dropped) store per slot
+    // a start after an earlier one in this lane ends a segment that lies inside the lane
+    const bool inner = f[j] && nf > 0;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)run), part, inner ? (uint32_t)(open + nf) * 4u : kDrop,
+                                          0, 0);
+    head = (f[j] && nf == 0) ? run : head;
+    run = f[j] ? 0.0 : run;
+    nf += f[j] ? 1 : 0;
+    run += sc[j];
+  }
+  const bool has = nf > 0;
+  // scan over lanes: value = tail sum (whole lane when it holds no start)
+  const unsigned long long H = __ballot(has);
+  const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+  const unsigned long long m = H & le;
+  const int seg0 = m ? 63 - __clzll(m) : -1;
+  double P = run;
+  seg_scan_step_src<0x111, 0xf>(P, lane - 1, seg0);                     // row_shr:1
+  seg_scan_step_src<0x112, 0xf>(P, lane - 2, seg0);                     // row_shr:2
+  seg_scan_step_src<0x114, 0xf>(P, lane - 4, seg0);                     // row_shr:4
+  seg_scan_step_src<0x118, 0xf>(P, lane - 8, seg0);                     // row_shr:8
+  seg_scan_step_src<0x142, 0xa>(P, (lane & ~15) - 1, seg0);             // row_bcast:15 -> rows 1, 3
+  seg_scan_step_src<0x143, 0xc>(P, 31, seg0);                           // row_bcast:31 -> rows 2, 3
+  if (seg0 < 0) P += carry;  // the window's open segment
+  // value of the segment open before this lane, at the end of lane - 1
+  const int plo = __builtin_amdgcn_update_dpp(0, __double2loint(P), 0x138, 0xf, 0xf, false);  // wave_shr:1
+  const int phi = __builtin_amdgcn_update_dpp(0, __double2hiint(P), 0x138, 0xf, 0xf, false);
+  const double Pprev = (lane == 0) ? carry : __hiloint2double(phi, plo);
+  // a lane holding a start completes the segment open before it
+  const bool done = has && !(lane == 0 && open < first);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)(Pprev + head)), part,
+                                        done ? (uint32_t)open * 4u : kDrop, 0, 0);
+  const int lo = __builtin_amdgcn_readlane(__double2loint(P), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(P), 63);
+  carry = __hiloint2double(hi, lo);
+  cur += total;
+}
+
+template <int K>
+__global__ __launch_bounds__(kLdsThreads) void cheb_lds3_kernel(Lds2Args A) {
+  constexpr int D = 2;  // windows in flight
+  const Lds1Args& a = A.e;
+  const int b = A.wblock[blockIdx.x];
+  const int zslot = a.lchunks * 32;
+  {
+    const int n4 = a.lchunks * 8;
+    const float4* src = reinterpret_cast<const float4*>(a.u_in);
+    float4* dst = reinterpret_cast<float4*>(g_u_lds);
+    for (int i = threadIdx.x; i < n4; i += kLdsThreads) {
+      const int64_t g4 = ((int64_t)(i >> 3) * a.nb + b) * 8 + (i & 7);
+      dst[i] = src[g4];
+    }
+    if (threadIdx.x == 0) g_u_lds[zslot] = 0.0f;
+  }
+  const int lane = threadIdx.x & 63;
+  const int4 wd = A.wdesc[blockIdx.x * (kLdsThreads / 64) + (threadIdx.x >> 6)];
+  const int32_t c0 = wd.x, c1 = wd.y;
+  const uint4* __restrict__ ch = A.chunk;
+  const uint32_t zz = (uint32_t)zslot | ((uint32_t)zslot << 16);
+  const int32_t last = max(c1 - 1, 0);
+  const __amdgpu_buffer_rsrc_t part = __builtin_amdgcn_make_buffer_rsrc(a.part, 0, A.n_part * 4, 0x00020000);
+  constexpr int W = 64 * K;  // chunks per window
+  uint4 q[D][K];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) q[i][j] = load_chunk(ch, c0 + W * i + K * lane + j, last);
+#pragma unroll
+    for (int j = 0; j < K + 1; ++j) __builtin_amdgcn_raw_buffer_store_b32(0u, part, 0x80000000u, 0, 0);  // loop's pattern
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();
+  const float* __restrict__ u = g_u_lds;
+  int32_t cur = wd.z - 1;
+  double carry = 0.0;
+  for (int32_t cw = c0; cw < c1; cw += W * D) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int32_t w0 = cw + W * i;
+      uint4 cq[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        cq[j] = mask_chunk(q[i][j], w0 + K * lane + j < c1, zz);
+        q[i][j] = load_chunk(ch, w0 + W * D + K * lane + j, last);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      lds3_window<K>(cq, u, part, lane, wd.z, cur, carry);
+    }
+  }
+  if (lane == 0 && cur >= wd.z) a.part[cur] = (float)carry;
 }
 
 __global__ __launch_bounds__(256) void combine_lds2_kernel(Lds2Args A) {
   const Lds1Args& a = A.e;
   const int32_t row = blockIdx.x * 256 + threadIdx.x;
   if (row >= a.n) return;
+  // 8 blocks at a time: all segment ids, then all partials, from clamped
+  // indices (no load behind a branch, so they overlap); fixed block order
   double acc = 0.0;
-  for (int b = 0; b < a.nb; ++b) {  // fixed block order
-    const int32_t p = A.pos[(int64_t)b * a.n + row];
-    if (p >= 0) acc += (double)a.part[p];
+  for (int b0 = 0; b0 < a.nb; b0 += 8) {
+    int32_t p[8];
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = A.pos[(int64_t)min(b0 + j, a.nb - 1) * a.n + row];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = a.part[max(p[j], 0)];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += (b0 + j < a.nb && p[j] >= 0) ? (double)v[j] : 0.0;
   }
   lds1_epilogue(a, row, acc);
 }
@@ -410,10 +615,32 @@ int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cn
   constexpr int kW = kLdsThreads / 64;
   int n_wg = L->tune.lds_wg > 0 ? L->tune.lds_wg : n_cus(L->device);
   n_wg = (int)std::max<int64_t>(nb, std::min<int64_t>(n_wg, ceil_div(chunks + p->n_pairs, 256)));
+  // workgroups per block in proportion to the block's cost (the hub columns
+  // make block 0 the heaviest), at least one each, largest remainders first
+  std::vector<int64_t> bcost(nb);
+  int64_t all = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    bcost[b] = (seg_chunk[bseg[b + 1]] - seg_chunk[bseg[b]]) + (bseg[b + 1] - bseg[b]);
+    all += bcost[b];
+  }
+  std::vector<int> mb(nb, 1);
+  {
+    int left = n_wg - (int)nb;
+    std::vector<std::pair<double, int64_t>> rem;
+    for (int64_t b = 0; b < nb && all > 0; ++b) {
+      const double want = (double)n_wg * bcost[b] / all - 1.0;
+      const int extra = std::max(0, std::min(left, (int)want));
+      mb[b] += extra;
+      left -= extra;
+      rem.push_back({want - extra, b});
+    }
+    std::sort(rem.begin(), rem.end(), [](auto& x, auto& y) { return x.first > y.first; });
+    for (size_t i = 0; left > 0 && i < rem.size(); ++i, --left) ++mb[rem[i].second];
+  }
   std::vector<int4> wd;
   std::vector<int32_t> wb;
   for (int64_t b = 0; b < nb; ++b) {
-    const int m = (int)(n_wg / nb + (b < n_wg % nb ? 1 : 0));
+    const int m = mb[b];
     const int64_t s0 = bseg[b], s1 = bseg[b + 1];
     const int64_t tot = (seg_chunk[s1] - seg_chunk[s0]) + (s1 - s0);
     int64_t sg = s0;
@@ -453,6 +680,11 @@ int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cn
            (long long)n, p->n_cols, (long long)p->nnz, (long long)nb, p->lchunks * 32, p->n_pairs, (long long)chunks,
            p->nnz ? 100.0 * (8.0 * chunks - p->nnz) / p->nnz : 0.0, p->n_wg);
   p->text = buf;
+  for (int64_t b = 0; b < nb; ++b) {
+    snprintf(buf, sizeof(buf), "  block %lld: cost %lld (%.1f%%) workgroups %d\n", (long long)b, (long long)bcost[b],
+             all ? 100.0 * bcost[b] / all : 0.0, mb[b]);
+    p->text += buf;
+  }
   return WG_OK;
 }
 }  // namespace
@@ -664,8 +896,21 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
     A.wdesc = p->wdesc;
     A.wblock = p->wblock;
     A.pos = p->pos;
+    A.n_part = p->n_pairs;
     A.e = a;
-    if (depth == 8)
+    const int kpl = L->tune.lds_k;
+    if (kpl == 2 || kpl == 4) {
+      const void* fn3 = kpl == 4 ? (const void*)cheb_lds3_kernel<4> : (const void*)cheb_lds3_kernel<2>;
+      static bool attr3[2] = {false, false};
+      if (!attr3[kpl == 4]) {
+        WG_HIP_TRY(hipFuncSetAttribute(fn3, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
+        attr3[kpl == 4] = true;
+      }
+      if (kpl == 4)
+        hipLaunchKernelGGL(cheb_lds3_kernel<4>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);
+      else
+        hipLaunchKernelGGL(cheb_lds3_kernel<2>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);
+    } else if (depth == 8)
       hipLaunchKernelGGL(cheb_lds2_kernel<8>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);
     else if (depth == 4)
       hipLaunchKernelGGL(cheb_lds2_kernel<4>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);

@@ -64,6 +64,10 @@ SIGNATURES = {
     "wg_row_l1_normalize": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp]),
     "wg_laplacian_map_rows": (ctypes.c_int, [c_vp, c_i32, c_vp, c_i64, c_vp, c_vp]),
     "wg_gather_rows": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "wg_cheb_u_len": (ctypes.c_int, [c_vp, ctypes.POINTER(c_i64)]),
+    "wg_scale_dinv": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "wg_lds_plan_info": (ctypes.c_int, [c_vp, c_i32, ctypes.POINTER(c_i64)]),
+    "wg_cheb_step_u": (ctypes.c_int, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_vp]),
 }
 
 _lib = None

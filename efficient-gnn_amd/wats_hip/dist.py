@@ -242,6 +242,45 @@ class ShardedWavelet:
                     launches=st["launches"])
 
     # -------------------------------------------------------------- chain
+    def u_len(self) -> int:
+        """Length of the F == 1 LDS kernel's gather vector u (0: kernel not applicable)."""
+        if not hasattr(self, "_u_len"):
+            n = ctypes.c_int64(0)
+            with torch.cuda.device(self.device):
+                check(_lib.load().wg_cheb_u_len(self.L.handle, ctypes.byref(n)), "cheb_u_len")
+            self._u_len = int(n.value)
+        return self._u_len
+
+    def _wavelet_features_u(self, X: torch.Tensor, k: int, s: float):
+        """F == 1, unweighted: the column-blocked LDS kernel; the per-step halo
+        exchange carries u = T_{k-1} * dinv (what the kernel gathers)."""
+        import math
+        p, L, lib = self.plan, self.L, _lib.load()
+        ulen = self.u_len()
+        U = (self._buf("U0", ulen, 1), self._buf("U1", ulen, 1))
+        T = (self._buf("A", p.n_own, 1), self._buf("B", p.n_own, 1))
+        S = self._buf("S", p.n_own, 1)
+        with torch.cuda.device(self.device):
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            check(lib.wg_permute_rows(L.handle, 0, 1, ptr(X), ptr(T[0]), st), "permute_rows")
+            check(lib.wg_scale_dinv(L.handle, ptr(T[0]), ptr(U[0]), st), "scale_dinv")
+        for i in range(1, k + 1):
+            cur_u, nxt_u = U[(i - 1) % 2], U[i % 2]
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if (self.profile and p.world > 1) else None
+            if ev:
+                ev[0].record()
+            self._halo_exchange(cur_u[: p.n_cols])
+            if ev:
+                ev[1].record()
+                self.events.append(ev)
+            with torch.cuda.device(self.device):
+                st = torch.cuda.current_stream(self.device).cuda_stream
+                check(lib.wg_cheb_step_u(L.handle, i, ptr(cur_u), ptr(T[(i - 1) % 2]),
+                                         None if i == 1 else ptr(T[i % 2]), None if i == k else ptr(T[i % 2]),
+                                         None if i == k else ptr(nxt_u), ptr(S), 1.0, math.exp(-s * i), st),
+                      "cheb_step_u")
+        return S
+
     def wavelet_features(self, X0_local: torch.Tensor, k: int = 3, s: float = 0.8):
         """Owned rows of (H, S) for signal rows X0_local (caller order)."""
         import math
@@ -249,6 +288,11 @@ class ShardedWavelet:
         L = self.L
         X = X0_local.to(self.device, torch.float32).reshape(p.n_own, -1).contiguous()
         F = X.shape[1]
+        if F == 1 and k >= 1 and p.n_own and self.u_len() > 0:
+            S = self._wavelet_features_u(X, k, s)
+            from .wavelet import row_l1_normalize
+            H_int = row_l1_normalize(S)
+            return L.permute(H_int, to_internal=False), L.permute(S, to_internal=False)
         A = self._buf("A", p.n_cols, F)
         B = self._buf("B", p.n_cols, F)
         S = self._buf("S", p.n_own, F)

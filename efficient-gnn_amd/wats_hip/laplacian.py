@@ -199,6 +199,16 @@ class NormalizedLaplacian:
         for k, v in knobs.items():
             check(_lib.load().wg_laplacian_tune(self.handle, k.encode(), int(v)), f"tune {k}")
 
+    def lds_plan_info(self, active_only: bool = True) -> dict | None:
+        """Shape of the F == 1 LDS kernel's plan (None when it does not apply)."""
+        out = (ctypes.c_int64 * 8)()
+        with torch.cuda.device(self.device):
+            check(_lib.load().wg_lds_plan_info(self.handle, 1 if active_only else 0, out), "lds_plan_info")
+        if out[0] == 0:
+            return None
+        keys = ("mode", "blocks", "rows", "cols", "nnz", "segments", "chunks", "workgroups")
+        return dict(zip(keys, [int(v) for v in out]))
+
     def describe(self, F: int = 1) -> str:
         """The step kernel's launch plan for an F-column signal."""
         return _lib.load().wg_laplacian_describe(self.handle, int(F)).decode()

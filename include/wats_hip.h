@@ -140,6 +140,32 @@ int wg_cheb_step(wg_laplacian_t L, int32_t k, int64_t F, const float* t_km1,
                  const float* t_km2, float* t_k, float* S, float* H,
                  double alpha0, double alpha_k, void* stream);
 
+/* F == 1 on an unweighted graph: the column-blocked LDS step kernel
+ * (csrc/lds1.hip) gathers u_{k-1} = T_{k-1} * dinv instead of T_{k-1}
+ * (dinv_j = 1 / sqrt(w_j), w_j = 0 -> 1), so a row-sharded caller exchanges
+ * halo rows of u.  Same recurrence as wg_cheb_step (calibration/WATS.py:32-36,
+ * heat sum WATS.py:65-68), internal row order.
+ * wg_cheb_u_len: *len = floats a u buffer must hold (n_cols rounded up to whole
+ *   column blocks; entries past n_cols are never used), or 0 when this kernel
+ *   does not apply (weighted graph, too many column blocks, "lds" tuned off).
+ *   Builds the plan (synchronous, once).
+ * wg_scale_dinv: u[i] = x[i] * dinv[i] for the handle's own rows i < n_rows.
+ * wg_cheb_step_u: u_km1 has wg_cheb_u_len floats (own rows then halo rows,
+ *   as t_km1 of wg_cheb_step); t_km1 / t_km2 / t_k are own rows only; u_k
+ *   (nullable) receives u_k for the own rows.  WG_ERR_UNSUPPORTED when
+ *   wg_cheb_u_len is 0. */
+int wg_cheb_u_len(wg_laplacian_t L, int64_t* len_host);
+/* Shape of the LDS kernel's plan (for byte accounting), or all zeros when it
+ * does not apply: out[0] mode (1 row teams, 2 chunk windows), [1] column
+ * blocks, [2] rows, [3] columns, [4] nonzeros, [5] non-empty (row, block)
+ * segments, [6] 16-B chunks (padded ids), [7] workgroups.  active_only = 1:
+ * the plan wg_wavelet_features uses (rows that enter the chain). */
+int wg_lds_plan_info(wg_laplacian_t L, int32_t active_only, int64_t* out8_host);
+int wg_scale_dinv(wg_laplacian_t L, const float* x, float* u, void* stream);
+int wg_cheb_step_u(wg_laplacian_t L, int32_t k, const float* u_km1, const float* t_km1,
+                   const float* t_km2, float* t_k, float* u_k, float* S, double alpha0,
+                   double alpha_k, void* stream);
+
 /* Row permutation between the caller's order and the internal order:
  * direction 0: dst[i_internal] = src[perm[i]]  (caller -> internal)
  * direction 1: dst[perm[i]] = src[i_internal]  (internal -> caller). */
