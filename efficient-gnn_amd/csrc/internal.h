@@ -166,6 +166,9 @@ struct wg_laplacian_s {
 };
 
 namespace wg {
+// prologue.hip
+int build_operator(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, const float* values,
+                   const float* w_cols, bool raw, hipStream_t stream);
 // step.hip
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out);

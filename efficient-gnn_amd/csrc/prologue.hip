@@ -31,7 +31,8 @@ namespace {
 __global__ __launch_bounds__(kBlock) void row_info_kernel(
     int64_t n_rows, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
     const float* __restrict__ values, int32_t* __restrict__ offdiag_len, double* __restrict__ rowsum,
-    float* __restrict__ diag, double* __restrict__ colsum, int32_t* __restrict__ colcnt, int32_t* __restrict__ nonunit) {
+    float* __restrict__ diag, double* __restrict__ colsum, int32_t* __restrict__ colcnt, int32_t* __restrict__ nonunit,
+    int raw) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n_rows) return;
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(kBlock) void row_info_kernel(
     const int32_t c = indices[e];
     const float v = values ? values[e] : 1.0f;
     rs += (double)v;
-    if (c == row) {
+    if (c == row && !raw) {
       dg += v;
     } else {
       ++cnt;
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void fill_lhat_kernel(
     int64_t n_rows, const int32_t* __restrict__ perm, const int32_t* __restrict__ iperm,
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, const float* __restrict__ values,
     const float* __restrict__ sw, const int32_t* __restrict__ rowptr, int32_t* __restrict__ col,
-    float* __restrict__ val) {
+    float* __restrict__ val, int raw) {
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= n_rows) return;
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void fill_lhat_kernel(
     bool keep = false;
     if (e < e1) {
       c = indices[e];
-      keep = (c != r);
+      keep = raw || (c != r);
     }
     const unsigned long long m = __ballot(keep);
     const int before = __popcll(m & ((1ull << lane) - 1ull));
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(kBlock) void fill_lhat_kernel(
       const float a = values ? values[e] : 1.0f;
       // scipy _laplacian.py:472-474: data /= w[row]; data /= w[col]; data *= -1
       col[pos + before] = (c < n_rows) ? iperm[c] : c;
-      val[pos + before] = -((a / swr) / sw[c]);
+      val[pos + before] = raw ? a : -((a / swr) / sw[c]);
     }
     pos += __popcll(m);
   }
@@ -306,8 +307,13 @@ struct Scratch {
   }
 };
 
-int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, const float* values, const float* w_cols,
-          hipStream_t stream) {
+}  // namespace
+
+// raw = false: L_hat of the adjacency (the Laplacian prologue).  raw = true: a
+// general CSR operator -- every entry kept with its given value, no isolated
+// diagonal, no closed-form rows (the row-normalised GCN adjacency, gcn.hip).
+int build_operator(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, const float* values,
+                   const float* w_cols, bool raw, hipStream_t stream) {
   const int64_t n_rows = L->n_rows, n_cols = L->n_cols, nnz = L->nnz_input;
   const int64_t nb_rows = std::max<int64_t>(1, ceil_div(n_rows, 256));
   const int64_t nb_cols = std::max<int64_t>(1, ceil_div(n_cols, 256));
@@ -342,7 +348,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   }
   if (n_rows > 0) {
     hipLaunchKernelGGL(row_info_kernel, dim3(ceil_div(n_rows, 4)), dim3(kBlock), 0, stream, n_rows, indptr, indices,
-                       values, len, rowsum64, diag, colsum64, colcnt, nonunit_d);
+                       values, len, rowsum64, diag, colsum64, colcnt, nonunit_d, raw ? 1 : 0);
     WG_LAUNCH_CHECK();
   }
   if (w_cols == nullptr && n_cols > 0) {
@@ -379,6 +385,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
     hipLaunchKernelGGL(degree_kernel, dim3(nb_cols), dim3(256), 0, stream, n_cols, n_rows, colsum32, diag, w_cols, sw,
                        iso_col);
     WG_LAUNCH_CHECK();
+    if (raw) WG_HIP_TRY(hipMemsetAsync(iso_col, 0, n_cols, stream));  // no diagonal term
   }
   if (n_rows == 0) {
     WG_HIP_TRY(hipMemsetAsync(L->rowptr, 0, sizeof(int32_t), stream));
@@ -391,7 +398,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   WG_LAUNCH_CHECK();
   if (L->reordered) {
     // closed-form rows only on a whole-graph handle (a shard's rows may be halo rows elsewhere)
-    const int allow_closed = (w_cols == nullptr) ? 1 : 0;
+    const int allow_closed = (w_cols == nullptr && !raw) ? 1 : 0;
     hipLaunchKernelGGL(sort_key_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, len, colcnt, iso_col, allow_closed,
                        key);
     WG_LAUNCH_CHECK();
@@ -431,7 +438,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   WG_HIP_TRY(hipMemsetAsync(L->col + L->nnz, 0, 4 * sizeof(int32_t), stream));
   WG_HIP_TRY(hipMemsetAsync(L->val + L->nnz, 0, 4 * sizeof(float), stream));
   hipLaunchKernelGGL(fill_lhat_kernel, dim3(ceil_div(n_rows, 4)), dim3(kBlock), 0, stream, n_rows, L->perm, L->iperm,
-                     indptr, indices, values, sw, L->rowptr, L->col, L->val);
+                     indptr, indices, values, sw, L->rowptr, L->col, L->val, raw ? 1 : 0);
   WG_LAUNCH_CHECK();
   WG_HIP_TRY(hipMemsetAsync(hist, 0, sizeof(unsigned int) * kBuckets, stream));
   hipLaunchKernelGGL(bucket_hist_kernel, dim3(std::min<int64_t>(nb_rows, 1024)), dim3(256), 0, stream, n_rows,
@@ -454,7 +461,7 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   }
   int32_t nonunit = 0;
   WG_HIP_TRY(hipMemcpy(&nonunit, nonunit_d, sizeof(int32_t), hipMemcpyDeviceToHost));
-  L->unit = (nonunit == 0);
+  L->unit = (nonunit == 0) && !raw;
   int64_t niso = 0;
   for (auto v : isoh) niso += v;
   L->n_iso = niso;
@@ -464,7 +471,6 @@ int build(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, cons
   return WG_OK;
 }
 
-}  // namespace
 }  // namespace wg
 
 using namespace wg;
@@ -540,7 +546,7 @@ int wg_laplacian_create(int64_t n_rows, int64_t n_cols, int64_t nnz, const int64
   L->n_cols = n_cols;
   L->nnz_input = nnz;
   L->reordered = !(flags & WG_FLAG_NO_REORDER);
-  const int rc = build(L, indptr, indices, values, w_cols, as_stream(stream_));
+  const int rc = build_operator(L, indptr, indices, values, w_cols, /*raw=*/false, as_stream(stream_));
   if (rc != WG_OK) {
     (void)hipStreamSynchronize(as_stream(stream_));
     delete L;

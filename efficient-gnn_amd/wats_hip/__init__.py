@@ -7,6 +7,8 @@ gfx950 HIP kernels behind a C ABI (``include/wats_hip.h``).
 Public surface (reference names):
     compute_normalized_laplacian, chebyshev_polynomials, graph_wavelet_features,
     WATS  (calibrator), NormalizedLaplacian (device L_hat handle).
+Section 8(f): SparseCompatibleGCN / RowNormalizedAdjacency (the base model's
+propagation as a HIP SpMM), metrics (device ECE).
 """
 from ._lib import LIB_PATH, WaveletError  # noqa: F401
 from .graphgen import CSRGraph, named_graph, rmat_graph  # noqa: F401
@@ -20,5 +22,6 @@ from .wavelet import (  # noqa: F401
     row_l1_normalize,
 )
 from .WATS import WATS, accuracy  # noqa: F401
+from .gcn import RowNormalizedAdjacency, SparseCompatibleGCN, propagate  # noqa: F401
 
 __version__ = "0.1.0"

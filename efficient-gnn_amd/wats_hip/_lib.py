@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("WATS_HIP_LIB") or os.path.join(_HERE, "libwats_hip.so
 
 WG_FLAG_NONE = 0
 WG_FLAG_NO_REORDER = 1
+WG_FLAG_TRANSPOSE = 2
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
@@ -68,6 +69,8 @@ SIGNATURES = {
     "wg_scale_dinv": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
     "wg_lds_plan_info": (ctypes.c_int, [c_vp, c_i32, ctypes.POINTER(c_i64)]),
     "wg_cheb_step_u": (ctypes.c_int, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_vp]),
+    "wg_rownorm_create": (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_vp, ctypes.POINTER(c_vp)]),
+    "wg_spmm": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

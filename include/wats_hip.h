@@ -42,6 +42,7 @@ enum wg_status {
 /* creation flags */
 #define WG_FLAG_NONE 0u
 #define WG_FLAG_NO_REORDER 1u   /* keep the caller's row order (no degree relabelling) */
+#define WG_FLAG_TRANSPOSE 2u    /* wg_rownorm_create: build adj_norm^T instead of adj_norm */
 
 typedef struct wg_laplacian_s* wg_laplacian_t;
 
@@ -212,6 +213,21 @@ int wg_laplacian_map_rows(wg_laplacian_t L, int32_t direction, const int32_t* ro
 /* Multi-GPU halo pack: dst[i] = src[rows[i]] for i < n (row stride F). */
 int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, float* dst,
                    void* stream);
+
+/* -------------------------------------------------------------------------
+ * Section 8(f)-2: the base model's propagation.  CompatibleGCN.forward
+ * (reference src/gnn/model.py:43-52) computes deg = adj.sum(dim=1),
+ * deg[deg == 0] = 1, adj_norm = adj / deg and twice x -> adj_norm @ x with a
+ * dense (N,N) torch.mm.  wg_rownorm_create builds adj_norm (every stored
+ * entry, self loops included, value a_ij / deg_i in float32) from the CSR
+ * rows of adj (square, n x n; values NULL = all ones) as a handle of the same
+ * step kernel; WG_FLAG_TRANSPOSE builds adj_norm^T (the backward operator).
+ * wg_spmm: y = op @ x for x, y (n, F) row-major in the caller's order, sums in
+ * float64.  Handles are freed with wg_laplacian_destroy.  Create is synchronous.
+ * ---------------------------------------------------------------------- */
+int wg_rownorm_create(int64_t n, int64_t nnz, const int64_t* indptr, const int32_t* indices,
+                      const float* values, uint32_t flags, void* stream, wg_laplacian_t* out);
+int wg_spmm(wg_laplacian_t op, int64_t F, const float* x, float* y, void* stream);
 
 #ifdef __cplusplus
 }

@@ -350,3 +350,75 @@ def test_lds1_arxiv_f1_vs_oracle():
     H, S = wats_hip.graph_wavelet_features(L, k=16, return_S=True)
     assert_parity(_np(S), ref["S"], what="arxiv F=1 S")
     assert_parity(_np(H), ref["H"], what="arxiv F=1 H")
+
+
+# ----------------------------------------------------------------- 8(f)-2: base-model propagation
+def _dense_norm(A):
+    adj = torch.tensor(A.toarray(), dtype=torch.float32, device="cuda")
+    deg = adj.sum(dim=1, keepdim=True)
+    deg[deg == 0] = 1
+    return adj, adj / deg
+
+
+@pytest.mark.parametrize("F", [1, 7, 64, 130, 500])
+@pytest.mark.parametrize("kind", ["weighted_directed", "rmat"])
+def test_rownorm_spmm_forward_backward_vs_dense_torch(F, kind):
+    """adj_norm @ x (reference src/gnn/model.py:43-47) and its x-gradient
+    against the dense torch fp32 product; rel tolerance 1e-5 of max|ref|."""
+    if kind == "rmat":
+        g = rmat_graph(3000, 30000, seed=F)
+    else:
+        g = random_graph(900, 0.01, seed=F, directed=True, weighted=True, self_loop_frac=0.1, isolated_frac=0.05)
+    A = g.to_scipy()
+    adj, norm = _dense_norm(A)
+    op = wats_hip.RowNormalizedAdjacency.from_dense(adj)
+    x = torch.randn(g.n, F, device="cuda", generator=torch.Generator("cuda").manual_seed(F), requires_grad=True)
+    y = wats_hip.propagate(op, x)
+    ref = norm.double() @ x.detach().double()
+    assert_parity(_np(y), _np(ref), what=f"spmm F={F}")
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    gref = norm.double().t() @ gy.double()
+    assert_parity(_np(x.grad), _np(gref), what=f"spmm grad F={F}")
+
+
+def test_sparse_gcn_matches_dense_compatible_gcn():
+    """SparseCompatibleGCN == the reference CompatibleGCN (same weights, eval mode):
+    logits and parameter gradients."""
+    from models import CompatibleGCN
+    g = rmat_graph(2708, 10556, seed=3)
+    adj, _ = _dense_norm(g.to_scipy() + __import__("scipy").sparse.eye(g.n))
+    torch.manual_seed(0)
+    x = torch.randn(g.n, 300, device="cuda")
+    ref = CompatibleGCN(300, 7, nhid=64).cuda().eval()
+    sp_model = wats_hip.SparseCompatibleGCN(300, nclass=7, nhid=64).cuda().eval()
+    sp_model.load_state_dict(ref.state_dict())
+    out_ref, out = ref(x, adj), sp_model(x, adj)
+    assert_parity(_np(out), _np(out_ref).astype(np.float64), tol=1e-5, what="gcn logits")
+    out_ref.square().sum().backward()
+    out.square().sum().backward()
+    for (n1, p1), (n2, p2) in zip(ref.named_parameters(), sp_model.named_parameters()):
+        assert_parity(_np(p2.grad), _np(p1.grad).astype(np.float64), tol=1e-4, what=f"grad {n1}")
+    with pytest.raises(NotImplementedError):
+        sp_model(x, adj.clone().requires_grad_(True))
+
+
+def test_wats_with_sparse_base_model_matches_reference_fixture():
+    """The WATS drop-in over SparseCompatibleGCN reproduces the reference
+    WATS.forward fixture (same head and base weights)."""
+    d = load_golden("wats_forward120")
+    n, nfeat = d["x"].shape
+    ncls = d["base.gc2.weight"].shape[0]
+    base = wats_hip.SparseCompatibleGCN(nfeat, nclass=ncls, nhid=d["base.gc1.weight"].shape[0])
+    base.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in d.items() if k.startswith("base.")})
+    base.eval()
+    for p in base.parameters():
+        p.requires_grad = False
+    x, y = torch.from_numpy(d["x"]), torch.from_numpy(d["y"])
+    adj, val = torch.from_numpy(d["adj"]), torch.from_numpy(d["val_mask"])
+    w = wats_hip.WATS(base, x, y, adj, val, verbose=False)
+    w.net.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in d.items() if k.startswith("net.")})
+    w.eval()
+    with torch.no_grad():
+        out = _np(w(x, adj))
+    np.testing.assert_allclose(out, d["out"], rtol=1e-5, atol=1e-5)

@@ -146,3 +146,21 @@ def test_ece_matches_reference_restatement(logits):
     assert abs(got - ref) < 1e-6
     for k in range(c):
         assert abs(M.calculate_ece(out, y, k, logits=logits) - E.calculate_ece(out, y, k, logits=logits)) < 1e-6
+
+
+def test_rownorm_create_rejects_bad_shapes_without_gpu_work():
+    lib = _lib.load()
+    rc = lib.wg_rownorm_create(-1, 0, None, None, None, 0, None, ctypes.byref(ctypes.c_void_p()))
+    assert rc == -1 and b"bad shape" in lib.wg_last_error()
+    rc = lib.wg_spmm(None, 1, None, None, None)
+    assert rc == -1
+
+
+def test_sparse_gcn_state_dict_matches_reference_layout():
+    """SparseCompatibleGCN keeps CompatibleGCN's parameter names (src/gnn/model.py:33-35)."""
+    from models import CompatibleGCN
+    a = CompatibleGCN(12, 5, nhid=8)
+    b = wats_hip.SparseCompatibleGCN(12, nclass=5, nhid=8)
+    assert set(a.state_dict()) == set(b.state_dict())
+    b.load_state_dict(a.state_dict())
+    assert wats_hip.SparseCompatibleGCN(4, dataset_name="ogbn-arxiv").gc2.out_features == 40
