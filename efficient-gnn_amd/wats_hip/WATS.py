@@ -14,7 +14,9 @@ Differences: the features are computed on the GPU from the dense ``adj``
 (no ``adj.cpu().numpy()`` round trip, WATS.py:99); keyword-only extras
 ``k``/``s`` (defaults 3 / 0.8 as hard-coded at WATS.py:99), ``X0`` (signal),
 ``graph`` (a sparse graph to use instead of the dense ``adj`` for the
-features), ``wavelet_feats`` (precomputed features, e.g. a cache) and
+features), ``wavelet_feats`` (precomputed features, e.g. a cache),
+``fused_head`` (default on: the temperature head + log_softmax as the fused
+HIP kernels of ``head.py``; off: the reference's torch ops) and
 ``verbose``; ``fit()`` is an alias of ``calib_train``.
 """
 from __future__ import annotations
@@ -41,8 +43,9 @@ def accuracy(outputs: torch.Tensor, labels: torch.Tensor) -> float:
 
 class WATS(torch.nn.Module):
     def __init__(self, base_model, features, labels, adj, val_mask, *, k: int = 3, s: float = 0.8, X0=None,
-                 graph=None, wavelet_feats=None, verbose: bool = True):
+                 graph=None, wavelet_feats=None, verbose: bool = True, fused_head: bool = True):
         super().__init__()
+        self.fused_head = bool(fused_head) and torch.cuda.is_available()
         # WATS.py:91 picks cuda when available; the HIP feature path requires it.
         self.device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
         self.base_model = base_model.to(self.device)
@@ -78,6 +81,9 @@ class WATS(torch.nn.Module):
     def forward(self, x, adj):
         """WATS.py:112-130."""
         x, adj = x.to(self.device), adj.to(self.device)
+        if self.fused_head:
+            from .head import wats_head
+            return wats_head(self.wavelet_feats, self.base_model(x, adj), self.net)
         temperatures = self.temperatures()
         logits = self.base_model(x, adj)
         calibrated_logits = logits / temperatures.unsqueeze(1)

@@ -23,5 +23,6 @@ from .wavelet import (  # noqa: F401
 )
 from .WATS import WATS, accuracy  # noqa: F401
 from .gcn import RowNormalizedAdjacency, SparseCompatibleGCN, propagate  # noqa: F401
+from .head import wats_head  # noqa: F401
 
 __version__ = "0.1.0"

@@ -229,6 +229,27 @@ int wg_rownorm_create(int64_t n, int64_t nnz, const int64_t* indptr, const int32
                       const float* values, uint32_t flags, void* stream, wg_laplacian_t* out);
 int wg_spmm(wg_laplacian_t op, int64_t F, const float* x, float* y, void* stream);
 
+/* -------------------------------------------------------------------------
+ * Section 8(f)-3: the WATS temperature head, fused.  Reference
+ * calibration/WATS.py:101-105 (net = Linear(F,16) - ReLU - Linear(16,1)) and
+ * :124-130 (T = log(exp(net(H)) + 1.1); out = log_softmax(logits / T)).
+ * H (n,F), logits (n,C), out (n,C) row-major; W1 [hid][F], b1 [hid], W2 [hid]
+ * (Linear(hid,1).weight), b2 [1] (torch nn.Linear layout); hid <= 64.
+ * forward: out, and t_save[n] = net(H) (nullable; speeds up the backward).
+ * backward: from grad_out (n,C): grad_logits (nullable) and the parameter
+ * gradients gW1 [hid][F], gb1, gW2, gb2 (overwritten, not accumulated), float64
+ * sums in a fixed order; `workspace` holds wg_wats_head_workspace bytes.
+ * ---------------------------------------------------------------------- */
+int wg_wats_head_forward(int64_t n, int64_t F, int64_t C, int32_t hid, const float* H,
+                         const float* logits, const float* W1, const float* b1, const float* W2,
+                         const float* b2, float* out, float* t_save, void* stream);
+int wg_wats_head_workspace(int64_t n, int64_t F, int32_t hid, int64_t* bytes_host);
+int wg_wats_head_backward(int64_t n, int64_t F, int64_t C, int32_t hid, const float* H,
+                          const float* logits, const float* W1, const float* b1, const float* W2,
+                          const float* b2, const float* out, const float* t_save,
+                          const float* grad_out, float* grad_logits, float* gW1, float* gb1,
+                          float* gW2, float* gb2, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -422,3 +422,55 @@ def test_wats_with_sparse_base_model_matches_reference_fixture():
     with torch.no_grad():
         out = _np(w(x, adj))
     np.testing.assert_allclose(out, d["out"], rtol=1e-5, atol=1e-5)
+
+
+# ----------------------------------------------------------------- 8(f)-3: fused temperature head
+@pytest.mark.parametrize("F,C,n", [(1, 7, 2708), (1, 40, 5000), (40, 41, 3000), (3, 1, 17), (1, 130, 900)])
+def test_fused_head_forward_backward_vs_torch(F, C, n):
+    """wats_head == log_softmax(logits / log(exp(net(H)) + 1.1)) (WATS.py:124-130)
+    in torch fp32, forward and all gradients."""
+    from torch import nn
+    torch.manual_seed(F * 100 + C)
+    net = nn.Sequential(nn.Linear(F, 16), nn.ReLU(), nn.Linear(16, 1)).cuda()
+    H = torch.randn(n, F, device="cuda")
+    logits = (3 * torch.randn(n, C, device="cuda")).requires_grad_(True)
+    out = wats_hip.wats_head(H, logits, net)
+    t = net(H).squeeze(-1)
+    T = torch.log(torch.exp(t) + 1.1)
+    ref = torch.log_softmax(logits / T.unsqueeze(1), dim=1)
+    assert_parity(_np(out), _np(ref).astype(np.float64), what="head forward")
+    g = torch.randn_like(ref)
+    grads = torch.autograd.grad((out * g).sum(), [logits] + list(net.parameters()))
+    refg = torch.autograd.grad((ref * g).sum(), [logits] + list(net.parameters()))
+    for a, b, name in zip(grads, refg, ["logits", "W1", "b1", "W2", "b2"]):
+        assert_parity(_np(a).reshape(-1, 1), _np(b).reshape(-1, 1).astype(np.float64), tol=2e-5, what=f"d{name}")
+
+
+def test_fused_head_deterministic_and_wats_trains_with_it():
+    """Bitwise-reproducible backward; WATS calib_train with the fused head
+    reaches the same loss as with the reference torch ops."""
+    from models import CompatibleGCN
+    d = load_golden("wats_forward120")
+    n, nfeat = d["x"].shape
+    ncls = d["base.gc2.weight"].shape[0]
+    x, y = torch.from_numpy(d["x"]), torch.from_numpy(d["y"])
+    adj, val = torch.from_numpy(d["adj"]), torch.from_numpy(d["val_mask"])
+    outs = []
+    for fused in (True, False):
+        base = CompatibleGCN(nfeat, ncls, nhid=d["base.gc1.weight"].shape[0])
+        base.load_state_dict({k[5:]: torch.from_numpy(v) for k, v in d.items() if k.startswith("base.")})
+        base.eval()
+        torch.manual_seed(0)
+        w = wats_hip.WATS(base, x, y, adj, val, verbose=False, fused_head=fused)
+        w.eval()
+        with torch.no_grad():
+            outs.append(_np(w(x, adj)))
+    np.testing.assert_allclose(outs[0], outs[1], rtol=2e-4, atol=2e-4)
+    # determinism of the fused backward
+    from torch import nn
+    net = nn.Sequential(nn.Linear(1, 16), nn.ReLU(), nn.Linear(16, 1)).cuda()
+    H = torch.randn(10000, 1, device="cuda")
+    lg = torch.randn(10000, 7, device="cuda")
+    g1 = torch.autograd.grad(wats_hip.wats_head(H, lg, net).sum(), list(net.parameters()))
+    g2 = torch.autograd.grad(wats_hip.wats_head(H, lg, net).sum(), list(net.parameters()))
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
