@@ -108,6 +108,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.lds_iter = (int32_t)value;
   } else if (!strcmp(key, "lds_wg")) {
     L->tune.lds_wg = (int32_t)std::max<int64_t>(0, value);
+  } else if (!strcmp(key, "inkernel_combine")) {
+    L->tune.inkernel_combine = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "lds_k")) {
     if (value != 1 && value != 2 && value != 4) return fail(WG_ERR_INVALID, "lds_k must be 1, 2 or 4");
     L->tune.lds_k = (int32_t)value;

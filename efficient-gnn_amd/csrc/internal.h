@@ -74,6 +74,7 @@ struct Plan {
   ChunkDesc* chunks = nullptr;  // device [n_chunks]
   double* partial = nullptr;    // device [n_chunks][width]
   int2* rowchunks = nullptr;    // device [n_split] {first chunk, chunk count}
+  int32_t* arrivals = nullptr;  // device [n_split] monotonic arrival counters (in-kernel combine)
   std::string text;
   void release();
 };
@@ -120,6 +121,7 @@ struct Tuning {
   int32_t waves = 4;         // waves per step-kernel workgroup: 4, 8 or 16
   int32_t hot = 0;           // F == 1: LDS hot-column cache size (columns), 0 = off
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments
+  int32_t inkernel_combine = 1;  // split rows: last-arriving chunk combines (sc1 hand-off) vs combine_kernel
   int32_t lds = 2;           // F == 1, unit weights: column-blocked LDS kernel (0 = off, 1 = row teams, 2 = chunk windows)
   int32_t lds_cb = 32768;    // LDS floats per column block (multiple of 32, <= 40960)
   int32_t lds_iter = 8;      // target entries per lane per row team

@@ -47,6 +47,8 @@ struct StepArgs {
   double alpha_k;
   const ChunkDesc* chunks;
   double* partial;
+  const int2* rowchunks;  // split rows: {first chunk, chunk count}
+  int32_t* arrivals;      // split rows: in-kernel combine counters (nullable = combine_kernel)
   int64_t seg_mask;
   int32_t nt;
   int32_t bcast;
@@ -469,7 +471,39 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     } else {
       double* p = a.partial + (int64_t)cid * (LF * VEC) + t * VEC;
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) p[j] = acc[j];
+      for (int j = 0; j < VEC; ++j) {
+        if (a.arrivals) __hip_atomic_store(p + j, acc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+        else p[j] = acc[j];
+      }
+    }
+  }
+  if (seg.mode == 2 && a.arrivals) {
+    // In-kernel combine of a split row, fence-free (MI355X_MICROARCH.md, hand-off table row 1):
+    // the partials are sc1 (write-through) stores drained by every storing wave, then ONE
+    // agent-scope atomic per chunk; the workgroup whose add completes the row reads every
+    // chunk's partial with sc1 loads, in chunk order (deterministic), after a barrier.
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int2 rc = a.rowchunks[row];
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(a.arrivals + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = ((old + 1) % rc.y) == 0;  // monotonic counter: every rc.y-th arrival completes a step
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < LF) {
+      const int t = threadIdx.x;
+      EpiIn<VEC> in2;
+      epi_prefetch<VEC>(a, row, t, in2);
+      double sum[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) sum[j] = 0.0;
+      for (int q = 0; q < rc.y; ++q) {
+        const double* pp = a.partial + (int64_t)(rc.x + q) * (LF * VEC) + t * VEC;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) sum[j] += __hip_atomic_load(pp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      step_epilogue<VEC>(a, row, t, sum, in2, 0);
     }
   }
 }
@@ -676,7 +710,7 @@ int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
     else launch_main<VEC, 4>(plan, a, stream);
     WG_LAUNCH_CHECK();
   }
-  if (plan.n_split > 0 && ((a.seg_mask >> tab.n) & 1)) {
+  if (plan.n_split > 0 && !a.arrivals && ((a.seg_mask >> tab.n) & 1)) {
     const int G = 64 / a.LF;
     hipLaunchKernelGGL(combine_kernel<VEC>, dim3((unsigned)ceil_div(plan.n_split, 4 * G)), dim3(kBlock), 0, stream, a,
                        plan.n_split, plan.rowchunks);
@@ -702,6 +736,8 @@ void Plan::release() {
   (void)hipFree(chunks);
   (void)hipFree(partial);
   (void)hipFree(rowchunks);
+  (void)hipFree(arrivals);
+  arrivals = nullptr;
   chunks = nullptr;
   partial = nullptr;
   rowchunks = nullptr;
@@ -724,7 +760,7 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 void default_knobs(const Tuning& t, int G, int* iter, int* block_iter, int* chunk_iter) {
   const bool wide = G <= 16;
   *iter = t.iter > 0 ? t.iter : (wide ? 24 : 16);
-  *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 128 : 32);
+  *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
   *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? 32 : 16);
 }
 
@@ -803,6 +839,8 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
     int rc_ = dmalloc(&p.chunks, ch.size());
     if (!rc_) rc_ = dmalloc(&p.partial, ch.size() * (size_t)p.width);
     if (!rc_) rc_ = dmalloc(&p.rowchunks, rc.size());
+    if (!rc_) rc_ = dmalloc(&p.arrivals, rc.size());
+    if (!rc_ && hipMemset(p.arrivals, 0, sizeof(int32_t) * rc.size()) != hipSuccess) rc_ = WG_ERR_HIP;
     if (rc_) {
       p.release();
       return rc_;
@@ -907,6 +945,8 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.alpha_k = alpha_k;
     a.chunks = plan->chunks;
     a.partial = plan->partial;
+    a.rowchunks = plan->rowchunks;
+    a.arrivals = (L->tune.inkernel_combine && plan->n_split > 0) ? plan->arrivals : nullptr;
     a.seg_mask = L->tune.seg_mask;
     a.nt = L->tune.nt;
     a.bcast = L->tune.bcast;

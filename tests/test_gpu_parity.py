@@ -249,7 +249,9 @@ def test_wats_dropin_on_gpu_matches_reference():
 @pytest.mark.parametrize("knobs", [dict(bcast=0), dict(nt=0), dict(iter=2, block_iter=1, chunk_iter=1),
                                    dict(iter=64, block_iter=256, chunk_iter=256), dict(tile_f=8),
                                    dict(bcast=0, iter=4, block_iter=2, chunk_iter=2),
-                                   dict(waves=16, block_iter=4, chunk_iter=2), dict(waves=8, iter=4, block_iter=8)])
+                                   dict(waves=16, block_iter=4, chunk_iter=2), dict(waves=8, iter=4, block_iter=8),
+                                   dict(inkernel_combine=0, iter=2, block_iter=1, chunk_iter=1),
+                                   dict(inkernel_combine=1, iter=2, block_iter=1, chunk_iter=2, waves=8)])
 def test_tuning_knobs_preserve_results(knobs):
     _check_knobs(knobs, F=12)
 
@@ -275,7 +277,7 @@ def _check_knobs(knobs, F):
     H1, S1 = wats_hip.graph_wavelet_features(L, k=8, X0=torch.from_numpy(X), return_S=True)
     assert_parity(_np(S1), ref["S"], what=f"{knobs} S")
     assert_parity(_np(H1), ref["H"], what=f"{knobs} H")
-    if set(knobs) <= {"bcast", "nt"}:
+    if set(knobs) <= {"bcast", "nt", "inkernel_combine"}:
         assert torch.equal(S0, S1), "same plan must give bitwise-identical results"
 
 
@@ -474,3 +476,19 @@ def test_fused_head_deterministic_and_wats_trains_with_it():
     g1 = torch.autograd.grad(wats_hip.wats_head(H, lg, net).sum(), list(net.parameters()))
     g2 = torch.autograd.grad(wats_hip.wats_head(H, lg, net).sum(), list(net.parameters()))
     assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+
+
+def test_split_rows_inkernel_combine_bitwise_equals_combine_kernel():
+    """Hub rows split over workgroups: the in-kernel last-arriver combine (sc1
+    hand-off) sums the same partials in the same order as combine_kernel, so the
+    two are bitwise identical, and stable over repeated calls."""
+    g = named_graph("ogbn-arxiv")
+    X = torch.randn(g.n, 40, generator=torch.Generator().manual_seed(5))
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(chunk_iter=4, block_iter=8)  # many split rows
+    assert "split rows" in L.describe(40)
+    outs = []
+    for ink in (1, 0, 1):
+        L.tune(inkernel_combine=ink)
+        outs.append(wats_hip.graph_wavelet_features(L, k=16, X0=X, return_S=True)[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
