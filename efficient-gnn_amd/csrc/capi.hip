@@ -108,6 +108,12 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.lds_iter = (int32_t)value;
   } else if (!strcmp(key, "lds_wg")) {
     L->tune.lds_wg = (int32_t)std::max<int64_t>(0, value);
+  } else if (!strcmp(key, "hubf")) {
+    L->tune.hubf = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 4096));
+    return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "gbuf")) {
+    L->tune.gbuf = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "inkernel_combine")) {
     L->tune.inkernel_combine = value ? 1 : 0;
     return WG_OK;  // launch-time choice

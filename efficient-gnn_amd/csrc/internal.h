@@ -70,6 +70,7 @@ struct Plan {
   int32_t width = 0;            // LF * VEC doubles per partial
   int32_t nw = 4;               // waves per workgroup of the step kernel
   int32_t hot = 0;              // F == 1: columns [0, hot) of T_{k-1} staged in LDS (0 = off)
+  int32_t hubf = 0;             // F > 1: rows [0, hubf) of the gathered tile staged in LDS (0 = off)
   int32_t n_split = 0;          // split rows = internal rows [0, n_split)
   ChunkDesc* chunks = nullptr;  // device [n_chunks]
   double* partial = nullptr;    // device [n_chunks][width]
@@ -121,6 +122,8 @@ struct Tuning {
   int32_t waves = 4;         // waves per step-kernel workgroup: 4, 8 or 16
   int32_t hot = 0;           // F == 1: LDS hot-column cache size (columns), 0 = off
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments
+  int32_t gbuf = 0;          // F > 1: branch-free raw-buffer gathers (accumulate_bcast_buf); no gain measured
+  int32_t hubf = 0;          // F > 1: rows [0, hubf) of T_{k-1} staged in LDS by a persistent kernel (0 = off)
   int32_t inkernel_combine = 1;  // split rows: last-arriving chunk combines (sc1 hand-off) vs combine_kernel
   int32_t lds = 2;           // F == 1, unit weights: column-blocked LDS kernel (0 = off, 1 = row teams, 2 = chunk windows)
   int32_t lds_cb = 32768;    // LDS floats per column block (multiple of 32, <= 40960)

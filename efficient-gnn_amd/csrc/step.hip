@@ -53,6 +53,9 @@ struct StepArgs {
   int32_t nt;
   int32_t bcast;
   int32_t vidx;
+  int32_t gbuf;        // F > 1 bcast gathers as raw buffer loads (accumulate_bcast_buf)
+  int32_t hubf;        // F > 1, hub kernel: rows [0, hubf) of the tile from LDS
+  int64_t xm1_bytes;   // extent of T_{k-1} from xm1 (gbuf: < 2^31)
 };
 
 template <int VEC>
@@ -332,6 +335,80 @@ __device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, i
   }
 }
 
+// Branch-free form of accumulate_bcast (same elements, same order, so the same
+// sums bit for bit).  The gathers are raw buffer loads of T_{k-1}: a masked
+// slot gets an out-of-range offset, which the hardware answers with zeros and
+// no memory request.  The inner loop has a fixed trip count, and the next LF
+// (col, val) pairs are loaded from a clamped index while the current ones are
+// gathered.  With the loads behind branches (accumulate_bcast), the waitcnt
+// pass drains every in-flight gather (vmcnt(0)) at each batch of U.
+// xoff_f: this lane's column offset in floats (fs * VEC); rs spans T_{k-1}.
+// HUB: rows [0, a.hubf) of the gathered tile come from the LDS copy at
+// g_hub_lds ([hubf][W] floats, then W zeros): their global load gets the
+// dropped offset, every other column reads the LDS zero row; x = global + LDS.
+extern __shared__ float g_hub_lds[];
+
+template <int VEC, int U, bool HUB>
+__device__ __forceinline__ void accumulate_bcast_buf(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                                     __amdgpu_buffer_rsrc_t rs, uint32_t xoff_b,
+                                                     double (&acc)[VEC], int fs, int base) {
+  constexpr uint32_t kDrop = 0x80000000u;
+  const int LF = a.LF;
+  const uint32_t ldb = (uint32_t)a.ld * 4u;
+  if (e >= e1) return;
+  const int32_t n = (e1 - e + stride - 1) / stride;
+  int32_t idx = e + min(fs, n - 1) * stride;
+  int32_t myc = a.col[idx];
+  float myv = a.val[idx];
+  for (int32_t t0 = 0; t0 < n; t0 += LF) {
+    const int32_t cc = myc;
+    const float cv = myv;
+    idx = e + min(t0 + LF + fs, n - 1) * stride;  // next LF pairs (clamped: always a valid entry)
+    myc = a.col[idx];
+    myv = a.val[idx];
+    const int cnt = min(LF, n - t0);
+    for (int j = 0; j < LF; j += U) {
+      int32_t c[U];
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int src = base + min(j + u, LF - 1);  // stays inside the sub-group
+        c[u] = __shfl(cc, src, 64);
+        v[u] = __shfl(cv, src, 64);
+      }
+      float x[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool hub = HUB && c[u] < a.hubf;
+        const uint32_t off = (j + u < cnt && !hub) ? (uint32_t)c[u] * ldb + xoff_b : kDrop;
+        // the builtins return integer data: reinterpret the bits
+        if constexpr (VEC == 4) {
+          const f32x4 g = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+          x[u][0] = g[0]; x[u][1] = g[1]; x[u][2] = g[2]; x[u][3] = g[3];
+        } else if constexpr (VEC == 2) {
+          const f32x2 g = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+          x[u][0] = g[0]; x[u][1] = g[1];
+        } else {
+          x[u][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+        if constexpr (HUB) {
+          const int W = LF * VEC;
+          const int hrow = (j + u < cnt && hub) ? c[u] : a.hubf;  // row hubf = zeros
+          const float* hp = g_hub_lds + hrow * W + fs * VEC;
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) x[u][q] += hp[q];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double vv = (j + u < cnt) ? (double)v[u] : 0.0;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[q] = fma(vv, (double)x[u][q], acc[q]);
+      }
+    }
+  }
+}
+
 // F == 1: each lane takes 4 consecutive nonzeros with one 16-B int4 / float4
 // load of col / val (4x fewer index instructions through the texture-address
 // unit).  Chunks are 4-aligned in the CSR (arrays padded by 4 entries), lane
@@ -360,15 +437,24 @@ __device__ __forceinline__ void accumulate_vidx1(const StepArgs& a, int32_t e0, 
   }
 }
 
-template <int VEC, bool BCAST, bool HOT>
+template <int VEC, bool BCAST, bool HOT, bool HUB = false>
 __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
                                           const float* __restrict__ xb, double (&acc)[VEC], int32_t H, int fs,
                                           int base) {
   if constexpr (HOT && VEC == 1) {
     accumulate_hot1(a, e, e1, stride, xb, H, acc);
   } else if constexpr (BCAST) {
-    if (a.LF % 5 == 0) accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
-    else accumulate_bcast<VEC, 4>(a, e, e1, stride, xb, acc, fs, base);
+    if (HUB || a.gbuf) {  // T_{k-1} as a raw buffer: [xm1, xm1 + xm1_bytes), this lane's column offset from xb
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0, (int)a.xm1_bytes, 0x00020000);
+      const uint32_t xoff = (uint32_t)((xb - a.xm1) * 4);
+      if (a.LF % 5 == 0) accumulate_bcast_buf<VEC, 5, HUB>(a, e, e1, stride, rs, xoff, acc, fs, base);
+      else accumulate_bcast_buf<VEC, 4, HUB>(a, e, e1, stride, rs, xoff, acc, fs, base);
+    } else if (a.LF % 5 == 0) {
+      accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
+    } else {
+      accumulate_bcast<VEC, 4>(a, e, e1, stride, xb, acc, fs, base);
+    }
   } else {
     accumulate<VEC>(a, e, e1, stride, xb, acc);
   }
@@ -376,7 +462,7 @@ __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t 
 
 // One work unit of the plan (a group of team rows, a block row or a split
 // chunk) processed by one workgroup of NW waves.
-template <int VEC, bool BCAST, int NW, bool HOT>
+template <int VEC, bool BCAST, int NW, bool HOT, bool HUB = false>
 __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restrict__ segs, int nseg, int32_t unit,
                                           int32_t H) {
   __shared__ double red[NW * 64 * VEC];
@@ -409,9 +495,9 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
       if constexpr (VEC == 1 && !HOT) {
         if (a.vidx && LF == 1) accumulate_vidx1(a, e0, e1, ns, LN, a.xm1, acc);
-        else acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+        else acc_range<VEC, BCAST, HOT, HUB>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
       } else {
-        acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+        acc_range<VEC, BCAST, HOT, HUB>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
       }
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
@@ -446,10 +532,10 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       // neighbouring chunks never both take an aligned 4-group (masking keeps the bounds exact anyway)
       accumulate_vidx1(a, e0, e1, wave * G + sg, NW * G, a.xm1, acc);
     } else if (sg < G) {
-      acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+      acc_range<VEC, BCAST, HOT, HUB>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
     }
   } else if (sg < G) {
-    acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+    acc_range<VEC, BCAST, HOT, HUB>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
   }
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
@@ -522,6 +608,24 @@ __global__ __launch_bounds__(NW * 64) void cheb_step_hot_kernel(StepArgs a, cons
   __syncthreads();
   for (int32_t unit = blockIdx.x; unit < total_units; unit += gridDim.x) {
     unit_body<1, false, NW, true>(a, segs, nseg, unit, H);
+    __syncthreads();  // the block-mode LDS partials are reused by the next unit
+  }
+}
+
+// F > 1 persistent variant with the LDS hub: each workgroup stages rows
+// [0, hubf) of the gathered tile of T_{k-1} (plus a zero row) once, then walks
+// the plan's work units round-robin.
+template <int VEC, int NW>
+__global__ __launch_bounds__(NW * 64) void cheb_step_hub_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg,
+                                                                int32_t total_units) {
+  const int W = a.LF * VEC;
+  for (int32_t i = threadIdx.x; i < (a.hubf + 1) * W; i += NW * 64) {
+    const int32_t r = i / W, c = i - r * W;
+    g_hub_lds[i] = (r < a.hubf) ? a.xm1[(int64_t)r * a.ld + c] : 0.0f;
+  }
+  __syncthreads();
+  for (int32_t unit = blockIdx.x; unit < total_units; unit += gridDim.x) {
+    unit_body<VEC, true, NW, false, true>(a, segs, nseg, unit, 0);
     __syncthreads();  // the block-mode LDS partials are reused by the next unit
   }
 }
@@ -698,10 +802,40 @@ int launch_hot(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   return WG_OK;
 }
 
+template <int VEC, int NW>
+int launch_hub(const Plan& plan, const StepArgs& a, hipStream_t stream) {
+  static int n_cu = 0;
+  static bool attr_set = false;
+  if (!n_cu) {
+    int dev = 0;
+    WG_HIP_TRY(hipGetDevice(&dev));
+    WG_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  if (!attr_set) {
+    WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_step_hub_kernel<VEC, NW>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - NW * 64 * VEC * 8 - 64));
+    attr_set = true;
+  }
+  const size_t lds = (size_t)(a.hubf + 1) * a.LF * VEC * sizeof(float);
+  int per_cu = 0;  // resident workgroups per CU (registers and LDS): the persistent grid
+  WG_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)cheb_step_hub_kernel<VEC, NW>,
+                                                          NW * 64, lds));
+  const int grid = std::min<int>(plan.tab.total_blocks, n_cu * std::max(1, per_cu));
+  hipLaunchKernelGGL((cheb_step_hub_kernel<VEC, NW>), dim3(grid), dim3(NW * 64), lds, stream, a,
+                     (const Seg*)plan.d_segs, plan.tab.n, plan.tab.total_blocks);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
 template <int VEC>
 int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const SegTable& tab = plan.tab;
-  if (VEC == 1 && plan.hot > 0 && tab.total_blocks > 0) {
+  if (VEC == 4 && a.hubf > 0 && a.LF > 1 && a.bcast && tab.total_blocks > 0) {
+    int rc = plan.nw == 16 ? launch_hub<4, 16>(plan, a, stream)
+             : plan.nw == 8 ? launch_hub<4, 8>(plan, a, stream)
+                            : launch_hub<4, 4>(plan, a, stream);
+    if (rc) return rc;
+  } else if (VEC == 1 && plan.hot > 0 && tab.total_blocks > 0) {
     int rc = plan.nw == 16 ? launch_hot<16>(plan, a, stream) : launch_hot<4>(plan, a, stream);
     if (rc) return rc;
   } else if (tab.total_blocks > 0) {
@@ -951,6 +1085,14 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.nt = L->tune.nt;
     a.bcast = L->tune.bcast;
     a.vidx = L->tune.vidx;
+    a.xm1_bytes = (L->n_cols * F - f0) * (int64_t)sizeof(float);
+    a.gbuf = (L->tune.gbuf && a.xm1_bytes < ((int64_t)1 << 31)) ? 1 : 0;
+    // hub rows: LDS = (hubf + 1) * tile + the block-mode buffer (NW*64*VEC doubles) <= 160 KiB
+    a.hubf = (vec == 4 && a.xm1_bytes < ((int64_t)1 << 31))
+                 ? (int32_t)std::min<int64_t>({(int64_t)L->tune.hubf, L->n_cols,
+                                               (int64_t)((160 * 1024 - 64 - plan->nw * 64 * vec * 8) /
+                                                         (LF * vec * 4)) - 1})
+                 : 0;
     if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
     else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
     else rc = launch_step_vec<1>(*plan, a, stream);
