@@ -98,7 +98,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.seg_mask = value;
     return WG_OK;  // no replan
   } else if (!strcmp(key, "lds")) {
-    if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "lds must be 0, 1 or 2");
+    if (value < 0 || value > 3) return fail(WG_ERR_INVALID, "lds must be 0, 1, 2 or 3 (auto)");
     L->tune.lds = (int32_t)value;
   } else if (!strcmp(key, "lds_cb")) {
     if (value < 32 || value > 40704) return fail(WG_ERR_INVALID, "lds_cb must be in [32, 40704]");

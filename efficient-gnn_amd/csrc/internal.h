@@ -125,7 +125,7 @@ struct Tuning {
   int32_t gbuf = 0;          // F > 1: branch-free raw-buffer gathers (accumulate_bcast_buf); no gain measured
   int32_t hubf = 0;          // F > 1: rows [0, hubf) of T_{k-1} staged in LDS by a persistent kernel (0 = off)
   int32_t inkernel_combine = 1;  // split rows: last-arriving chunk combines (sc1 hand-off) vs combine_kernel
-  int32_t lds = 2;           // F == 1, unit weights: column-blocked LDS kernel (0 = off, 1 = row teams, 2 = chunk windows)
+  int32_t lds = 3;           // F == 1, unit weights: LDS kernel (0 = off, 1 = row teams, 2 = chunk windows, 3 = auto)
   int32_t lds_cb = 32768;    // LDS floats per column block (multiple of 32, <= 40960)
   int32_t lds_iter = 8;      // target entries per lane per row team
   int32_t lds_wg = 0;        // workgroups of the LDS kernel (0 = auto)

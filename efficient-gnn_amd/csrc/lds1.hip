@@ -726,8 +726,23 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
   if (!L->unit || !L->dinv || L->tune.lds == 0 || L->lds1_failed[slot]) return WG_OK;
   const int64_t n = active_only ? L->n_active : L->n_rows;
   const int64_t n_cols = active_only ? L->n_active : L->n_cols;
+  // mode: 1 row teams, 2 chunk windows; 3 = auto (measured, profiles/r01/s14): one column
+  // block -> teams (one launch, epilogue in place: PubMed 6.0 vs 6.8 us gather, 12.2
+  // windows); several blocks -> windows on long rows (avg >= 64 per row: Reddit 60 vs 588
+  // us), else the gather kernel (ogbn-arxiv F=1, avg 25: 12.5 vs 14.0 / 14.6 us)
+  int mode = L->tune.lds;
+  int32_t nnz_rows = 0;
+  if (n > 0) WG_HIP_TRY(hipMemcpy(&nnz_rows, L->rowptr + n, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (mode == 3) {
+    const int64_t nb1 = ceil_div(ceil_div(std::max<int64_t>(n_cols, 1), 32), 40704 / 32);
+    mode = (nb1 == 1) ? 1 : (n > 0 && nnz_rows / n >= 64) ? 2 : 0;
+  }
+  if (mode == 0) {
+    L->lds1_failed[slot] = true;
+    return WG_OK;
+  }
   // + static LDS <= 160 KiB; windows: 15-bit local ids and a zero slot at 32 * lchunks
-  const int cb = std::max(32, std::min(L->tune.lds == 2 ? 32736 : 40704, L->tune.lds_cb / 32 * 32));
+  const int cb = std::max(32, std::min(mode == 2 ? 32736 : 40704, L->tune.lds_cb / 32 * 32));
   const int64_t nchunks = ceil_div(std::max<int64_t>(n_cols, 1), 32);
   const int64_t nb = ceil_div(nchunks, cb / 32);
   if (n == 0 || nb > std::min(L->tune.lds_maxnb, 64)) {
@@ -757,7 +772,7 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
   // exclusive scan on the host (the plan is built once per graph; brp is small)
   std::vector<int32_t> h(ncnt);
   WG_HIP_TRY(hipMemcpy(h.data(), p->brp, sizeof(int32_t) * ncnt, hipMemcpyDeviceToHost));
-  if (L->tune.lds == 2) {
+  if (mode == 2) {
     rc = build_windows(L, p, h);
     if (rc) return bail(rc);
     L->lds1[slot] = p;

@@ -323,7 +323,7 @@ def test_lds1_directed_isolated_selfloops(seed):
     g = random_graph(3000, 0.004, seed=seed, directed=True, weighted=False, self_loop_frac=0.05, isolated_frac=0.05)
     A = g.to_scipy()
     L = NormalizedLaplacian.from_graph(g)
-    L.tune(lds_cb=512 if seed else 32768)
+    L.tune(lds=2 if seed else 3, lds_cb=512 if seed else 32768)  # auto picks row teams for one block
     assert "lds1:" in L.describe(1)
     X = np.random.default_rng(seed).standard_normal((g.n, 1)).astype(np.float32)
     ref = O.graph_wavelet_features(A, k=7, s=0.8, X0=X, return_all=True)
@@ -349,7 +349,9 @@ def test_lds1_arxiv_f1_vs_oracle():
     g = named_graph("ogbn-arxiv")
     A = g.to_scipy()
     L = NormalizedLaplacian.from_graph(g)
-    assert "lds1:" in L.describe(1)
+    assert "lds1:" not in L.describe(1)  # auto: 3 blocks, short rows -> the gather kernel
+    L.tune(lds=2)
+    assert "windows" in L.describe(1)
     ref = O.graph_wavelet_features(A, k=16, s=0.8, return_all=True)
     H, S = wats_hip.graph_wavelet_features(L, k=16, return_S=True)
     assert_parity(_np(S), ref["S"], what="arxiv F=1 S")
