@@ -108,6 +108,11 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.lds_iter = (int32_t)value;
   } else if (!strcmp(key, "lds_wg")) {
     L->tune.lds_wg = (int32_t)std::max<int64_t>(0, value);
+  } else if (!strcmp(key, "sortcols")) {
+    if (value) {
+      WG_HIP_TRY(hipDeviceSynchronize());
+      if (int rc = sort_row_columns(L, nullptr)) return rc;
+    }
   } else if (!strcmp(key, "hubf")) {
     L->tune.hubf = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 4096));
     return WG_OK;  // launch-time choice
@@ -126,6 +131,8 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "lds_maxnb")) {
     L->tune.lds_maxnb = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 64));
+  } else if (!strcmp(key, "lds_perm")) {
+    L->tune.lds_perm = value ? 1 : 0;
   } else {
     return fail(WG_ERR_INVALID, "wg_laplacian_tune: unknown key '%s'", key);
   }

@@ -170,6 +170,7 @@ int wg_rownorm_create(int64_t n, int64_t nnz, const int64_t* indptr, const int32
   L->nnz_input = nnz;
   L->reordered = !(flags & WG_FLAG_NO_REORDER);
   rc = build_operator(L, op_indptr, op_indices, op_values, nullptr, /*raw=*/true, stream);
+  if (rc == WG_OK && !(flags & WG_FLAG_KEEP_COLUMN_ORDER)) rc = sort_row_columns(L, stream);
   if (rc == WG_OK && hipStreamSynchronize(stream) != hipSuccess) rc = fail(WG_ERR_HIP, "wg_rownorm_create: sync");
   if (rc != WG_OK) {
     (void)hipStreamSynchronize(stream);

@@ -132,6 +132,7 @@ struct Tuning {
   int32_t lds_maxnb = 16;    // largest block count the LDS kernel takes (else the gather kernel)
   int32_t lds_depth = 2;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
   int32_t lds_k = 4;         // windows: chunks per lane (1 = cheb_lds2_kernel, 2 / 4 = cheb_lds3_kernel)
+  int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
 };
 
 }  // namespace wg
@@ -156,6 +157,7 @@ struct wg_laplacian_s {
   // unweighted graph (every off-diagonal a_ij == 1): L_hat_ij = -dinv_i dinv_j
   // up to scipy's float32 rounding, so the F == 1 LDS kernel reads no values
   bool unit = false;
+  bool cols_sorted = false;   // rows' entries in ascending internal column (sort_row_columns)
   double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
   bool lds1_failed[2] = {false, false};        // not applicable (too many blocks): use the gather kernel
@@ -174,6 +176,7 @@ namespace wg {
 // prologue.hip
 int build_operator(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indices, const float* values,
                    const float* w_cols, bool raw, hipStream_t stream);
+int sort_row_columns(wg_laplacian_s* L, hipStream_t stream);
 // step.hip
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out);

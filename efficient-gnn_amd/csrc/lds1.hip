@@ -531,7 +531,10 @@ __global__ __launch_bounds__(256) void combine_lds2_kernel(Lds2Args A) {
 // segment fill: wave per row; lane b owns the row's segment of block b
 // (start chunk cpt[b * n + r]); ids keep CSR order, pad ids -> zero slot,
 // bit 15 on the segment's first id
-__global__ __launch_bounds__(256) void lds2_fill_kernel(int32_t n, int32_t nb, int32_t zslot,
+// perm = 1: a segment's k entries are dealt column-major over its nch = ceil(k/8)
+// chunks (rank t -> chunk t % nch, slot t / nch), so one lane's chunks span
+// the whole (column-sorted) segment instead of one narrow column range.
+__global__ __launch_bounds__(256) void lds2_fill_kernel(int32_t n, int32_t nb, int32_t zslot, int32_t perm,
                                                        const int32_t* __restrict__ rowptr,
                                                        const int32_t* __restrict__ col, const int32_t* __restrict__ cpt,
                                                        const int32_t* __restrict__ cnt, uint16_t* __restrict__ ids) {
@@ -555,9 +558,14 @@ __global__ __launch_bounds__(256) void lds2_fill_kernel(int32_t n, int32_t nb, i
       const int64_t p0 = __shfl(mypos, bb, 64);
       const int64_t s0 = __shfl(start, bb, 64);
       if (blk == bb) {
-        const int64_t dst = p0 + __popcll(m & lt);
+        int64_t dst = p0 + __popcll(m & lt);
         uint32_t id = (uint32_t)((((c >> 5) / nb) << 5) | (c & 31));
         if (dst == s0) id |= 0x8000u;
+        if (perm) {
+          const int64_t rank = dst - s0;
+          const int64_t nch = ((int64_t)cnt[(int64_t)bb * n + r] + 7) / 8;
+          dst = s0 + (rank % nch) * 8 + rank / nch;
+        }
         ids[dst] = (uint16_t)id;
       }
       if (lane == bb) mypos += __popcll(m);
@@ -565,7 +573,9 @@ __global__ __launch_bounds__(256) void lds2_fill_kernel(int32_t n, int32_t nb, i
   }
   if (lane < nb) {
     const int32_t k = cnt[(int64_t)lane * n + r];
-    for (int64_t q = start + k; q < start + ((int64_t)k + 7) / 8 * 8; ++q) ids[q] = (uint16_t)zslot;
+    const int64_t nch = ((int64_t)k + 7) / 8;
+    for (int64_t q = 0; q < nch * 8; ++q)
+      if (perm ? ((q >> 3) + (q & 7) * nch >= k) : (q >= k)) ids[start + q] = (uint16_t)zslot;
   }
 }
 
@@ -669,7 +679,7 @@ int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cn
       hipMemcpy(p->wblock, wb.data(), sizeof(int32_t) * wb.size(), hipMemcpyHostToDevice) != hipSuccess)
     return done(fail(WG_ERR_HIP, "lds2 plan: upload failed"));
   hipLaunchKernelGGL(lds2_fill_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, 0, (int32_t)n, (int32_t)nb,
-                     p->lchunks * 32, L->rowptr, L->col, cpt_d, p->brp, reinterpret_cast<uint16_t*>(p->chunk));
+                     p->lchunks * 32, L->tune.lds_perm, L->rowptr, L->col, cpt_d, p->brp, reinterpret_cast<uint16_t*>(p->chunk));
   if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return done(fail(WG_ERR_HIP, "lds2 plan: fill failed"));
   done(0);

@@ -473,6 +473,45 @@ int build_operator(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indi
 
 }  // namespace wg
 
+namespace wg {
+// Each row's entries in ascending internal column id (values follow): rows of
+// a power-law graph then start with their hub columns, so neighbouring lanes
+// and iterations of the step kernel share cache lines.  Synchronous.
+int sort_row_columns(wg_laplacian_s* L, hipStream_t stream) {
+  const int64_t n = L->n_rows, nnz = L->nnz;
+  if (n == 0 || nnz == 0 || L->cols_sorted) {
+    L->cols_sorted = true;
+    return WG_OK;
+  }
+  int32_t* col2 = nullptr;
+  float* val2 = nullptr;
+  int rc = 0;
+  if ((rc = dmalloc(&col2, nnz + 4)) || (rc = dmalloc(&val2, nnz + 4))) {
+    (void)hipFree(col2);
+    return rc;
+  }
+  WG_HIP_TRY(hipMemsetAsync(col2 + nnz, 0, 4 * sizeof(int32_t), stream));
+  WG_HIP_TRY(hipMemsetAsync(val2 + nnz, 0, 4 * sizeof(float), stream));
+  int end_bit = 1;
+  while (end_bit < 32 && (1ll << end_bit) < L->n_cols) ++end_bit;
+  rc = cub_call(stream, [&](void* t, size_t& b) {
+    return hipcub::DeviceSegmentedRadixSort::SortPairs(t, b, L->col, col2, L->val, val2, (int)nnz, (int)n, L->rowptr,
+                                                       L->rowptr + 1, 0, end_bit, stream);
+  });
+  if (rc) {
+    (void)hipFree(col2);
+    (void)hipFree(val2);
+    return rc;
+  }
+  (void)hipFree(L->col);
+  (void)hipFree(L->val);
+  L->col = col2;
+  L->val = val2;
+  L->cols_sorted = true;
+  return WG_OK;
+}
+}  // namespace wg
+
 using namespace wg;
 
 wg_laplacian_s::~wg_laplacian_s() {
@@ -546,7 +585,8 @@ int wg_laplacian_create(int64_t n_rows, int64_t n_cols, int64_t nnz, const int64
   L->n_cols = n_cols;
   L->nnz_input = nnz;
   L->reordered = !(flags & WG_FLAG_NO_REORDER);
-  const int rc = build_operator(L, indptr, indices, values, w_cols, /*raw=*/false, as_stream(stream_));
+  int rc = build_operator(L, indptr, indices, values, w_cols, /*raw=*/false, as_stream(stream_));
+  if (rc == WG_OK && !(flags & WG_FLAG_KEEP_COLUMN_ORDER)) rc = sort_row_columns(L, as_stream(stream_));
   if (rc != WG_OK) {
     (void)hipStreamSynchronize(as_stream(stream_));
     delete L;
@@ -584,6 +624,29 @@ int wg_laplacian_export(wg_laplacian_t L, int64_t* indptr, int32_t* indices, flo
   hipLaunchKernelGGL(export_fill_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, stream, n, L->perm, L->iperm, L->rowptr,
                      L->col, L->val, indptr, indices, values);
   WG_LAUNCH_CHECK();
+  if (L->cols_sorted && L->nnz > 0) {
+    // rows were sorted by internal column: back to ascending caller column
+    int32_t* idx2 = nullptr;
+    float* val2 = nullptr;
+    if ((rc = dmalloc(&idx2, L->nnz)) || (rc = dmalloc(&val2, L->nnz))) {
+      (void)hipFree(idx2);
+      return rc;
+    }
+    int end_bit = 1;
+    while (end_bit < 32 && (1ll << end_bit) < L->n_cols) ++end_bit;
+    rc = cub_call(stream, [&](void* t, size_t& b) {
+      return hipcub::DeviceSegmentedRadixSort::SortPairs(t, b, indices, idx2, values, val2, (int)L->nnz, (int)n,
+                                                         indptr, indptr + 1, 0, end_bit, stream);
+    });
+    if (!rc) {
+      (void)hipMemcpyAsync(indices, idx2, sizeof(int32_t) * L->nnz, hipMemcpyDeviceToDevice, stream);
+      (void)hipMemcpyAsync(values, val2, sizeof(float) * L->nnz, hipMemcpyDeviceToDevice, stream);
+      rc = hipStreamSynchronize(stream) == hipSuccess ? WG_OK : fail(WG_ERR_HIP, "export: sync");
+    }
+    (void)hipFree(idx2);
+    (void)hipFree(val2);
+    if (rc) return rc;
+  }
   if (iso) {
     hipLaunchKernelGGL(export_iso_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, stream, n, L->iperm, L->iso, iso);
     WG_LAUNCH_CHECK();

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("WATS_HIP_LIB") or os.path.join(_HERE, "libwats_hip.so
 WG_FLAG_NONE = 0
 WG_FLAG_NO_REORDER = 1
 WG_FLAG_TRANSPOSE = 2
+WG_FLAG_KEEP_COLUMN_ORDER = 4
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32

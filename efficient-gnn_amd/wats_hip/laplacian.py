@@ -66,12 +66,14 @@ class NormalizedLaplacian:
     Build with :meth:`from_csr`, :meth:`from_dense`, :meth:`from_scipy` or
     :func:`compute_normalized_laplacian`.  For a row shard (multi-GPU) the
     columns are ``[owned rows | halo rows]`` and ``w_cols`` carries the global
-    column degrees (see ``wats_hip.dist``).
+    column degrees (see ``wats_hip.dist``).  ``sort_columns=False`` keeps
+    each row's entries in the caller's order (``WG_FLAG_KEEP_COLUMN_ORDER``)
+    instead of sorting them by internal column, which the gather kernels prefer.
     """
 
     def __init__(self, n_rows: int, indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor | None = None,
                  n_cols: int | None = None, w_cols: torch.Tensor | None = None, reorder: bool = True,
-                 device=None):
+                 sort_columns: bool = True, device=None):
         device = require_gpu(device if device is not None else (indptr.device if indptr.is_cuda else None))
         self.device = device
         n_cols = n_rows if n_cols is None else int(n_cols)
@@ -89,6 +91,8 @@ class NormalizedLaplacian:
         lib = _lib.load()
         handle = ctypes.c_void_p()
         flags = _lib.WG_FLAG_NONE if reorder else _lib.WG_FLAG_NO_REORDER
+        if not sort_columns:
+            flags |= _lib.WG_FLAG_KEEP_COLUMN_ORDER
         with torch.cuda.device(device):
             check(lib.wg_laplacian_create(n_rows, n_cols, nnz, ptr(indptr), ptr(indices) if nnz else None,
                                           ptr(values) if nnz else None, ptr(w_cols), flags,

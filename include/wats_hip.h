@@ -43,6 +43,9 @@ enum wg_status {
 #define WG_FLAG_NONE 0u
 #define WG_FLAG_NO_REORDER 1u   /* keep the caller's row order (no degree relabelling) */
 #define WG_FLAG_TRANSPOSE 2u    /* wg_rownorm_create: build adj_norm^T instead of adj_norm */
+#define WG_FLAG_KEEP_COLUMN_ORDER 4u /* keep each row's input entry order (default: ascending
+                                        internal column, which shares cache lines between
+                                        neighbouring gathers on power-law graphs) */
 
 typedef struct wg_laplacian_s* wg_laplacian_t;
 
@@ -114,7 +117,8 @@ int wg_laplacian_get_info(wg_laplacian_t L, wg_laplacian_info* info_host);
 
 /* Export L_hat in the CALLER's row/column numbering: the off-diagonal
  * entries as CSR (int64 indptr[n_rows+1], int32 indices / float32 values
- * sized info.nnz, the input's column order) plus iso[n_rows] (1 where
+ * sized info.nnz; each row in ascending column order, or in the input's
+ * order under WG_FLAG_KEEP_COLUMN_ORDER) plus iso[n_rows] (1 where
  * L_hat_ii = -1; nullable).  For bit-exact parity tests against scipy.  Async. */
 int wg_laplacian_export(wg_laplacian_t L, int64_t* indptr, int32_t* indices,
                         float* values, uint8_t* iso, void* stream);

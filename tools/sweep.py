@@ -53,6 +53,7 @@ def main():
                     help="knob grid, e.g. 'iter=16,24;chunk_iter=64,128;nt=0,7'")
     ap.add_argument("--segments", action="store_true")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--keep-order", action="store_true", help="WG_FLAG_KEEP_COLUMN_ORDER (no per-row column sort)")
     a = ap.parse_args()
     global REPS
     REPS = a.reps
@@ -63,11 +64,11 @@ def main():
     if nnz > 20_000_000:   # numpy generator too slow: same recipe on the GPU
         from wats_hip.graphgen import rmat_graph_device
         ip, ix = rmat_graph_device(n, nnz, seed=0)
-        L = wats_hip.NormalizedLaplacian(n, ip, ix)
+        L = wats_hip.NormalizedLaplacian(n, ip, ix, sort_columns=not a.keep_order)
         del ip, ix
     else:
         g = named_graph(a.config)
-        L = wats_hip.NormalizedLaplacian.from_graph(g)
+        L = wats_hip.NormalizedLaplacian.from_graph(g, sort_columns=not a.keep_order)
     X = torch.randn(L.n, F, device="cuda") if F > 1 else L.log1p_degree()
     n_act = L.n - int(L.info["n_closed_form"])
     bstep = 8 * L.nnz + 4 * (n_act + 1) + 20 * n_act * F
@@ -79,7 +80,7 @@ def main():
         first = first or knobs
         L.tune(seg_mask=-1, **knobs)
         r = time_chain(L, X, K)
-        r.update(config=a.config, F=F, K=K, GBs=bstep / (r["step_us"] * 1e-6) / 1e9, **knobs)
+        r.update(config=a.config, keep_order=a.keep_order, F=F, K=K, GBs=bstep / (r["step_us"] * 1e-6) / 1e9, **knobs)
         print(json.dumps(r), flush=True)
     if a.segments:
         L.tune(**first)
