@@ -65,6 +65,12 @@ def parse():
                     help="also measure this config row-sharded over all ranks (RCCL halo exchange) and attach it "
                          "as the 'sharded' object of the line; 'none' to skip")
     ap.add_argument("--sharded-steps", type=int, default=5)
+    ap.add_argument("--exchange", default="rccl", choices=["rccl", "nccl"],
+                    help="sharded halo exchange: native chain (rccl) or torch all_to_all_single per step (nccl)")
+    ap.add_argument("--cold-reps", type=int, default=5,
+                    help="chains timed after writing a 512 MiB scratch buffer (cold Infinity Cache / L2); 0 = skip")
+    ap.add_argument("--f1-companion", type=int, default=1,
+                    help="also time the same graph with the F=1 log1p-degree signal (SURVEY 8(d) 'also report F=1')")
     ap.add_argument("--mode", default="graphs", choices=["graphs", "sharded"],
                     help="graphs: one independent graph per rank (default); sharded: one graph row-sharded over all "
                          "ranks with a per-step RCCL halo exchange")
@@ -112,7 +118,7 @@ def cpu_baseline(g, K, F, s, X, seconds):
                        f"matvecs, {t_total:.1f} s")
 
 
-def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device):
+def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl"):
     """One graph (generated identically on every rank, on the GPU) split into
     nnz-balanced row blocks; per Chebyshev step one all_to_all_single halo
     exchange (RCCL) + the step kernel.  Strong scaling (fixed graph).
@@ -132,27 +138,32 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device):
     nnz_global = int(indptr[-1])
     del indptr_d, indices_d
     torch.cuda.empty_cache()
-    sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange="nccl", device=device)
+    sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device)
     if F == 1:
         X = sw.L.log1p_degree()
     else:
         g = torch.Generator(device=device)
         g.manual_seed(1 + rank)
         X = torch.randn(r1 - r0, F, generator=g, device=device)
-    for _ in range(warmup):
-        sw.wavelet_features(X, k=K, s=s_heat)
+    out = (torch.empty(r1 - r0, F, device=device), torch.empty(r1 - r0, F, device=device))
+    run = (lambda: sw.wavelet_features(X, k=K, s=s_heat, out=out)) if exchange == "rccl" else \
+        (lambda: sw.wavelet_features(X, k=K, s=s_heat))
+    for _ in range(max(2, warmup)):   # the native chain is captured into a hipGraph on its 2nd call
+        run()
     torch.cuda.synchronize(device)
-    sw.profile_start()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(steps):
-        sw.wavelet_features(X, k=K, s=s_heat)
+        run()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # kernel / exchange attribution: one more pass, eager, with HIP events (outside the timed region)
+    sw.profile_start()
+    run()
     prof = sw.profile_collect()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -183,7 +194,9 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device):
         "dtype": "f32",
         "data": "synthetic",
         "config": {"workload": f"{config}-size R-MAT (GPU generator, seed {seed}), one graph row-sharded over "
-                               f"{world} ranks, halo all_to_all_single (RCCL) per Chebyshev step; K={K} F={F}",
+                               f"{world} ranks, halo exchange per Chebyshev step "
+                               + ("(native: grouped ncclSend/ncclRecv, chain replayed as a hipGraph)"
+                                  if exchange == "rccl" else "(torch all_to_all_single, RCCL)") + f"; K={K} F={F}",
                    "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
                    "rank0_rows": p.n_own, "rank0_halo_rows": p.n_halo, "parallelism": f"rows x{world}"},
         "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
@@ -199,8 +212,72 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device):
     }
 
 
+def cold_chains(step, L, reps, device):
+    """SURVEY.md 8(d) 'cold' protocol: before each timed pass, write a 512 MiB
+    scratch buffer (evicts the 256 MiB Infinity Cache and every L2), then time
+    the pass alone (HIP events on the stream it runs on)."""
+    scratch = torch.empty(512 << 20, dtype=torch.uint8, device=device)
+    ms, launch_ms, launches = [], 0.0, 0
+    for _ in range(reps):
+        scratch.fill_(1)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        L.profile_enable(True)
+        a.record()
+        step()
+        b.record()
+        torch.cuda.synchronize(device)
+        p = L.profile_collect()
+        L.profile_enable(False)
+        ms.append(a.elapsed_time(b))
+        launch_ms += p["sum_ms"]
+        launches += p["launches"]
+    del scratch
+    torch.cuda.empty_cache()
+    ms.sort()
+    return {"reps": reps, "step_ms": ms[len(ms) // 2], "avg_launch_us": launch_ms / max(1, launches) * 1e3,
+            "protocol": "512 MiB scratch write before each pass; median pass time"}
+
+
+def f1_companion(lib, L, K, s_heat, steps, device):
+    """The same graph with the reference's own F = 1 signal log1p(rowsum)
+    (WATS.py:58-59): the kernel auto-selection's choice and its step time."""
+    import wats_hip
+    X = L.log1p_degree()
+    n = L.n
+    S = torch.empty(n, 1, dtype=torch.float32, device=device)
+    H = torch.empty(n, 1, dtype=torch.float32, device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def run():
+        wats_hip._lib.check(lib.wg_wavelet_features(L.handle, X.data_ptr(), 1, K, s_heat, S.data_ptr(),
+                                                    H.data_ptr(), stream), "wavelet_features")
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize(device)
+    L.profile_enable(True)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        run()
+    b.record()
+    torch.cuda.synchronize(device)
+    p = L.profile_collect()
+    L.profile_enable(False)
+    ms = a.elapsed_time(b) / steps
+    avg_ms = p["sum_ms"] / max(1, p["launches"])
+    n_active = n - int(L.info["n_closed_form"])
+    info = L.lds_plan_info(active_only=True)
+    b_step = lds_algorithmic_bytes(info) if info else algorithmic_bytes(n_active, L.nnz, 1)
+    return {"F": 1, "signal": "log1p(rowsum) (WATS.py:58-59)", "value": float(L.nnz) * K / (ms * 1e-3),
+            "unit": "edges*K/s", "ms_per_step": ms, "avg_launch_us": avg_ms * 1e3,
+            "kernel": ("cheb_lds3_kernel + combine_lds2_kernel" if info and info["mode"] == 2 else
+                       "cheb_lds1_kernel" if info else "cheb_step_kernel"),
+            "algorithmic_bytes_per_launch": b_step, "frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def sharded_main(args, world, rank, device):
-    line = run_sharded(args.config, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device)
+    line = run_sharded(args.config, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
+                       args.exchange)
     if rank == 0:
         js = json.dumps(line)
         print(js, flush=True)
@@ -260,8 +337,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    evs[0].record()
+    for i in range(args.steps):
         step()
+        evs[i + 1].record()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -269,6 +349,12 @@ def main():
     prof = L.profile_collect()
     L.profile_enable(False)
     elapsed = t1 - t0
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2] if step_ms else None
+    cold = cold_chains(step, L, args.cold_reps, device) if args.cold_reps > 0 else None
+    f1 = None
+    if args.f1_companion and F > 1:
+        f1 = f1_companion(lib, L, K, args.s, args.steps, device)
     edges_k = float(nnz) * K * args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -287,7 +373,7 @@ def main():
             del S, H
             torch.cuda.empty_cache()
             sharded = run_sharded(args.sharded_extra, None, None, args.sharded_steps, 1, args.seed, args.s, world,
-                                  rank, device)
+                                  rank, device, args.exchange)
         except Exception as exc:  # noqa: BLE001
             sharded = {"error": f"{type(exc).__name__}: {exc}"}
 
@@ -344,7 +430,16 @@ def main():
                 "launches": prof["launches"],
             },
             "chain_ms": prof["sum_ms"] / args.steps,
+            "median_step_ms": median_ms,
+            "edges_K_F_per_s": edges_k * F / elapsed,
         }
+        if cold is not None:
+            cold["edges_K_per_s"] = float(nnz) * K / (cold["step_ms"] * 1e-3)
+            cold["achieved_GBs"] = b_step / (cold["avg_launch_us"] * 1e-6) / 1e9
+            cold["frac"] = cold["achieved_GBs"] / HBM_PEAK_GBS
+            line["cold"] = cold
+        if f1 is not None:
+            line["f1_companion"] = f1
         if sharded is not None:
             line["sharded"] = sharded
         if world == 1 and not args.no_cpu_baseline:

@@ -75,6 +75,12 @@ SIGNATURES = {
     "wg_wats_head_forward": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32] + [c_vp] * 8 + [c_vp]),
     "wg_wats_head_workspace": (ctypes.c_int, [c_i64, c_i64, c_i32, ctypes.POINTER(c_i64)]),
     "wg_wats_head_backward": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32] + [c_vp] * 15 + [c_vp]),
+    "wg_dist_unique_id": (ctypes.c_int, [c_vp]),
+    "wg_dist_create": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, ctypes.POINTER(c_vp)]),
+    "wg_dist_destroy": (ctypes.c_int, [c_vp]),
+    "wg_dist_set_graph": (ctypes.c_int, [c_vp, c_i32]),
+    "wg_dist_wavelet_features": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_f64, c_vp, c_vp, c_vp]),
+    "wg_dist_profile_collect": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
 }
 
 _lib = None

@@ -6,9 +6,11 @@ into contiguous 1-D row blocks balanced by nonzeros.  Each rank owns the rows
 rows]``, with the halo rows grouped by owner rank.  Row i of ``T_k`` needs
 ``T_{k-1}`` at i's neighbours, plus ``T_{k-2}`` and ``S`` at row i only.  So the
 only exchange per Chebyshev step (reference ``calibration/WATS.py:35-36``) is
-the halo rows of ``T_{k-1}``.  That is one all-to-all-v, done with
-``torch.distributed.all_to_all_single``, which is RCCL over xGMI with the
-"nccl" backend.  The heat sum and the row-L1 normalisation are row-local.
+the halo rows of ``T_{k-1}``.  That is one all-to-all-v: grouped
+ncclSend/ncclRecv in native code (``csrc/dist.hip``, the default, the whole
+chain replayed as a hipGraph), or ``torch.distributed.all_to_all_single``
+(RCCL over xGMI with the "nccl" backend, or gloo on host copies in tests).
+The heat sum and the row-L1 normalisation are row-local.
 
 Setup also needs the Laplacian's column degree ``w = colsum(A) - diag(A)``
 (scipy ``_laplacian.py:467``).  It spans all shards, so it costs one
@@ -166,13 +168,17 @@ def halo_exchange(ext: torch.Tensor, plan: HaloPlan, pack, sendbuf: torch.Tensor
 class ShardedWavelet:
     """One rank's shard of ``L_hat`` on its GPU, plus the halo exchange.
 
-    ``exchange="nccl"``: all_to_all_single on device buffers (RCCL/xGMI).
-    ``exchange="host"``: the same collective on host copies (gloo) -- lets
-    several ranks share one GPU in tests; never used for timing.
+    ``exchange="rccl"`` (default): the whole chain in native code
+    (``wg_dist_*``, ``csrc/dist.hip``): its own RCCL communicator, grouped
+    ncclSend/ncclRecv per step, captured into a hipGraph and replayed.
+    ``exchange="nccl"``: the same exchange from Python, one
+    ``torch.distributed.all_to_all_single`` per step (RCCL/xGMI).
+    ``exchange="host"``: that collective on host copies (gloo) -- lets several
+    ranks share one GPU in tests (RCCL refuses two ranks on one device).
     """
 
     def __init__(self, indptr_local, indices_global, values_local, n_global: int, bounds, group=None,
-                 exchange: str = "nccl", device=None):
+                 exchange: str = "rccl", device=None):
         from .laplacian import NormalizedLaplacian, require_gpu
         self.device = require_gpu(device)
         self.group = group
@@ -204,6 +210,48 @@ class ShardedWavelet:
         self._bufs = {}
         self.profile = False          # record (exchange, step) event pairs per Chebyshev step
         self.events = []
+        self._dist = None
+        if exchange == "rccl":
+            self._dist = self._create_native()
+        elif exchange not in ("nccl", "host"):
+            raise ValueError(f"exchange must be 'rccl', 'nccl' or 'host', not {exchange!r}")
+
+    def _create_native(self):
+        """The native chain's handle: RCCL unique id from rank 0, broadcast over
+        the group, then ncclCommInitRank on every rank (collective)."""
+        lib, p = _lib.load(), self.plan
+        uid = (ctypes.c_uint8 * 128)()
+        if p.rank == 0:
+            check(lib.wg_dist_unique_id(uid), "dist_unique_id")
+        if p.world > 1:
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(self.group, 0) if self.group else 0,
+                                       group=self.group)
+            ctypes.memmove(uid, obj[0], 128)
+        sc = np.ascontiguousarray(p.send_counts, dtype=np.int64)
+        rc = np.ascontiguousarray(p.recv_counts, dtype=np.int64)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.wg_dist_create(self.L.handle, uid, p.rank, p.world,
+                                     ptr(self.send_rows) if self.send_rows.numel() else None,
+                                     sc.ctypes.data, rc.ctypes.data, ctypes.byref(h)), "dist_create")
+        return h
+
+    def set_graph(self, enable: bool) -> None:
+        """Replay the native chain as a hipGraph (default) or run it eagerly."""
+        if self._dist is not None:
+            check(_lib.load().wg_dist_set_graph(self._dist, 1 if enable else 0), "dist_set_graph")
+
+    def close(self) -> None:
+        if getattr(self, "_dist", None) is not None:
+            _lib.load().wg_dist_destroy(self._dist)
+            self._dist = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
 
     # -------------------------------------------------------------- exchange
     def _pack(self, ext: torch.Tensor, out: torch.Tensor) -> None:
@@ -234,6 +282,11 @@ class ShardedWavelet:
         torch.cuda.synchronize(self.device)
         ex = [e[0].elapsed_time(e[1]) for e in self.events]
         self.events = []
+        if self._dist is not None:
+            tot, cnt = ctypes.c_double(0), ctypes.c_int64(0)
+            check(_lib.load().wg_dist_profile_collect(self._dist, ctypes.byref(tot), ctypes.byref(cnt)),
+                  "dist_profile_collect")
+            ex = [tot.value / cnt.value] * cnt.value if cnt.value else []
         st = self.L.profile_collect()
         self.L.profile_enable(False)
         self.profile = False
@@ -281,13 +334,36 @@ class ShardedWavelet:
                       "cheb_step_u")
         return S
 
-    def wavelet_features(self, X0_local: torch.Tensor, k: int = 3, s: float = 0.8):
-        """Owned rows of (H, S) for signal rows X0_local (caller order)."""
+    def _wavelet_features_native(self, X: torch.Tensor, k: int, s: float, out):
+        """The native chain: inputs copied into a persistent buffer and outputs
+        written to persistent ones (stable pointers, so the captured hipGraph is
+        replayed), then cloned -- unless the caller passes ``out=(H, S)``."""
+        p, F = self.plan, X.shape[1]
+        xb = self._buf("X", p.n_own, F)
+        if xb.data_ptr() != X.data_ptr():
+            xb.copy_(X)
+        if out is not None:
+            H, S = out
+            if H.shape != (p.n_own, F) or S.shape != (p.n_own, F) or not (H.is_contiguous() and S.is_contiguous()):
+                raise ValueError("out=(H, S) must be contiguous (n_own, F) float32 tensors")
+        else:
+            H, S = self._buf("Hout", p.n_own, F), self._buf("Sout", p.n_own, F)
+        with torch.cuda.device(self.device):
+            check(_lib.load().wg_dist_wavelet_features(self._dist, ptr(xb), F, int(k), float(s), ptr(S), ptr(H),
+                                                       torch.cuda.current_stream(self.device).cuda_stream),
+                  "dist_wavelet_features")
+        return (H, S) if out is not None else (H.clone(), S.clone())
+
+    def wavelet_features(self, X0_local: torch.Tensor, k: int = 3, s: float = 0.8, out=None):
+        """Owned rows of (H, S) for signal rows X0_local (caller order).
+        ``out=(H, S)``: write into these (native exchange only)."""
         import math
         p = self.plan
         L = self.L
         X = X0_local.to(self.device, torch.float32).reshape(p.n_own, -1).contiguous()
         F = X.shape[1]
+        if self._dist is not None and p.n_own:
+            return self._wavelet_features_native(X, k, s, out)
         if F == 1 and k >= 1 and p.n_own and self.u_len() > 0:
             S = self._wavelet_features_u(X, k, s)
             from .wavelet import row_l1_normalize

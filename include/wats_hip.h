@@ -219,6 +219,34 @@ int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, 
                    void* stream);
 
 /* -------------------------------------------------------------------------
+ * Section 8(e): the row-sharded chain with its halo exchange in native code.
+ * One process per GPU.  `L` is this rank's shard (n_rows own rows; columns
+ * [own | halo], the halo grouped by owner rank, as wats_hip/dist.py plans
+ * it).  Per Chebyshev step (reference calibration/WATS.py:35-36) the own rows
+ * peers asked for are packed (send_rows: internal ids, grouped by peer,
+ * send_counts[q] for peer q) and exchanged with grouped ncclSend / ncclRecv
+ * (RCCL over xGMI) into the halo rows (recv_counts[q] from peer q), then the
+ * step kernel runs.  The chain is captured into a hipGraph on its second call
+ * with the same arguments and replayed from then on (wg_dist_set_graph(D, 0)
+ * keeps it eager; profiling via wg_profile_enable(L) also runs eagerly).
+ * wg_dist_unique_id fills NCCL_UNIQUE_ID_BYTES (128) bytes on one rank; every
+ * rank passes the same bytes to wg_dist_create (collective: blocks until all
+ * ranks joined).  X0, S, H: own rows (n_rows, F) in the caller's order.
+ * ---------------------------------------------------------------------- */
+typedef struct wg_dist_s* wg_dist_t;
+int wg_dist_unique_id(void* id_out /* 128 bytes, host */);
+int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world,
+                   const int32_t* send_rows, const int64_t* send_counts_host,
+                   const int64_t* recv_counts_host, wg_dist_t* out);
+int wg_dist_destroy(wg_dist_t D);
+int wg_dist_set_graph(wg_dist_t D, int32_t enable);
+int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K, double s, float* S,
+                             float* H, void* stream);
+/* Total time (ms) and count of the halo exchanges (pack + RCCL) recorded
+ * while profiling was enabled on the shard's handle; resets. */
+int wg_dist_profile_collect(wg_dist_t D, double* exchange_ms_host, int64_t* count_host);
+
+/* -------------------------------------------------------------------------
  * Section 8(f)-2: the base model's propagation.  CompatibleGCN.forward
  * (reference src/gnn/model.py:43-52) computes deg = adj.sum(dim=1),
  * deg[deg == 0] = 1, adj_norm = adj / deg and twice x -> adj_norm @ x with a

@@ -176,3 +176,100 @@ def test_sharded_chain_gpu_multi_rank(world, kind, F, lds):
     else:  # H = S / (|S| + 1e-8) is ill-conditioned where a random signal cancels (|S| ~ 1e-8..1e-4)
         ok = np.abs(ref["S"]) > 1e-3 * np.abs(ref["S"]).max()
         assert np.abs(H[ok] - ref["H"][ok]).max() <= 1e-5
+
+
+# ------------------------------------------------------------------ GPU, native chain (csrc/dist.hip)
+def _native_graph(kind):
+    if kind == "dense-rmat":   # avg degree ~ 80: the F = 1 LDS window kernel applies
+        return rmat_graph(3000, 240000, seed=7)
+    return _graph(kind)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,F,lds", [("rmat", 1, 3), ("dense-rmat", 1, 2), ("rmat", 40, 3), ("weighted", 4, 3),
+                                        ("weighted", 1, 3)])
+def test_native_chain_world1(kind, F, lds):
+    """wg_dist_* at world 1 (its own one-rank RCCL communicator, no halo):
+    eager first call, captured second, replayed after -- all equal the oracle
+    and each other bit for bit."""
+    from wats_hip.dist import ShardedWavelet
+    g = _native_graph(kind)
+    sw = ShardedWavelet(g.indptr, g.indices, g.values, g.n, np.array([0, g.n]), exchange="rccl", device="cuda:0")
+    sw.L.tune(lds=lds)
+    rng = np.random.default_rng(2)
+    X = torch.from_numpy(rng.standard_normal((g.n, F)).astype(np.float32)).cuda()
+    K = 8
+    outs = [sw.wavelet_features(X, k=K, s=0.8) for _ in range(3)]
+    ref = O.graph_wavelet_features(g.to_scipy(), k=K, s=0.8, X0=X.cpu().numpy(), return_all=True)
+    for H, S in outs:
+        assert torch.equal(S, outs[0][1]) and torch.equal(H, outs[0][0])
+    S, H = outs[0][1].cpu().numpy(), outs[0][0].cpu().numpy()
+    assert_parity(S, ref["S"], what=f"native world=1 {kind} F={F} S")
+    ok = np.abs(ref["S"]) > 1e-3 * np.abs(ref["S"]).max(axis=0, keepdims=True) if F == 1 else np.ones_like(S, bool)
+    assert np.abs(H[ok] - ref["H"][ok]).max() <= 1e-5
+    sw.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F,lds,graph", [(1, 2, 1), (1, 0, 1), (8, 3, 1), (8, 3, 0), (40, 3, 1)])
+def test_native_chain_loopback_exchange(F, lds, graph):
+    """The native exchange with real RCCL traffic on one GPU: a one-rank shard
+    whose column space is [own | halo] where the halo columns are copies of own
+    rows (every entry (i, j) with j % 3 == 0 and (i + j) odd reads the copy).
+    Per step the pack kernel + ncclSend/ncclRecv to self must refresh the
+    copies, so the result equals the unsharded chain."""
+    import ctypes
+    import wats_hip
+    from wats_hip import _lib
+    from wats_hip._lib import check, ptr
+    g = _native_graph("dense-rmat")
+    n = g.n
+    J = np.arange(0, n, 3)
+    slot = np.full(n, -1, np.int64)
+    slot[J] = np.arange(J.size)
+    rows = np.repeat(np.arange(n), np.diff(g.indptr))
+    cols = g.indices.astype(np.int64).copy()
+    move = (slot[cols] >= 0) & ((rows + cols) % 2 == 1)
+    cols[move] = n + slot[cols[move]]
+    deg = np.bincount(g.indices, minlength=n).astype(np.float32)   # unweighted, symmetric, no loops: w = degree
+    w_ext = np.concatenate([deg, deg[J]])
+    L = wats_hip.NormalizedLaplacian(n, torch.from_numpy(g.indptr), torch.from_numpy(cols.astype(np.int32)), None,
+                                     n_cols=n + J.size, w_cols=torch.from_numpy(w_ext), device="cuda:0")
+    L.tune(lds=lds)
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    caller = torch.from_numpy(J.astype(np.int32)).to(dev)
+    internal = torch.empty_like(caller)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    check(lib.wg_laplacian_map_rows(L.handle, 0, ptr(caller), caller.numel(), ptr(internal), st), "map_rows")
+    uid = (ctypes.c_uint8 * 128)()
+    check(lib.wg_dist_unique_id(uid), "unique_id")
+    counts = np.array([J.size], np.int64)
+    h = ctypes.c_void_p()
+    check(lib.wg_dist_create(L.handle, uid, 0, 1, ptr(internal), counts.ctypes.data, counts.ctypes.data,
+                             ctypes.byref(h)), "dist_create")
+    try:
+        check(lib.wg_dist_set_graph(h, graph), "set_graph")
+        rng = np.random.default_rng(4)
+        X = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
+        S = torch.empty(n, F, device=dev)
+        H = torch.empty(n, F, device=dev)
+        K = 8
+        res = []
+        for _ in range(3):
+            S.fill_(float("nan"))
+            check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")
+            res.append(S.cpu().numpy().copy())
+        ref = O.graph_wavelet_features(g.to_scipy(), k=K, s=0.8, X0=X.cpu().numpy(), return_all=True)
+        for r in res:
+            assert np.array_equal(r, res[0])
+        assert_parity(res[0], ref["S"], what=f"loopback F={F} lds={lds} graph={graph}")
+        L.profile_enable(True)
+        check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")
+        tot, cnt = ctypes.c_double(0), ctypes.c_int64(0)
+        check(lib.wg_dist_profile_collect(h, ctypes.byref(tot), ctypes.byref(cnt)), "profile_collect")
+        L.profile_collect()
+        L.profile_enable(False)
+        assert cnt.value == K and tot.value > 0
+    finally:
+        lib.wg_dist_destroy(h)
