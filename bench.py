@@ -65,6 +65,8 @@ def parse():
                     help="also measure this config row-sharded over all ranks (RCCL halo exchange) and attach it "
                          "as the 'sharded' object of the line; 'none' to skip")
     ap.add_argument("--sharded-steps", type=int, default=5)
+    ap.add_argument("--sharded-timeout", type=float, default=240.0,
+                    help="seconds the sharded extra may take before the line is printed without it")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "nccl"],
                     help="sharded halo exchange: native chain (rccl) or torch all_to_all_single per step (nccl)")
     ap.add_argument("--cold-reps", type=int, default=5,
@@ -138,7 +140,8 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     nnz_global = int(indptr[-1])
     del indptr_d, indices_d
     torch.cuda.empty_cache()
-    sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device)
+    with _stdout_to_stderr():   # RCCL prints its version banner at communicator init: keep stdout one JSON line
+        sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device)
     if F == 1:
         X = sw.L.log1p_degree()
     else:
@@ -364,19 +367,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
         edges_k = float(e.item())
 
-    sharded = None
-    if args.sharded_extra and args.sharded_extra != "none":
-        # BASELINE configs 3-4: one big graph row-sharded over all ranks with the
-        # per-step RCCL halo exchange.  Measured after the main line's timing;
-        # a Python-level failure is reported in the line instead of losing it.
-        try:
-            del S, H
-            torch.cuda.empty_cache()
-            sharded = run_sharded(args.sharded_extra, None, None, args.sharded_steps, 1, args.seed, args.s, world,
-                                  rank, device, args.exchange)
-        except Exception as exc:  # noqa: BLE001
-            sharded = {"error": f"{type(exc).__name__}: {exc}"}
-
+    line = None
     if rank == 0:
         avg_ms = prof["sum_ms"] / max(1, prof["launches"])
         # the step kernel processes the rows that enter the chain; purely
@@ -440,20 +431,66 @@ def main():
             line["cold"] = cold
         if f1 is not None:
             line["f1_companion"] = f1
-        if sharded is not None:
-            line["sharded"] = sharded
         if world == 1 and not args.no_cpu_baseline:
             if X_host is None:
                 X_host = L.log1p_degree().cpu().numpy()
             line["cpu_baseline"] = cpu_baseline(g, K, F, args.s, X_host, args.cpu_seconds)
             line["cpu_baseline"]["host_cpu"] = _cpu_model()
-        js = json.dumps(line)
-        print(js, flush=True)
-        if args.out:
-            with open(args.out, "w") as f:
-                f.write(js + "\n")
+
+    sharded = None
+    if args.sharded_extra and args.sharded_extra != "none":
+        # BASELINE configs 3-4: one big graph row-sharded over all ranks with the
+        # per-step halo exchange.  Measured after the main line is complete; a
+        # Python-level failure is reported in the line instead of losing it, and
+        # a watchdog prints the line and ends the process if the sharded run
+        # (a collective on several GPUs) does not finish in time.
+        import threading
+
+        def _expire():
+            if rank == 0:
+                line["sharded"] = {"error": f"timeout after {args.sharded_timeout:.0f} s"}
+                _emit(line, args.out)
+            os._exit(0)
+        watchdog = threading.Timer(args.sharded_timeout, _expire)
+        watchdog.daemon = True
+        watchdog.start()
+        try:
+            del S, H
+            torch.cuda.empty_cache()
+            sharded = run_sharded(args.sharded_extra, None, None, args.sharded_steps, 1, args.seed, args.s, world,
+                                  rank, device, args.exchange)
+        except Exception as exc:  # noqa: BLE001
+            sharded = {"error": f"{type(exc).__name__}: {exc}"}
+        watchdog.cancel()
+    if rank == 0:
+        if sharded is not None:
+            line["sharded"] = sharded
+        _emit(line, args.out)
     if world > 1:
         dist.destroy_process_group()
+
+
+class _stdout_to_stderr:
+    """Point file descriptor 1 at stderr for the duration (native libraries'
+    prints included)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+def _emit(line: dict, out: str | None) -> None:
+    js = json.dumps(line)
+    print(js, flush=True)
+    if out:
+        with open(out, "w") as f:
+            f.write(js + "\n")
 
 
 def _cpu_model() -> str:
