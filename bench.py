@@ -299,7 +299,9 @@ def main():
     device = torch.device("cuda", dev_idx)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        with _stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=device)
+            dist.barrier()
     if args.mode == "sharded":
         sharded_main(args, world, rank, device)
         if world > 1:
