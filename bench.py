@@ -61,11 +61,11 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    ap.add_argument("--sharded-extra", default="reddit",
-                    help="also measure this config row-sharded over all ranks (RCCL halo exchange) and attach it "
-                         "as the 'sharded' object of the line; 'none' to skip")
+    ap.add_argument("--sharded-extra", default="reddit,rmat-8m",
+                    help="comma-separated configs also measured row-sharded over all ranks (RCCL halo exchange), "
+                         "attached as 'sharded' (first) and 'sharded_<config>' objects of the line; 'none' to skip")
     ap.add_argument("--sharded-steps", type=int, default=5)
-    ap.add_argument("--sharded-timeout", type=float, default=240.0,
+    ap.add_argument("--sharded-timeout", type=float, default=360.0,
                     help="seconds the sharded extra may take before the line is printed without it")
     ap.add_argument("--exchange", default="rccl", choices=["rccl", "nccl"],
                     help="sharded halo exchange: native chain (rccl) or torch all_to_all_single per step (nccl)")
@@ -439,34 +439,37 @@ def main():
             line["cpu_baseline"] = cpu_baseline(g, K, F, args.s, X_host, args.cpu_seconds)
             line["cpu_baseline"]["host_cpu"] = _cpu_model()
 
-    sharded = None
-    if args.sharded_extra and args.sharded_extra != "none":
+    extras = [c for c in (args.sharded_extra or "none").split(",") if c and c != "none"]
+    results = {}
+    if extras:
         # BASELINE configs 3-4: one big graph row-sharded over all ranks with the
         # per-step halo exchange.  Measured after the main line is complete; a
         # Python-level failure is reported in the line instead of losing it, and
-        # a watchdog prints the line and ends the process if the sharded run
-        # (a collective on several GPUs) does not finish in time.
+        # a watchdog prints the line and ends the process if a sharded run (a
+        # collective on several GPUs) does not finish in time.
         import threading
 
         def _expire():
             if rank == 0:
-                line["sharded"] = {"error": f"timeout after {args.sharded_timeout:.0f} s"}
+                for c in extras:
+                    results.setdefault(c, {"error": f"timeout after {args.sharded_timeout:.0f} s"})
+                _attach(line, results)
                 _emit(line, args.out)
             os._exit(0)
         watchdog = threading.Timer(args.sharded_timeout, _expire)
         watchdog.daemon = True
         watchdog.start()
-        try:
-            del S, H
-            torch.cuda.empty_cache()
-            sharded = run_sharded(args.sharded_extra, None, None, args.sharded_steps, 1, args.seed, args.s, world,
-                                  rank, device, args.exchange)
-        except Exception as exc:  # noqa: BLE001
-            sharded = {"error": f"{type(exc).__name__}: {exc}"}
+        del S, H
+        for c in extras:
+            try:
+                torch.cuda.empty_cache()
+                results[c] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
+                                         device, args.exchange)
+            except Exception as exc:  # noqa: BLE001
+                results[c] = {"error": f"{type(exc).__name__}: {exc}"}
         watchdog.cancel()
     if rank == 0:
-        if sharded is not None:
-            line["sharded"] = sharded
+        _attach(line, results)
         _emit(line, args.out)
     if world > 1:
         dist.destroy_process_group()
@@ -485,6 +488,12 @@ class _stdout_to_stderr:
         sys.stdout.flush()
         os.dup2(self.saved, 1)
         os.close(self.saved)
+
+
+def _attach(line: dict, results: dict) -> None:
+    """First sharded config -> line["sharded"], the others -> line["sharded_<config>"]."""
+    for i, (c, r) in enumerate(results.items()):
+        line["sharded" if i == 0 else "sharded_" + c.replace("-", "")] = r
 
 
 def _emit(line: dict, out: str | None) -> None:
