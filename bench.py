@@ -67,8 +67,10 @@ def parse():
     ap.add_argument("--sharded-steps", type=int, default=5)
     ap.add_argument("--sharded-timeout", type=float, default=360.0,
                     help="seconds the sharded extra may take before the line is printed without it")
-    ap.add_argument("--exchange", default="rccl", choices=["rccl", "nccl"],
-                    help="sharded halo exchange: native chain (rccl) or torch all_to_all_single per step (nccl)")
+    ap.add_argument("--exchange", default="ipc,rccl",
+                    help="comma-separated sharded halo exchanges: native chain with the one-sided IPC pull (ipc) or "
+                         "grouped ncclSend/ncclRecv (rccl), or torch all_to_all_single per step (nccl); the sharded "
+                         "extras run once per exchange (--mode sharded: the first one)")
     ap.add_argument("--cold-reps", type=int, default=5,
                     help="chains timed after writing a 512 MiB scratch buffer (cold Infinity Cache / L2); 0 = skip")
     ap.add_argument("--f1-companion", type=int, default=1,
@@ -131,8 +133,10 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     n_t, nnz_t, K_def, F_def = NAMED_CONFIGS[config]
     K = K if K is not None else K_def
     F = F if F is not None else F_def
+    _log(f"sharded {config} ({exchange}): generating")
     indptr_d, indices_d = rmat_graph_device(n_t, nnz_t, seed=seed, device=device)
     indptr = indptr_d.cpu().numpy()
+    _log(f"sharded {config} ({exchange}): generated; building the shard")
     bounds = partition_rows(indptr, world)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
     lo, hi = int(indptr[r0]), int(indptr[r1])
@@ -141,7 +145,8 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     del indptr_d, indices_d
     torch.cuda.empty_cache()
     with _stdout_to_stderr():   # RCCL prints its version banner at communicator init: keep stdout one JSON line
-        sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device)
+        sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device,
+                            max_features=F)
     if F == 1:
         X = sw.L.log1p_degree()
     else:
@@ -149,11 +154,13 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         g.manual_seed(1 + rank)
         X = torch.randn(r1 - r0, F, generator=g, device=device)
     out = (torch.empty(r1 - r0, F, device=device), torch.empty(r1 - r0, F, device=device))
-    run = (lambda: sw.wavelet_features(X, k=K, s=s_heat, out=out)) if exchange == "rccl" else \
+    _log(f"sharded {config} ({exchange}): shard ready ({r1 - r0} rows, {sw.plan.n_halo} halo rows); warmup")
+    run = (lambda: sw.wavelet_features(X, k=K, s=s_heat, out=out)) if exchange in ("rccl", "ipc") else \
         (lambda: sw.wavelet_features(X, k=K, s=s_heat))
-    for _ in range(max(2, warmup)):   # the native chain is captured into a hipGraph on its 2nd call
+    for i in range(max(2, warmup)):   # the native chain is captured into a hipGraph on its 2nd call
         run()
-    torch.cuda.synchronize(device)
+        torch.cuda.synchronize(device)
+        _log(f"sharded {config} ({exchange}): warmup call {i + 1} done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -164,18 +171,14 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    _log(f"sharded {config} ({exchange}): timed {steps} chains in {elapsed:.3f} s; profiling pass")
     # kernel / exchange attribution: one more pass, eager, with HIP events (outside the timed region)
     sw.profile_start()
     run()
     prof = sw.profile_collect()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    nnz_lhat = torch.tensor([float(sw.L.nnz)], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(nnz_lhat)
-    nnz_lhat = float(nnz_lhat.item())
+        elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
+    nnz_lhat = _allreduce(float(sw.L.nnz), dist.ReduceOp.SUM, device) if world > 1 else float(sw.L.nnz)
     p = sw.plan
     b_8d = algorithmic_bytes(p.n_own, sw.L.nnz, F)
     lds_info = sw.L.lds_plan_info(active_only=False) if (F == 1 and sw.u_len() > 0) else None
@@ -198,8 +201,11 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         "data": "synthetic",
         "config": {"workload": f"{config}-size R-MAT (GPU generator, seed {seed}), one graph row-sharded over "
                                f"{world} ranks, halo exchange per Chebyshev step "
-                               + ("(native: grouped ncclSend/ncclRecv, chain replayed as a hipGraph)"
-                                  if exchange == "rccl" else "(torch all_to_all_single, RCCL)") + f"; K={K} F={F}",
+                               + {"rccl": "(native: grouped ncclSend/ncclRecv, chain replayed as a hipGraph)",
+                                  "ipc": "(native: one-sided pull from IPC-mapped peer memory, flag-ordered "
+                                         "phases, chain replayed as a hipGraph)",
+                                  "nccl": "(torch all_to_all_single, RCCL)"}[exchange] + f"; K={K} F={F}",
+                   "exchange": exchange,
                    "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
                    "rank0_rows": p.n_own, "rank0_halo_rows": p.n_halo, "parallelism": f"rows x{world}"},
         "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
@@ -280,7 +286,7 @@ def f1_companion(lib, L, K, s_heat, steps, device):
 
 def sharded_main(args, world, rank, device):
     line = run_sharded(args.config, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
-                       args.exchange)
+                       args.exchange.split(",")[0])
     if rank == 0:
         js = json.dumps(line)
         print(js, flush=True)
@@ -299,8 +305,14 @@ def main():
     device = torch.device("cuda", dev_idx)
     torch.cuda.set_device(device)
     if world > 1:
+        # WATS_BENCH_PG=gloo: rehearse several ranks on one GPU (RCCL refuses two
+        # ranks per device); with the IPC exchange the sharded path needs no RCCL
+        backend = os.environ.get("WATS_BENCH_PG", "nccl")
         with _stdout_to_stderr():
-            dist.init_process_group("nccl", device_id=device)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group(backend)
             dist.barrier()
     if args.mode == "sharded":
         sharded_main(args, world, rank, device)
@@ -356,18 +368,15 @@ def main():
     elapsed = t1 - t0
     step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     median_ms = step_ms[len(step_ms) // 2] if step_ms else None
+    _log(f"main: timed {args.steps} passes in {elapsed:.3f} s; cold / F=1 companion")
     cold = cold_chains(step, L, args.cold_reps, device) if args.cold_reps > 0 else None
     f1 = None
     if args.f1_companion and F > 1:
         f1 = f1_companion(lib, L, K, args.s, args.steps, device)
     edges_k = float(nnz) * K * args.steps
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        e = torch.tensor([edges_k], dtype=torch.float64, device=device)
-        dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        edges_k = float(e.item())
+        elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
+        edges_k = _allreduce(edges_k, dist.ReduceOp.SUM, device)
 
     line = None
     if rank == 0:
@@ -451,8 +460,8 @@ def main():
 
         def _expire():
             if rank == 0:
-                for c in extras:
-                    results.setdefault(c, {"error": f"timeout after {args.sharded_timeout:.0f} s"})
+                results["timeout"] = {"error": f"timeout after {args.sharded_timeout:.0f} s; the runs not "
+                                                f"listed did not finish"}
                 _attach(line, results)
                 _emit(line, args.out)
             os._exit(0)
@@ -460,13 +469,16 @@ def main():
         watchdog.daemon = True
         watchdog.start()
         del S, H
+        exchanges = [x for x in args.exchange.split(",") if x]
         for c in extras:
-            try:
-                torch.cuda.empty_cache()
-                results[c] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
-                                         device, args.exchange)
-            except Exception as exc:  # noqa: BLE001
-                results[c] = {"error": f"{type(exc).__name__}: {exc}"}
+            for j, x in enumerate(exchanges):
+                key = c if j == 0 else f"{c}_{x}"
+                try:
+                    torch.cuda.empty_cache()
+                    results[key] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
+                                               device, x)
+                except Exception as exc:  # noqa: BLE001
+                    results[key] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
         watchdog.cancel()
     if rank == 0:
         _attach(line, results)
@@ -490,8 +502,24 @@ class _stdout_to_stderr:
         os.close(self.saved)
 
 
+os.environ.setdefault("WATS_DIST_LOG", "1")
+
+
+def _log(msg: str) -> None:
+    """Progress on stderr (rank-prefixed), so long multi-rank runs show where they are."""
+    print(f"[bench rank {os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr,
+          flush=True)
+
+
+def _allreduce(x: float, op, device) -> float:
+    on = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
 def _attach(line: dict, results: dict) -> None:
-    """First sharded config -> line["sharded"], the others -> line["sharded_<config>"]."""
+    """First sharded run -> line["sharded"], the others -> line["sharded_<config>[_<exchange>]"]."""
     for i, (c, r) in enumerate(results.items()):
         line["sharded" if i == 0 else "sharded_" + c.replace("-", "")] = r
 

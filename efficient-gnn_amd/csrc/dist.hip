@@ -33,6 +33,76 @@ __global__ void pack_rows_kernel(int64_t n, int64_t F, const int32_t* __restrict
   dst[idx] = src[(int64_t)rows[i] * F + (idx - i * F)];
 }
 
+// ---- one-sided exchange over IPC-mapped peer memory (exchange mode "ipc") ----
+// Each rank exposes one allocation: two slots of its extended vector ([own |
+// halo] rows, ping-pong) and `world` int64 flags.  A rank's flag q holds how
+// many chain phases peer q has completed (phase 0: the chain's first vector,
+// phase k: step k).  Before phase p a rank waits until every peer has
+// completed p phases: then each peer's step-(p-1) vector is final, and no peer
+// still reads the slot phase p overwrites (its last read of that slot was in
+// its phase p-1).  The wait and the pull of the halo rows (system-scope loads
+// straight from the owners' slots over xGMI) are one kernel; the signal is a
+// one-lane kernel after the phase's last kernel.
+constexpr int kMaxPeers = 16;
+
+struct IpcPull {
+  const float* slot_base[kMaxPeers];  // peer q's slot 0 (mapped); slot 1 at + slot_floats[q]
+  int64_t slot_floats[kMaxPeers];
+  const int64_t* flags;               // mine: flags[q] = phases peer q completed
+  const int64_t* count;               // phases this rank completed
+  int32_t* err;
+  int32_t world, rank;
+};
+
+__device__ __forceinline__ void ipc_wait(const IpcPull& p) {
+  if (threadIdx.x < 64) {
+    const int q = threadIdx.x;
+    const int64_t target = *p.count;
+    bool ok = true;
+    if (q < p.world && q != p.rank) {
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(p.flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > 100ull * 1000 * 1000 * 60) {  // 60 s at the 100 MHz constant clock
+          ok = false;
+          break;
+        }
+      }
+    }
+    if (!ok) __hip_atomic_fetch_or(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+  __syncthreads();
+}
+
+// halo row h (owner owner[h], row src[h] of the owner's extended vector) -> ext[n_own + h]
+__global__ __launch_bounds__(256) void ipc_pull_kernel(IpcPull p, int slot, int64_t n_own, int64_t n_halo, int64_t F,
+                                                       const int32_t* __restrict__ owner,
+                                                       const int32_t* __restrict__ src, float* __restrict__ ext) {
+  ipc_wait(p);
+  const int64_t total = n_halo * F;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t h = idx / F;
+    const int q = owner[h];
+    const float* from = p.slot_base[q] + slot * p.slot_floats[q] + (int64_t)src[h] * F + (idx - h * F);
+    ext[n_own * F + idx] = __hip_atomic_load(from, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// wait only (before a phase that writes a slot but pulls nothing: the chain's first vector)
+__global__ void ipc_wait_kernel(IpcPull p) { ipc_wait(p); }
+
+// this rank completed one more phase: count += 1, then tell every peer
+__global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, int64_t* const* peer_flags) {
+  if (threadIdx.x != 0) return;
+  __threadfence_system();
+  const int64_t c = *count + 1;
+  *count = c;
+  for (int q = 0; q < world; ++q)
+    if (q != rank) __hip_atomic_store(peer_flags[q] + rank, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 int nccl_try(ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return WG_OK;
   return fail(WG_ERR_HIP, "%s: %s", what, ncclGetErrorString(r));
@@ -73,10 +143,25 @@ struct wg_dist_s {
   // exchange timing (profile mode, eager only)
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
+  // exchange mode "ipc" (wg_dist_ipc_local / wg_dist_ipc_connect)
+  bool ipc = false;
+  int64_t F_max = 0, slot_floats = 0;
+  float* region = nullptr;            // [slot 0][slot 1][flags: world int64]
+  int64_t* count = nullptr;           // phases completed (device)
+  int32_t* err = nullptr;             // wait timed out (device)
+  int32_t* halo_owner = nullptr;
+  int32_t* halo_src = nullptr;
+  std::vector<void*> peer_region;     // IPC-mapped, nullptr for self
+  int64_t** peer_flags = nullptr;     // device array [world]
+  IpcPull pull{};
 
   ~wg_dist_s() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (comm) (void)ncclCommDestroy(comm);
+    for (void* q : peer_region)
+      if (q) (void)hipIpcCloseMemHandle(q);
+    for (void* q : {(void*)region, (void*)count, (void*)err, (void*)halo_owner, (void*)halo_src, (void*)peer_flags})
+      (void)hipFree(q);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
@@ -101,8 +186,32 @@ struct wg_dist_s {
     return WG_OK;
   }
 
-  // refresh the halo rows ext[n_own ...] (F floats per row) from their owners
-  int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st) {
+  int ipc_signal(hipStream_t st) {
+    hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, st, count, world, rank, peer_flags);
+    WG_LAUNCH_CHECK();
+    return WG_OK;
+  }
+
+  int ipc_wait_only(hipStream_t st) {
+    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, st, pull);
+    WG_LAUNCH_CHECK();
+    return WG_OK;
+  }
+
+  // refresh the halo rows ext[n_own ...] (F floats per row) from their owners.
+  // ipc: `slot` is the region slot ext lives in (the owners' rows are read from
+  // the same slot of their regions)
+  int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot = 0) {
+    if (ipc && world == 1) return WG_OK;  // no peers: nothing to wait for or pull
+    if (ipc) {
+      if (int rc = mark(st, true)) return rc;
+      const int64_t total = n_halo * F;
+      const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(64, ceil_div(total, 256)));
+      hipLaunchKernelGGL(ipc_pull_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, n_halo, F, halo_owner,
+                         halo_src, ext);
+      WG_LAUNCH_CHECK();
+      return mark(st, false);
+    }
     if (world == 1 && n_send == 0) return WG_OK;
     if (int rc = mark(st, true)) return rc;
     if (n_send > 0) {
@@ -140,7 +249,7 @@ struct wg_dist_s {
     const size_t snd = ((size_t)std::max<int64_t>(n_send, 1) * F + 63) / 64 * 64;
     const size_t ulen = lp ? ((size_t)lp->lchunks * lp->nb * 32 + 63) / 64 * 64 : 0;
     // lds: T ping-pong (own rows) + u ping-pong (padded column space); else T ping-pong over [own | halo]
-    const size_t need = (lp ? 2 * own + 2 * ulen : 2 * ext) + own + snd;
+    const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd;
     if (ws_floats < need) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       WG_HIP_TRY(hipStreamIsCapturing(st, &cs));
@@ -158,37 +267,50 @@ struct wg_dist_s {
       p += n;
       return q;
     };
+    // ipc: the exchanged vectors live in the shared region's two slots, and
+    // every phase (first vector, each step) is bracketed by wait and signal
+    if (ipc && (lp ? (int64_t)ulen : (int64_t)ext) > slot_floats)
+      return fail(WG_ERR_UNSUPPORTED, "wg_dist: F=%lld exceeds the IPC region (F_max=%lld)", (long long)F,
+                  (long long)F_max);
+    const bool sig = ipc && K >= 1 && world > 1;
     if (lp) {
       float* T[2] = {take(own), take(own)};
-      float* U[2] = {take(ulen), take(ulen)};
+      float* U[2] = {ipc ? region : take(ulen), ipc ? region + slot_floats : take(ulen)};
       float* sint = take(own);
       float* sendbuf = take(snd);
       int rc = launch_permute(L, 0, 1, X0, T[0], st);
+      if (!rc && sig) rc = ipc_wait_only(st);
       if (!rc) rc = launch_scale_dinv(L, n_own, T[0], U[0], st);
+      if (!rc && sig) rc = ipc_signal(st);
       for (int32_t k = 1; k <= K && !rc; ++k) {
-        rc = exchange(U[(k - 1) & 1], sendbuf, 1, st);
+        rc = exchange(U[(k - 1) & 1], sendbuf, 1, st, (k - 1) & 1);
         if (!rc)
           rc = launch_lds1_step(L, lp, k, U[(k - 1) & 1], T[(k - 1) & 1], k >= 2 ? T[k & 1] : nullptr,
                                 k == K ? nullptr : T[k & 1], k == K ? nullptr : U[k & 1], sint, 1.0,
                                 std::exp(-s * (double)k), st);
+        if (!rc && sig) rc = ipc_signal(st);
       }
       if (!rc) rc = launch_finalize(L, 1, sint, nullptr, 0.0, S, H, st);
       return rc;
     }
-    float* A[2] = {take(ext), take(ext)};
+    float* A[2] = {ipc ? region : take(ext), ipc ? region + slot_floats : take(ext)};
     float* sint = take(own);
     float* sendbuf = take(snd);
-    int rc = launch_permute(L, 0, F, X0, A[0], st);
+    int rc = WG_OK;
+    if (sig) rc = ipc_wait_only(st);
+    if (!rc) rc = launch_permute(L, 0, F, X0, A[0], st);
+    if (!rc && sig) rc = ipc_signal(st);
     if (!rc && K == 0)
       rc = hipMemcpyAsync(sint, A[0], sizeof(float) * n_own * F, hipMemcpyDeviceToDevice, st) == hipSuccess
                ? WG_OK
                : fail(WG_ERR_HIP, "wg_dist: copy");
     for (int32_t k = 1; k <= K && !rc; ++k) {
       float* cur = A[(k - 1) & 1];
-      rc = exchange(cur, sendbuf, F, st);
+      rc = exchange(cur, sendbuf, F, st, (k - 1) & 1);
       if (!rc)
         rc = launch_step(L, k, F, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
                          std::exp(-s * (double)k), st);
+      if (!rc && sig) rc = ipc_signal(st);
     }
     if (!rc) rc = launch_finalize(L, F, sint, nullptr, 0.0, S, H, st);
     return rc;
@@ -209,7 +331,7 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
                    const int64_t* send_counts, const int64_t* recv_counts, wg_dist_t* out) {
   if (!out) return fail(WG_ERR_INVALID, "wg_dist_create: out is NULL");
   *out = nullptr;
-  if (!L || !unique_id || world < 1 || rank < 0 || rank >= world || !send_counts || !recv_counts)
+  if (!L || world < 1 || rank < 0 || rank >= world || !send_counts || !recv_counts)
     return fail(WG_ERR_INVALID, "wg_dist_create: bad arguments (rank=%d world=%d)", rank, world);
   auto* D = new wg_dist_s();
   D->L = L;
@@ -246,7 +368,7 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
               hipEventCreateWithFlags(&D->fork, hipEventDisableTiming) != hipSuccess ||
               hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess))
     rc = fail(WG_ERR_HIP, "wg_dist_create: stream/event");
-  if (!rc) {
+  if (!rc && unique_id) {  // NULL: no RCCL communicator (one-sided IPC exchange, wg_dist_ipc_*)
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
     rc = nccl_try(ncclCommInitRank(&D->comm, world, id, rank), "ncclCommInitRank");
@@ -276,6 +398,8 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
                              void* stream_) {
   if (!D || F < 1 || K < 0 || !S || !H || (D->n_own && !X0))
     return fail(WG_ERR_INVALID, "wg_dist_wavelet_features: bad arguments (F=%lld K=%d)", (long long)F, K);
+  if (!D->comm && !D->ipc && (D->n_send > 0 || D->n_halo > 0 || D->world > 1))
+    return fail(WG_ERR_INVALID, "wg_dist_wavelet_features: no exchange (no RCCL id given and IPC not connected)");
   hipStream_t st = as_stream(stream_);
   const GraphKey key{X0, S, H, F, K, s};
   if (!(key == D->key)) {
@@ -316,6 +440,87 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   WG_HIP_TRY(hipGraphLaunch(D->exec, D->cap));
   WG_HIP_TRY(hipEventRecord(D->join, D->cap));
   WG_HIP_TRY(hipStreamWaitEvent(st, D->join, 0));
+  return WG_OK;
+}
+
+int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
+  if (!D || F_max < 1 || !blob) return fail(WG_ERR_INVALID, "wg_dist_ipc_local: bad arguments");
+  if (D->world > kMaxPeers) return fail(WG_ERR_UNSUPPORTED, "wg_dist_ipc_local: world > %d", kMaxPeers);
+  if (D->region) return fail(WG_ERR_INVALID, "wg_dist_ipc_local: already set up");
+  // a slot holds the extended vector at F_max, or the F = 1 LDS kernel's u (padded column space)
+  int64_t ulen = 0;
+  Lds1Plan* lp = nullptr;
+  if (int rc = get_lds1_plan(D->L, /*active_only=*/false, &lp)) return rc;
+  if (lp) ulen = (int64_t)lp->lchunks * lp->nb * 32;
+  D->F_max = F_max;
+  D->slot_floats = (std::max<int64_t>(D->n_cols * F_max, ulen) + 63) / 64 * 64;
+  const size_t bytes = sizeof(float) * 2 * D->slot_floats + sizeof(int64_t) * D->world;
+  if (int rc = dmalloc(reinterpret_cast<char**>(&D->region), bytes)) return rc;
+  if (int rc = dmalloc(&D->count, 1)) return rc;
+  if (int rc = dmalloc(&D->err, 1)) return rc;
+  WG_HIP_TRY(hipMemset(D->region, 0, bytes));
+  WG_HIP_TRY(hipMemset(D->count, 0, sizeof(int64_t)));
+  WG_HIP_TRY(hipMemset(D->err, 0, sizeof(int32_t)));
+  hipIpcMemHandle_t h;
+  WG_HIP_TRY(hipIpcGetMemHandle(&h, D->region));
+  char* out = static_cast<char*>(blob);
+  std::memset(out, 0, 128);
+  std::memcpy(out, &h, sizeof(h));
+  std::memcpy(out + 64, &D->slot_floats, sizeof(int64_t));
+  WG_HIP_TRY(hipDeviceSynchronize());
+  return WG_OK;
+}
+
+int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src) {
+  if (!D || !blobs || (D->n_halo > 0 && !halo_src)) return fail(WG_ERR_INVALID, "wg_dist_ipc_connect: bad arguments");
+  if (!D->region) return fail(WG_ERR_INVALID, "wg_dist_ipc_connect: call wg_dist_ipc_local first");
+  const char* b = static_cast<const char*>(blobs);
+  D->peer_region.assign(D->world, nullptr);
+  std::vector<int64_t*> pf(D->world, nullptr);
+  IpcPull p{};
+  for (int q = 0; q < D->world; ++q) {
+    hipIpcMemHandle_t h;
+    int64_t sf = 0;
+    std::memcpy(&h, b + 128 * q, sizeof(h));
+    std::memcpy(&sf, b + 128 * q + 64, sizeof(int64_t));
+    float* base = D->region;
+    if (q != D->rank) {
+      void* mp = nullptr;
+      WG_HIP_TRY(hipIpcOpenMemHandle(&mp, h, hipIpcMemLazyEnablePeerAccess));
+      D->peer_region[q] = mp;
+      base = static_cast<float*>(mp);
+    }
+    p.slot_base[q] = base;
+    p.slot_floats[q] = sf;
+    pf[q] = reinterpret_cast<int64_t*>(base + 2 * sf);
+  }
+  if (int rc = dmalloc(&D->peer_flags, (size_t)D->world)) return rc;
+  WG_HIP_TRY(hipMemcpy(D->peer_flags, pf.data(), sizeof(int64_t*) * D->world, hipMemcpyHostToDevice));
+  std::vector<int32_t> owner(D->n_halo);
+  for (int q = 0; q < D->world; ++q)
+    for (int64_t i = D->recv_off[q]; i < D->recv_off[q + 1]; ++i) owner[i] = q;
+  if (D->n_halo > 0) {
+    if (int rc = dmalloc(&D->halo_owner, (size_t)D->n_halo)) return rc;
+    if (int rc = dmalloc(&D->halo_src, (size_t)D->n_halo)) return rc;
+    WG_HIP_TRY(hipMemcpy(D->halo_owner, owner.data(), sizeof(int32_t) * D->n_halo, hipMemcpyHostToDevice));
+    WG_HIP_TRY(hipMemcpy(D->halo_src, halo_src, sizeof(int32_t) * D->n_halo, hipMemcpyDefault));
+  }
+  p.flags = reinterpret_cast<const int64_t*>(D->region + 2 * D->slot_floats);
+  p.count = D->count;
+  p.err = D->err;
+  p.world = D->world;
+  p.rank = D->rank;
+  D->pull = p;
+  D->ipc = true;
+  return WG_OK;
+}
+
+int wg_dist_status(wg_dist_t D, int32_t* timed_out) {
+  if (!D || !timed_out) return fail(WG_ERR_INVALID, "wg_dist_status: NULL argument");
+  *timed_out = 0;
+  if (!D->err) return WG_OK;
+  WG_HIP_TRY(hipDeviceSynchronize());
+  WG_HIP_TRY(hipMemcpy(timed_out, D->err, sizeof(int32_t), hipMemcpyDeviceToHost));
   return WG_OK;
 }
 

@@ -34,6 +34,16 @@ from . import _lib
 from ._lib import check, ptr
 
 
+def _trace(msg: str) -> None:
+    """Setup progress on stderr when WATS_DIST_LOG=1 (long multi-rank setups)."""
+    import os
+    import sys
+    import time
+    if os.environ.get("WATS_DIST_LOG") == "1":
+        print(f"[dist rank {os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr,
+              flush=True)
+
+
 def partition_rows(indptr: np.ndarray, world: int) -> np.ndarray:
     """Contiguous row blocks balanced by (nnz + rows): returns ``bounds`` of
     length world+1 with rank q owning rows [bounds[q], bounds[q+1])."""
@@ -104,18 +114,24 @@ def exchange_int_lists(lists: list, group=None) -> list:
     return [out[offs[q]:offs[q + 1]] for q in range(world)]
 
 
-def build_halo_plan(indptr_local: np.ndarray, indices_global: np.ndarray, bounds: np.ndarray, group=None) -> HaloPlan:
+def build_halo_plan(indptr_local: np.ndarray, indices_global, bounds: np.ndarray, group=None,
+                    compute_device=None) -> HaloPlan:
     """Renumber this rank's CSR columns to [own | halo] and agree with every
-    peer on who sends which rows (collective)."""
+    peer on who sends which rows (collective).  The column work (unique,
+    searchsorted over nnz entries) runs with torch on ``compute_device`` (the
+    GPU for large shards; default CPU)."""
     rank, world = _rank_world(group)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
-    cols = np.asarray(indices_global, dtype=np.int64)
+    dev = torch.device(compute_device) if compute_device is not None else torch.device("cpu")
+    cols = torch.as_tensor(np.asarray(indices_global) if not isinstance(indices_global, torch.Tensor)
+                           else indices_global).to(dev, torch.int64)
     own = (cols >= r0) & (cols < r1)
-    halo_global = np.unique(cols[~own])
+    remote = cols[~own]
+    halo_t = torch.unique(remote, sorted=True)
     n_own = r1 - r0
-    local = np.empty(cols.shape, dtype=np.int64)
-    local[own] = cols[own] - r0
-    local[~own] = n_own + np.searchsorted(halo_global, cols[~own])
+    local = cols - r0
+    local[~own] = n_own + torch.searchsorted(halo_t, remote)
+    halo_global = halo_t.cpu().numpy()
     owner = np.searchsorted(bounds, halo_global, side="right") - 1
     recv_lists = [halo_global[owner == q] for q in range(world)]
     requested = exchange_int_lists(recv_lists, group) if world > 1 else recv_lists  # what each peer needs from us
@@ -124,9 +140,9 @@ def build_halo_plan(indptr_local: np.ndarray, indices_global: np.ndarray, bounds
     plan = HaloPlan(rank=rank, world=world, bounds=np.asarray(bounds), r0=r0, r1=r1, n_halo=int(halo_global.size),
                     halo_global=halo_global, recv_counts=[int(len(x)) for x in recv_lists],
                     send_counts=[int(len(x)) for x in requested], send_rows=send_rows.astype(np.int32),
-                    local_indices=local.astype(np.int32))
-    plan.stats = dict(n_own=n_own, n_halo=plan.n_halo, nnz_local=int(cols.size),
-                      nnz_remote=int((~own).sum()), send_rows=int(send_rows.size))
+                    local_indices=local.to(torch.int32).cpu().numpy())
+    plan.stats = dict(n_own=n_own, n_halo=plan.n_halo, nnz_local=int(cols.numel()),
+                      nnz_remote=int(remote.numel()), send_rows=int(send_rows.size))
     return plan
 
 
@@ -171,6 +187,9 @@ class ShardedWavelet:
     ``exchange="rccl"`` (default): the whole chain in native code
     (``wg_dist_*``, ``csrc/dist.hip``): its own RCCL communicator, grouped
     ncclSend/ncclRecv per step, captured into a hipGraph and replayed.
+    ``exchange="ipc"``: the same native chain with a one-sided exchange: the
+    ranks' vectors mapped into each other by IPC, halo rows pulled straight
+    from the owners' memory, phases ordered by flags (``wg_dist_ipc_*``).
     ``exchange="nccl"``: the same exchange from Python, one
     ``torch.distributed.all_to_all_single`` per step (RCCL/xGMI).
     ``exchange="host"``: that collective on host copies (gloo) -- lets several
@@ -178,14 +197,16 @@ class ShardedWavelet:
     """
 
     def __init__(self, indptr_local, indices_global, values_local, n_global: int, bounds, group=None,
-                 exchange: str = "rccl", device=None):
+                 exchange: str = "rccl", device=None, max_features: int = 1):
         from .laplacian import NormalizedLaplacian, require_gpu
         self.device = require_gpu(device)
         self.group = group
         self.exchange = exchange
         indptr_local = np.asarray(indptr_local, np.int64)
-        self.plan = build_halo_plan(indptr_local, indices_global, bounds, group)
+        _trace("halo plan")
+        self.plan = build_halo_plan(indptr_local, indices_global, bounds, group, compute_device=self.device)
         p = self.plan
+        _trace(f"halo plan done ({p.n_halo} halo rows); column degrees")
         # partial column degrees of this shard, on the GPU (float64 atomics)
         lib = _lib.load()
         ip = torch.from_numpy(indptr_local).to(self.device)
@@ -199,8 +220,10 @@ class ShardedWavelet:
                                        ptr(colsum), ptr(diag), st), "column_degree")
         w_cols = global_column_degree(colsum, diag, p, group).to(self.device)
         del colsum, diag
+        _trace("column degrees done; operator")
         self.L = NormalizedLaplacian(p.n_own, ip, torch.from_numpy(p.local_indices), vals, n_cols=p.n_cols,
                                      w_cols=w_cols, device=self.device)
+        _trace("operator done")
         rows = torch.from_numpy(p.send_rows).to(self.device)
         self.send_rows = torch.empty_like(rows)
         if rows.numel():
@@ -213,8 +236,15 @@ class ShardedWavelet:
         self._dist = None
         if exchange == "rccl":
             self._dist = self._create_native()
+        elif exchange == "ipc":
+            # the shared region is sized for max_features columns (large IPC
+            # mappings are slow to set up: keep it to what the chain uses); a
+            # call with more columns rebuilds it (collective, like the call)
+            self._ipc_F = int(max_features)
+            self._dist = self._create_ipc(self._ipc_F)
         elif exchange not in ("nccl", "host"):
-            raise ValueError(f"exchange must be 'rccl', 'nccl' or 'host', not {exchange!r}")
+            raise ValueError(f"exchange must be 'rccl', 'ipc', 'nccl' or 'host', not {exchange!r}")
+        _trace("exchange ready")
 
     def _create_native(self):
         """The native chain's handle: RCCL unique id from rank 0, broadcast over
@@ -236,6 +266,49 @@ class ShardedWavelet:
                                      ptr(self.send_rows) if self.send_rows.numel() else None,
                                      sc.ctypes.data, rc.ctypes.data, ctypes.byref(h)), "dist_create")
         return h
+
+    def _create_ipc(self, max_features: int):
+        """The native chain with the one-sided exchange: every rank exposes its
+        ping-pong vectors by IPC and pulls its halo rows straight from the
+        owners' memory (no RCCL communicator).  Setup is collective over the
+        group (any backend, gloo included)."""
+        lib, p = _lib.load(), self.plan
+        sc = np.ascontiguousarray(p.send_counts, dtype=np.int64)
+        rc = np.ascontiguousarray(p.recv_counts, dtype=np.int64)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.wg_dist_create(self.L.handle, None, p.rank, p.world,
+                                     ptr(self.send_rows) if self.send_rows.numel() else None,
+                                     sc.ctypes.data, rc.ctypes.data, ctypes.byref(h)), "dist_create")
+            blob = (ctypes.c_uint8 * 128)()
+            check(lib.wg_dist_ipc_local(h, int(max_features), blob), "dist_ipc_local")
+        _trace("ipc region ready; exchanging handles")
+        # what each owner sends me = its internal ids of my halo rows, in my halo order
+        send_int = self.send_rows.cpu().numpy().astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(p.send_counts)]).astype(np.int64)
+        if p.world > 1:
+            blobs = [None] * p.world
+            dist.all_gather_object(blobs, bytes(blob), group=self.group)
+            src = exchange_int_lists([send_int[offs[q]:offs[q + 1]] for q in range(p.world)], self.group)
+        else:
+            blobs = [bytes(blob)]
+            src = [send_int]
+        halo_src = torch.from_numpy(np.concatenate(src).astype(np.int32) if p.n_halo else
+                                    np.zeros(1, np.int32)).to(self.device)
+        assert sum(len(x) for x in src) == p.n_halo
+        allb = (ctypes.c_uint8 * (128 * p.world)).from_buffer_copy(b"".join(blobs))
+        _trace("handles exchanged; mapping the peers' regions")
+        with torch.cuda.device(self.device):
+            check(lib.wg_dist_ipc_connect(h, allb, ptr(halo_src)), "dist_ipc_connect")
+        return h
+
+    def check_exchange(self) -> None:
+        """Raise if an IPC phase wait timed out (synchronises the device)."""
+        if self._dist is not None:
+            t = ctypes.c_int32(0)
+            check(_lib.load().wg_dist_status(self._dist, ctypes.byref(t)), "dist_status")
+            if t.value:
+                raise RuntimeError("wats_hip: a peer did not complete its phase within 60 s (IPC exchange)")
 
     def set_graph(self, enable: bool) -> None:
         """Replay the native chain as a hipGraph (default) or run it eagerly."""
@@ -362,6 +435,10 @@ class ShardedWavelet:
         L = self.L
         X = X0_local.to(self.device, torch.float32).reshape(p.n_own, -1).contiguous()
         F = X.shape[1]
+        if self.exchange == "ipc" and F > self._ipc_F:
+            self.close()
+            self._ipc_F = F
+            self._dist = self._create_ipc(F)
         if self._dist is not None and p.n_own:
             return self._wavelet_features_native(X, k, s, out)
         if F == 1 and k >= 1 and p.n_own and self.u_len() > 0:

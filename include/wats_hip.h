@@ -231,7 +231,7 @@ int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, 
  * keeps it eager; profiling via wg_profile_enable(L) also runs eagerly).
  * wg_dist_unique_id fills NCCL_UNIQUE_ID_BYTES (128) bytes on one rank; every
  * rank passes the same bytes to wg_dist_create (collective: blocks until all
- * ranks joined).  X0, S, H: own rows (n_rows, F) in the caller's order.
+ * ranks joined); unique_id NULL = no RCCL communicator (IPC exchange below).  X0, S, H: own rows (n_rows, F) in the caller's order.
  * ---------------------------------------------------------------------- */
 typedef struct wg_dist_s* wg_dist_t;
 int wg_dist_unique_id(void* id_out /* 128 bytes, host */);
@@ -242,9 +242,26 @@ int wg_dist_destroy(wg_dist_t D);
 int wg_dist_set_graph(wg_dist_t D, int32_t enable);
 int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K, double s, float* S,
                              float* H, void* stream);
-/* Total time (ms) and count of the halo exchanges (pack + RCCL) recorded
- * while profiling was enabled on the shard's handle; resets. */
+/* Total time (ms) and count of the halo exchanges (pack + RCCL, or the IPC
+ * pull) recorded while profiling was enabled on the shard's handle; resets. */
 int wg_dist_profile_collect(wg_dist_t D, double* exchange_ms_host, int64_t* count_host);
+
+/* One-sided exchange over IPC-mapped peer memory, instead of RCCL (create
+ * with unique_id = NULL).  wg_dist_ipc_local allocates this rank's shared
+ * region (two slots of the extended vector at up to F_max columns, or of the
+ * F = 1 LDS kernel's u, plus `world` int64 phase flags) and writes a 128-byte
+ * blob (IPC handle + layout); every rank gathers all blobs (rank order) and
+ * calls wg_dist_ipc_connect, with halo_src[h] = the owner's internal row id
+ * of halo row h (device int32, n_halo entries).  Per phase a rank waits until
+ * every peer completed as many phases as itself (flags written by the peers
+ * with system-scope stores), pulls its halo rows with system-scope loads
+ * from the owners' slots, runs the step and signals its peers.  A wait gives
+ * up after 60 s and sets a flag that wg_dist_status reports (it synchronises
+ * the device). */
+int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob_out /* 128 bytes, host */);
+int wg_dist_ipc_connect(wg_dist_t D, const void* blobs_host /* world x 128 bytes */,
+                        const int32_t* halo_src);
+int wg_dist_status(wg_dist_t D, int32_t* timed_out_host);
 
 /* -------------------------------------------------------------------------
  * Section 8(f)-2: the base model's propagation.  CompatibleGCN.forward

@@ -120,7 +120,7 @@ def test_sharded_chain_cpu_gloo(world, kind):
 
 
 # ------------------------------------------------------------------ GPU, ranks share one device
-def _gpu_worker(rank, world, port, kind, K, F, q, lds=2):
+def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -133,29 +133,42 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2):
         r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
         lo, hi = g.indptr[r0], g.indptr[r1]
         sw = ShardedWavelet(g.indptr[r0:r1 + 1] - lo, g.indices[lo:hi],
-                            None if g.values is None else g.values[lo:hi], g.n, bounds, exchange="host",
+                            None if g.values is None else g.values[lo:hi], g.n, bounds, exchange=exchange,
                             device="cuda:0")
         sw.L.tune(lds=lds)
         q_path = "u" if (F == 1 and sw.u_len() > 0) else "t"
         rng = np.random.default_rng(0)
         X = rng.standard_normal((g.n, F)).astype(np.float32)
-        H, S = sw.wavelet_features(torch.from_numpy(X[r0:r1]), k=K, s=0.8)
-        q.put((rank, S.cpu().numpy(), H.cpu().numpy(), q_path))
+        runs = 3 if exchange == "ipc" else 1   # ipc: eager, captured, replayed
+        outs = [sw.wavelet_features(torch.from_numpy(X[r0:r1]), k=K, s=0.8) for _ in range(runs)]
+        H, S = outs[0]
+        same = all(torch.equal(o[1], S) and torch.equal(o[0], H) for o in outs)
+        if exchange == "ipc":
+            sw.check_exchange()
+            sw.close()
+        q.put((rank, S.cpu().numpy(), H.cpu().numpy(), q_path, same))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,kind,F,lds", [(2, "rmat", 1, 2), (4, "rmat", 1, 2), (2, "rmat", 1, 0),
-                                              (3, "rmat", 40, 2), (2, "weighted", 4, 2), (2, "weighted", 1, 2)])
-def test_sharded_chain_gpu_multi_rank(world, kind, F, lds):
+@pytest.mark.parametrize("world,kind,F,lds,exchange", [
+    (2, "rmat", 1, 2, "host"), (4, "rmat", 1, 2, "host"), (2, "rmat", 1, 0, "host"), (3, "rmat", 40, 2, "host"),
+    (2, "weighted", 4, 2, "host"), (2, "weighted", 1, 2, "host"),
+    (2, "rmat", 1, 2, "ipc"), (4, "rmat", 1, 2, "ipc"), (2, "rmat", 1, 0, "ipc"), (3, "rmat", 40, 2, "ipc"),
+    (2, "weighted", 4, 2, "ipc"), (3, "weighted", 1, 2, "ipc")])
+def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange):
+    """Several ranks on one GPU: the Python exchange over gloo host copies, or
+    the native chain with the one-sided IPC exchange (ranks pull from each
+    other's memory; same-device IPC stands in for xGMI peers)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     K = 8
-    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, kind, K, F, q, lds)) for r in range(world)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, kind, K, F, q, lds, exchange))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
@@ -170,6 +183,7 @@ def test_sharded_chain_gpu_multi_rank(world, kind, F, lds):
     H = np.concatenate([r[2] for r in res])
     # F == 1 on an unweighted graph with lds on: the LDS kernel with the u halo exchange
     assert all(r[3] == ("u" if (F == 1 and kind == "rmat" and lds) else "t") for r in res)
+    assert all(r[4] for r in res), "repeated calls differ (graph capture / replay)"
     assert_parity(S, ref["S"], what=f"sharded world={world} S")
     if F > 1:
         assert_parity(H, ref["H"], what=f"sharded world={world} H")
