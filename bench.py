@@ -87,6 +87,21 @@ def algorithmic_bytes(n: int, nnz: int, F: int) -> int:
     return 8 * nnz + 4 * (n + 1) + 20 * n * F
 
 
+def _byte_model(info) -> str:
+    if not info:
+        return "SURVEY 8(d)"
+    if info["mode"] == 4:
+        return "hub teams (int32 ids, no values; DESIGN.md 4.5)"
+    return "lds (16-bit ids, no values; DESIGN.md 4.4)"
+
+
+def lds_kernel_name(info) -> str:
+    if not info:
+        return "cheb_step_kernel"
+    return {1: "cheb_lds1_kernel", 2: "cheb_lds3_kernel + combine_lds2_kernel",
+            4: "cheb_hub1_kernel"}.get(info["mode"], "lds mode %d" % info["mode"])
+
+
 def lds_algorithmic_bytes(info: dict) -> int:
     """Bytes one step of the F == 1 column-blocked LDS kernel must move
     (its entries carry 16-bit column ids and no values):
@@ -97,6 +112,8 @@ def lds_algorithmic_bytes(info: dict) -> int:
     the per-workgroup LDS fills are L2 hits).  Chunk padding is excluded here
     (it is real traffic, visible in the PMC `traffic`)."""
     n, nb, nnz, segs, cols = info["rows"], info["blocks"], info["nnz"], info["segments"], info["cols"]
+    if info["mode"] == 4:   # hub teams: the operator's int32 columns and row pointers, no values
+        return 4 * nnz + 4 * (n + 1) + 33 * n + 4 * cols
     if info["mode"] == 2:
         return 2 * nnz + 8 * segs + 4 * nb * n + 33 * n + 4 * cols
     return 2 * nnz + 4 * (nb * n + 1) + (8 * nb * n if nb > 1 else 0) + 33 * n + 4 * cols
@@ -183,8 +200,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     b_8d = algorithmic_bytes(p.n_own, sw.L.nnz, F)
     lds_info = sw.L.lds_plan_info(active_only=False) if (F == 1 and sw.u_len() > 0) else None
     b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
-    kernel = ("cheb_lds2_kernel + combine_lds2_kernel" if lds_info and lds_info["mode"] == 2 else
-              "cheb_lds1_kernel" if lds_info else "cheb_step_kernel") + " (rank 0 shard)"
+    kernel = lds_kernel_name(lds_info) + " (rank 0 shard)"
     avg_ms = prof["step_ms"]
     return {
         "metric": f"Chebyshev SpMM-chain edges*K/s ({config}-size, K={K}, row-sharded)",
@@ -214,7 +230,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                      "traffic": None, "kernel": kernel,
                      "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
                      "avg_exchange_us": prof["exchange_ms"] * 1e3,
-                     "byte_model": "lds (16-bit ids, no values; DESIGN.md 4.4)" if lds_info else "SURVEY 8(d)",
+                     "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
                      "nominal_8d_bytes": b_8d,
                      "nominal_8d_frac": (b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None},
@@ -281,8 +297,7 @@ def f1_companion(lib, L, K, s_heat, steps, device):
     b_step = lds_algorithmic_bytes(info) if info else algorithmic_bytes(n_active, L.nnz, 1)
     return {"F": 1, "signal": "log1p(rowsum) (WATS.py:58-59)", "value": float(L.nnz) * K / (ms * 1e-3),
             "unit": "edges*K/s", "ms_per_step": ms, "avg_launch_us": avg_ms * 1e3,
-            "kernel": ("cheb_lds3_kernel + combine_lds2_kernel" if info and info["mode"] == 2 else
-                       "cheb_lds1_kernel" if info else "cheb_step_kernel"),
+            "kernel": lds_kernel_name(info),
             "algorithmic_bytes_per_launch": b_step, "frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
@@ -429,9 +444,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": ("cheb_lds2_kernel + combine_lds2_kernel" if lds_info and lds_info["mode"] == 2 else
-                           "cheb_lds1_kernel" if lds_info else "cheb_step_kernel"),
-                "byte_model": "lds (16-bit ids, no values; DESIGN.md 4.4)" if lds_info else "SURVEY 8(d)",
+                "kernel": lds_kernel_name(lds_info),
+                "byte_model": _byte_model(lds_info),
                 "algorithmic_bytes_per_launch": b_step,
                 "rows_per_launch": n_active,
                 "closed_form_rows": n - n_active,

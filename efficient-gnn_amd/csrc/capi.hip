@@ -98,7 +98,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.seg_mask = value;
     return WG_OK;  // no replan
   } else if (!strcmp(key, "lds")) {
-    if (value < 0 || value > 3) return fail(WG_ERR_INVALID, "lds must be 0, 1, 2 or 3 (auto)");
+    if (value < 0 || value > 4) return fail(WG_ERR_INVALID, "lds must be 0, 1, 2, 3 (auto) or 4");
     L->tune.lds = (int32_t)value;
   } else if (!strcmp(key, "lds_cb")) {
     if (value < 32 || value > 40704) return fail(WG_ERR_INVALID, "lds_cb must be in [32, 40704]");
@@ -131,6 +131,8 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "lds_maxnb")) {
     L->tune.lds_maxnb = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 64));
+  } else if (!strcmp(key, "hub_iter")) {
+    L->tune.hub_iter = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;
   } else {
@@ -173,7 +175,7 @@ int wg_cheb_u_len(wg_laplacian_t L, int64_t* len) {
   *len = 0;
   Lds1Plan* lp = nullptr;
   if (int rc = get_lds1_plan(L, /*active_only=*/false, &lp)) return rc;
-  if (lp) *len = (int64_t)lp->lchunks * lp->nb * 32;
+  if (lp) *len = lp->u_floats();
   return WG_OK;
 }
 
@@ -233,7 +235,7 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   }
   // workspace: T ping-pong (2) + internal S [+ u ping-pong, padded to whole column blocks], 256-B aligned
   const size_t stride = ((size_t)n * F + 63) / 64 * 64;
-  const size_t ustride = lp ? ((size_t)lp->lchunks * lp->nb * 32 + 63) / 64 * 64 : 0;
+  const size_t ustride = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
   const size_t need = 3 * stride + 2 * ustride;
   if (L->ws_floats < need) {
     WG_HIP_TRY(hipStreamSynchronize(stream));

@@ -247,7 +247,7 @@ struct wg_dist_s {
     const size_t ext = ((size_t)n_cols * F + 63) / 64 * 64;
     const size_t own = ((size_t)n_own * F + 63) / 64 * 64;
     const size_t snd = ((size_t)std::max<int64_t>(n_send, 1) * F + 63) / 64 * 64;
-    const size_t ulen = lp ? ((size_t)lp->lchunks * lp->nb * 32 + 63) / 64 * 64 : 0;
+    const size_t ulen = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
     // lds: T ping-pong (own rows) + u ping-pong (padded column space); else T ping-pong over [own | halo]
     const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd;
     if (ws_floats < need) {
@@ -451,7 +451,7 @@ int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
   int64_t ulen = 0;
   Lds1Plan* lp = nullptr;
   if (int rc = get_lds1_plan(D->L, /*active_only=*/false, &lp)) return rc;
-  if (lp) ulen = (int64_t)lp->lchunks * lp->nb * 32;
+  if (lp) ulen = lp->u_floats();
   D->F_max = F_max;
   D->slot_floats = (std::max<int64_t>(D->n_cols * F_max, ulen) + 63) / 64 * 64;
   const size_t bytes = sizeof(float) * 2 * D->slot_floats + sizeof(int64_t) * D->world;

@@ -99,7 +99,9 @@ struct Lds1Plan {
   float* part = nullptr;      // device: teams [nb * n] block partial sums (nb > 1); windows [n_pairs]
   // mode 2 (windows): (row, block) segments padded to 8-id chunks, bit 15 of a
   // segment's first id flags its start; one wave streams a contiguous chunk range
-  int32_t mode = 1;           // 1 = row teams, 2 = chunk windows
+  int32_t mode = 1;           // 1 = row teams, 2 = chunk windows, 4 = hub teams
+  int32_t hub = 0;            // mode 4: columns [0, hub) in LDS, the rest gathered from u
+  int64_t ulen = 0;           // mode 4: floats of u (the column space, padded to 32)
   int64_t n_chunks = 0;
   int32_t n_pairs = 0;        // non-empty (row, block) segments
   uint4* chunk = nullptr;     // device [n_chunks]
@@ -108,6 +110,8 @@ struct Lds1Plan {
   int32_t* wblock = nullptr;  // device [n_wg]: column block of each workgroup
   std::string text;
   void release();
+  // floats of the gather vector u the kernel reads (padded column space)
+  int64_t u_floats() const { return mode == 4 ? ulen : (int64_t)lchunks * nb * 32; }
 };
 
 struct Tuning {
@@ -132,6 +136,7 @@ struct Tuning {
   int32_t lds_maxnb = 16;    // largest block count the LDS kernel takes (else the gather kernel)
   int32_t lds_depth = 2;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
   int32_t lds_k = 4;         // windows: chunks per lane (1 = cheb_lds2_kernel, 2 / 4 = cheb_lds3_kernel)
+  int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
 };
 

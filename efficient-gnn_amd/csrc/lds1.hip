@@ -47,6 +47,9 @@ constexpr int kLdsThreads = 1024;
 struct Lds1Args {
   const int32_t* brp;
   const uint16_t* bcol;
+  const int32_t* gcol;  // mode 4: the operator's int32 columns (internal, sorted per row)
+  int32_t hub;          // mode 4: columns [0, hub) staged in LDS, LDS slot hub = 0
+  int32_t u_bytes;      // mode 4: extent of u_in (raw-buffer gathers of the tail columns)
   const int2* groups;
   const int4* wgs;
   const float* u_in;   // u_{k-1}, n_cols (padded to a multiple of 32)
@@ -143,6 +146,74 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_lds1_kernel(Lds1Args a) {
     }
   }
 }
+
+// Mode 4, "hub teams": the column space does not fit LDS, but the rows are
+// short (the windows' padding would dominate).  The hub columns [0, hub) --
+// the highest-degree ones after relabelling, which receive most gathers
+// (ogbn-arxiv-size R-MAT: the top 32 768 columns take 93 %) -- are staged in
+// LDS; the tail columns are raw-buffer loads of u.  Branch-free: every entry
+// reads LDS slot min(c, hub) (slot hub holds 0) and issues a buffer load
+// whose offset is dropped (out of range -> 0, no memory request) for hub
+// columns, and the two are added (one of them is 0, so the sum is exact).
+// Row teams, row groups and the LDS counter as cheb_lds1_kernel; one column
+// block, so the epilogue runs in place.
+__global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
+  __shared__ int s_next;
+  constexpr uint32_t kDrop = 0x80000000u;
+  const int4 d = a.wgs[blockIdx.x];
+  const int H = a.hub;
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.u_in);
+    float4* dst = reinterpret_cast<float4*>(g_u_lds);
+    for (int i = threadIdx.x; i < H / 4; i += kLdsThreads) dst[i] = src[i];
+    if (threadIdx.x < 32) g_u_lds[H + threadIdx.x] = 0.0f;
+  }
+  if (threadIdx.x == 0) s_next = d.y;
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.u_in), 0, a.u_bytes, 0x00020000);
+  const int lane = threadIdx.x & 63;
+  const float* __restrict__ u = g_u_lds;
+  const int32_t* __restrict__ col = a.gcol;
+  const int32_t* __restrict__ rp = a.brp;
+  auto x_of = [&](int32_t c) {
+    const float xl = u[min(c, H)];
+    const uint32_t off = c >= H ? (uint32_t)c * 4u : kDrop;
+    const float xg = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+    return xl + xg;
+  };
+  for (;;) {
+    int g = 0;
+    if (lane == 0) g = atomicAdd(&s_next, 1);
+    g = __builtin_amdgcn_readfirstlane(__shfl(g, 0, 64));
+    if (g >= d.z) break;
+    const int2 gd = a.groups[g];
+    const int nrows = gd.y & 0xffff;
+    const int ln = gd.y >> 16;
+    const int sh = __ffs(ln) - 1;
+    const int team = lane >> sh;
+    const int q = lane & (ln - 1);
+    const int32_t row = gd.x + team;
+    const bool act = team < nrows;
+    double acc = 0.0;
+    if (act) {
+      const int32_t e1 = rp[row + 1];
+      int32_t e = rp[row] + q;
+      for (; e + 3 * ln < e1; e += 4 * ln) {
+        const int32_t c0 = col[e], c1 = col[e + ln], c2 = col[e + 2 * ln], c3 = col[e + 3 * ln];
+        const float x0 = x_of(c0), x1 = x_of(c1), x2 = x_of(c2), x3 = x_of(c3);
+        acc += (double)x0;
+        acc += (double)x1;
+        acc += (double)x2;
+        acc += (double)x3;
+      }
+      for (; e < e1; e += ln) acc += (double)x_of(col[e]);
+    }
+    for (int o = ln >> 1; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (act && q == 0) lds1_epilogue(a, row, acc);
+  }
+}
+
 
 __global__ __launch_bounds__(256) void combine_lds1_kernel(Lds1Args a) {
   const int32_t row = blockIdx.x * 256 + threadIdx.x;
@@ -590,6 +661,72 @@ int n_cus(int dev) {
   return cached[dev];
 }
 
+// row groups of the teams kernels (modes 1 and 4) and their workgroup split.
+// h: block-major row pointers [nb * n + 1] (entries of block b, row r =
+// [h[b*n+r], h[b*n+r+1])).
+int build_groups(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& h, int64_t nb, int32_t iter_knob) {
+  const int64_t n = p->n;
+  // row groups per block: 64/LN consecutive rows, LN lanes per row
+  const int iter = std::max(1, iter_knob);
+  std::vector<int2> groups;
+  std::vector<int64_t> gcost;  // entries + per-row overhead, for the workgroup split
+  std::vector<int64_t> bfirst(nb + 1);
+  for (int64_t b = 0; b < nb; ++b) {
+    bfirst[b] = (int64_t)groups.size();
+    const int32_t* r = h.data() + b * n;
+    auto len = [&](int64_t i) { return (int64_t)(r[i + 1] - r[i]); };
+    int64_t i = 0;
+    while (i < n) {
+      int ln = 1;
+      while (ln < 64 && (int64_t)ln * iter < len(i)) ln <<= 1;
+      int rows = (int)std::min<int64_t>(64 / ln, n - i);
+      // a longer row further in the group widens the team (rows are only roughly sorted per block)
+      for (;;) {
+        int64_t mx = 0;
+        for (int j = 0; j < rows; ++j) mx = std::max(mx, len(i + j));
+        if (ln >= 64 || mx <= 2 * (int64_t)ln * iter) break;
+        ln <<= 1;
+        rows = (int)std::min<int64_t>(64 / ln, n - i);
+      }
+      int64_t c = 16;
+      for (int j = 0; j < rows; ++j) c += len(i + j) + 2;
+      groups.push_back(make_int2((int32_t)i, rows | (ln << 16)));
+      gcost.push_back(c);
+      i += rows;
+    }
+  }
+  bfirst[nb] = (int64_t)groups.size();
+  p->n_groups = (int32_t)groups.size();
+  // workgroups: about one per CU, split evenly over the blocks, each block's
+  // groups cut into equal-cost contiguous ranges
+  int n_wg = L->tune.lds_wg > 0 ? L->tune.lds_wg : n_cus(L->device);
+  n_wg = (int)std::max<int64_t>(nb, std::min<int64_t>(n_wg, ceil_div(p->nnz + 2 * n, 4096)));
+  std::vector<int4> wgs;
+  for (int64_t b = 0; b < nb; ++b) {
+    const int m = (int)(n_wg / nb + (b < n_wg % nb ? 1 : 0));
+    int64_t tot = 0;
+    for (int64_t g = bfirst[b]; g < bfirst[b + 1]; ++g) tot += gcost[g];
+    int64_t g = bfirst[b], acc = 0;
+    for (int w = 0; w < m; ++w) {
+      const int64_t target = tot * (w + 1) / m;
+      const int64_t g0 = g;
+      while (g < bfirst[b + 1] && (acc + gcost[g] <= target || w == m - 1)) acc += gcost[g++];
+      if (g > g0 || w == m - 1) wgs.push_back(make_int4((int)b, (int)g0, (int)g, 0));
+    }
+  }
+  p->n_wg = (int32_t)wgs.size();
+  int rc = 0;
+  if ((rc = dmalloc(&p->groups, groups.size())) || (rc = dmalloc(&p->wgs, wgs.size())) ||
+      (rc = dmalloc(&p->part, nb > 1 ? (size_t)(nb * n) : 1)))
+    return rc;
+  WG_HIP_TRY(hipMemcpy(p->groups, groups.data(), sizeof(int2) * std::max<size_t>(1, groups.size()),
+                       hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipMemcpy(p->wgs, wgs.data(), sizeof(int4) * std::max<size_t>(1, wgs.size()), hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipDeviceSynchronize());
+  return WG_OK;
+}
+
+
 
 // mode 2 plan: segment chunk offsets, segment ids, chunk array, wave ranges.
 // `cnt` = entries per (block, row) (block-major), p->brp holds the same on the device.
@@ -743,12 +880,53 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
   int mode = L->tune.lds;
   int32_t nnz_rows = 0;
   if (n > 0) WG_HIP_TRY(hipMemcpy(&nnz_rows, L->rowptr + n, sizeof(int32_t), hipMemcpyDeviceToHost));
+  int32_t hub = std::max(32, std::min(40672, L->tune.lds_cb / 32 * 32));
   if (mode == 3) {
     const int64_t nb1 = ceil_div(ceil_div(std::max<int64_t>(n_cols, 1), 32), 40704 / 32);
-    mode = (nb1 == 1) ? 1 : (n > 0 && nnz_rows / n >= 64) ? 2 : 0;
+    // hub teams when every workgroup's entries outnumber the hub floats it stages 8 to 1
+    // (8M R-MAT K=32: 1219 vs 1645 us gather; ogbn-arxiv-size F=1: 12.5-15.8 vs 11.6 us)
+    const int64_t hub_auto = std::min<int64_t>(40672, (int64_t)nnz_rows / (8 * (int64_t)n_cus(L->device)) / 32 * 32);
+    if (nb1 == 1) {
+      mode = 1;
+    } else if (n > 0 && nnz_rows / n >= 64) {
+      mode = 2;
+    } else if (hub_auto >= 16384) {
+      mode = 4;
+      hub = (int32_t)hub_auto;
+    } else {
+      mode = 0;
+    }
   }
-  if (mode == 0) {
+  if (mode == 0 || n == 0 || (mode == 4 && (int64_t)n_cols * 4 >= ((int64_t)1 << 31))) {
     L->lds1_failed[slot] = true;
+    return WG_OK;
+  }
+  if (mode == 4) {
+    // hub teams: one "block" of the hub columns, the operator's own CSR
+    auto* p = new Lds1Plan();
+    p->mode = 4;
+    p->n = (int32_t)n;
+    p->n_cols = (int32_t)n_cols;
+    p->nb = 1;
+    p->nnz = nnz_rows;
+    const int64_t cols32 = ceil_div(std::max<int64_t>(n_cols, 1), 32) * 32;
+    p->hub = (int32_t)std::min<int64_t>(cols32, hub);
+    p->lchunks = p->hub / 32 + 1;  // + the zero slot (and padding)
+    p->ulen = cols32;
+    std::vector<int32_t> h(n + 1);
+    WG_HIP_TRY(hipMemcpy(h.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+    const int rc = build_groups(L, p, h, 1, L->tune.hub_iter);
+    if (rc) {
+      p->release();
+      delete p;
+      return rc;
+    }
+    char buf[256];
+    snprintf(buf, sizeof(buf), "lds1: hub teams rows=%lld cols=%lld nnz=%d hub=%d groups=%d workgroups=%d\n",
+             (long long)n, (long long)n_cols, nnz_rows, p->hub, p->n_groups, p->n_wg);
+    p->text = buf;
+    L->lds1[slot] = p;
+    *out = p;
     return WG_OK;
   }
   // + static LDS <= 160 KiB; windows: 15-bit local ids and a zero slot at 32 * lchunks
@@ -805,61 +983,7 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
                      p->bcol);
   WG_LAUNCH_CHECK();
 
-  // row groups per block: 64/LN consecutive rows, LN lanes per row
-  const int iter = std::max(1, L->tune.lds_iter);
-  std::vector<int2> groups;
-  std::vector<int64_t> gcost;  // entries + per-row overhead, for the workgroup split
-  std::vector<int64_t> bfirst(nb + 1);
-  for (int64_t b = 0; b < nb; ++b) {
-    bfirst[b] = (int64_t)groups.size();
-    const int32_t* r = h.data() + b * n;
-    auto len = [&](int64_t i) { return (int64_t)(r[i + 1] - r[i]); };
-    int64_t i = 0;
-    while (i < n) {
-      int ln = 1;
-      while (ln < 64 && (int64_t)ln * iter < len(i)) ln <<= 1;
-      int rows = (int)std::min<int64_t>(64 / ln, n - i);
-      // a longer row further in the group widens the team (rows are only roughly sorted per block)
-      for (;;) {
-        int64_t mx = 0;
-        for (int j = 0; j < rows; ++j) mx = std::max(mx, len(i + j));
-        if (ln >= 64 || mx <= 2 * (int64_t)ln * iter) break;
-        ln <<= 1;
-        rows = (int)std::min<int64_t>(64 / ln, n - i);
-      }
-      int64_t c = 16;
-      for (int j = 0; j < rows; ++j) c += len(i + j) + 2;
-      groups.push_back(make_int2((int32_t)i, rows | (ln << 16)));
-      gcost.push_back(c);
-      i += rows;
-    }
-  }
-  bfirst[nb] = (int64_t)groups.size();
-  p->n_groups = (int32_t)groups.size();
-  // workgroups: about one per CU, split evenly over the blocks, each block's
-  // groups cut into equal-cost contiguous ranges
-  int n_wg = L->tune.lds_wg > 0 ? L->tune.lds_wg : n_cus(L->device);
-  n_wg = (int)std::max<int64_t>(nb, std::min<int64_t>(n_wg, ceil_div(nnz + 2 * n, 4096)));
-  std::vector<int4> wgs;
-  for (int64_t b = 0; b < nb; ++b) {
-    const int m = (int)(n_wg / nb + (b < n_wg % nb ? 1 : 0));
-    int64_t tot = 0;
-    for (int64_t g = bfirst[b]; g < bfirst[b + 1]; ++g) tot += gcost[g];
-    int64_t g = bfirst[b], acc = 0;
-    for (int w = 0; w < m; ++w) {
-      const int64_t target = tot * (w + 1) / m;
-      const int64_t g0 = g;
-      while (g < bfirst[b + 1] && (acc + gcost[g] <= target || w == m - 1)) acc += gcost[g++];
-      if (g > g0 || w == m - 1) wgs.push_back(make_int4((int)b, (int)g0, (int)g, 0));
-    }
-  }
-  p->n_wg = (int32_t)wgs.size();
-  if ((rc = dmalloc(&p->groups, groups.size())) || (rc = dmalloc(&p->wgs, wgs.size())) ||
-      (rc = dmalloc(&p->part, nb > 1 ? (size_t)(nb * n) : 1)))
-    return bail(rc);
-  WG_HIP_TRY(hipMemcpy(p->groups, groups.data(), sizeof(int2) * std::max<size_t>(1, groups.size()),
-                       hipMemcpyHostToDevice));
-  WG_HIP_TRY(hipMemcpy(p->wgs, wgs.data(), sizeof(int4) * std::max<size_t>(1, wgs.size()), hipMemcpyHostToDevice));
+  if ((rc = build_groups(L, p, h, nb, L->tune.lds_iter))) return bail(rc);
   WG_HIP_TRY(hipDeviceSynchronize());
   char buf[256];
   snprintf(buf, sizeof(buf), "lds1: rows=%lld cols=%lld nnz=%d blocks=%lld lds_floats=%d groups=%d workgroups=%d%s\n",
@@ -905,6 +1029,21 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
   a.k = k;
   a.alpha0 = alpha0;
   a.alpha_k = alpha_k;
+  if (p->mode == 4) {
+    static bool attr4 = false;
+    if (!attr4) {
+      WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_hub1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 64));
+      attr4 = true;
+    }
+    a.brp = L->rowptr;
+    a.gcol = L->col;
+    a.hub = p->hub;
+    a.u_bytes = (int32_t)(p->ulen * 4);
+    hipLaunchKernelGGL(cheb_hub1_kernel, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
+    WG_LAUNCH_CHECK();
+    return prof_mark(L, stream, false);
+  }
   if (p->mode == 2) {
     const int depth = L->tune.lds_depth >= 8 ? 8 : L->tune.lds_depth >= 4 ? 4 : 2;
     const void* fn2 = depth == 8   ? (const void*)cheb_lds2_kernel<8>

@@ -156,7 +156,7 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host"):
     (2, "rmat", 1, 2, "host"), (4, "rmat", 1, 2, "host"), (2, "rmat", 1, 0, "host"), (3, "rmat", 40, 2, "host"),
     (2, "weighted", 4, 2, "host"), (2, "weighted", 1, 2, "host"),
     (2, "rmat", 1, 2, "ipc"), (4, "rmat", 1, 2, "ipc"), (2, "rmat", 1, 0, "ipc"), (3, "rmat", 40, 2, "ipc"),
-    (2, "weighted", 4, 2, "ipc"), (3, "weighted", 1, 2, "ipc")])
+    (2, "weighted", 4, 2, "ipc"), (3, "weighted", 1, 2, "ipc"), (2, "rmat", 1, 4, "ipc"), (2, "rmat", 1, 4, "host")])
 def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange):
     """Several ranks on one GPU: the Python exchange over gloo host copies, or
     the native chain with the one-sided IPC exchange (ranks pull from each
