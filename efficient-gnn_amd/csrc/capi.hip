@@ -233,8 +233,10 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     int rc0 = get_lds1_plan(L, /*active_only=*/true, &lp);
     if (rc0) return rc0;
   }
+  // internal width: F padded to a multiple of 4 (zero columns) for float4 lanes
+  const int64_t Fp = lp ? F : padded_features(F);
   // workspace: T ping-pong (2) + internal S [+ u ping-pong, padded to whole column blocks], 256-B aligned
-  const size_t stride = ((size_t)n * F + 63) / 64 * 64;
+  const size_t stride = ((size_t)n * Fp + 63) / 64 * 64;
   const size_t ustride = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
   const size_t need = 3 * stride + 2 * ustride;
   if (L->ws_floats < need) {
@@ -248,9 +250,9 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   float* b0 = L->ws;               // T_0, then T_2, T_4, ... (in place)
   float* b1 = L->ws + stride;      // T_1, T_3, ...
   float* sint = L->ws + 2 * stride;
-  int rc = launch_permute(L, 0, F, X0, b0, stream);
+  int rc = launch_permute_pad(L, F, Fp, X0, b0, stream);
   if (rc) return rc;
-  if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * F, hipMemcpyDeviceToDevice, stream));
+  if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * Fp, hipMemcpyDeviceToDevice, stream));
   // purely isolated rows (internal rows >= n_active) never enter the chain:
   // T_k = (-1)^k X0 exactly, so S = X0 * sum_k (-1)^k alpha_k (WATS.py:65-68)
   double coef = 0.0;
@@ -274,10 +276,10 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
     float* xk = (k == K) ? nullptr : ((k & 1) ? b1 : b0);  // T_K itself is never re-read
     const double ak = std::exp(-s * (double)k);             // WATS.py:65
-    rc = launch_step(L, k, F, xm1, xm2, xk, sint, nullptr, 1.0, ak, stream, /*active_only=*/true);
+    rc = launch_step(L, k, Fp, xm1, xm2, xk, sint, nullptr, 1.0, ak, stream, /*active_only=*/true);
     if (rc) return rc;
   }
-  return launch_finalize(L, F, sint, b0, coef, S, H, stream);
+  return launch_finalize(L, F, sint, b0, coef, S, H, stream, Fp);
 }
 
 int wg_profile_enable(wg_laplacian_t L, int32_t enable) {

@@ -244,9 +244,10 @@ struct wg_dist_s {
     Lds1Plan* lp = nullptr;
     if (F == 1 && K >= 1)
       if (int rc = get_lds1_plan(L, /*active_only=*/false, &lp)) return rc;
-    const size_t ext = ((size_t)n_cols * F + 63) / 64 * 64;
-    const size_t own = ((size_t)n_own * F + 63) / 64 * 64;
-    const size_t snd = ((size_t)std::max<int64_t>(n_send, 1) * F + 63) / 64 * 64;
+    const int64_t Fp = lp ? F : padded_features(F);  // internal width (zero pad columns, float4 lanes)
+    const size_t ext = ((size_t)n_cols * Fp + 63) / 64 * 64;
+    const size_t own = ((size_t)n_own * Fp + 63) / 64 * 64;
+    const size_t snd = ((size_t)std::max<int64_t>(n_send, 1) * Fp + 63) / 64 * 64;
     const size_t ulen = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
     // lds: T ping-pong (own rows) + u ping-pong (padded column space); else T ping-pong over [own | halo]
     const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd;
@@ -298,21 +299,21 @@ struct wg_dist_s {
     float* sendbuf = take(snd);
     int rc = WG_OK;
     if (sig) rc = ipc_wait_only(st);
-    if (!rc) rc = launch_permute(L, 0, F, X0, A[0], st);
+    if (!rc) rc = launch_permute_pad(L, F, Fp, X0, A[0], st);
     if (!rc && sig) rc = ipc_signal(st);
     if (!rc && K == 0)
-      rc = hipMemcpyAsync(sint, A[0], sizeof(float) * n_own * F, hipMemcpyDeviceToDevice, st) == hipSuccess
+      rc = hipMemcpyAsync(sint, A[0], sizeof(float) * n_own * Fp, hipMemcpyDeviceToDevice, st) == hipSuccess
                ? WG_OK
                : fail(WG_ERR_HIP, "wg_dist: copy");
     for (int32_t k = 1; k <= K && !rc; ++k) {
       float* cur = A[(k - 1) & 1];
-      rc = exchange(cur, sendbuf, F, st, (k - 1) & 1);
+      rc = exchange(cur, sendbuf, Fp, st, (k - 1) & 1);
       if (!rc)
-        rc = launch_step(L, k, F, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
+        rc = launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
                          std::exp(-s * (double)k), st);
       if (!rc && sig) rc = ipc_signal(st);
     }
-    if (!rc) rc = launch_finalize(L, F, sint, nullptr, 0.0, S, H, st);
+    if (!rc) rc = launch_finalize(L, F, sint, nullptr, 0.0, S, H, st, Fp);
     return rc;
   }
 };
@@ -453,7 +454,7 @@ int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
   if (int rc = get_lds1_plan(D->L, /*active_only=*/false, &lp)) return rc;
   if (lp) ulen = lp->u_floats();
   D->F_max = F_max;
-  D->slot_floats = (std::max<int64_t>(D->n_cols * F_max, ulen) + 63) / 64 * 64;
+  D->slot_floats = (std::max<int64_t>(D->n_cols * padded_features(F_max), ulen) + 63) / 64 * 64;
   const size_t bytes = sizeof(float) * 2 * D->slot_floats + sizeof(int64_t) * D->world;
   if (int rc = dmalloc(reinterpret_cast<char**>(&D->region), bytes)) return rc;
   if (int rc = dmalloc(&D->count, 1)) return rc;

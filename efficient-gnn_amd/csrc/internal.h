@@ -188,7 +188,13 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out);
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false);
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef,
-                    float* S, float* H, hipStream_t stream);
+                    float* S, float* H, hipStream_t stream, int64_t ldi = 0);  // ldi: internal row stride (0 = F)
+// the internal signal width of an F-column chain: odd / 4-unaligned F >= 3 is
+// padded to a multiple of 4 (zero columns), so the step kernel runs float4
+// lanes (Reddit-size F = 41: 5383 -> 1878 us per step as F = 44)
+int padded_features(int64_t F);
+// caller rows (stride F) -> internal rows (stride Fp), pad columns zeroed
+int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);
 int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start);

@@ -660,7 +660,8 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
 // Rows >= closed_from are purely isolated (T_k = (-1)^k X0): S = coef * X0
 // with coef = sum_k (-1)^k alpha_k, read from the untouched T_0 rows.
 template <int VEC>
-__global__ __launch_bounds__(kBlock) void finalize_kernel(int64_t n, int64_t F, int LF, const int32_t* __restrict__ perm,
+__global__ __launch_bounds__(kBlock) void finalize_kernel(int64_t n, int64_t F, int64_t ldi, int LF,
+                                                          const int32_t* __restrict__ perm,
                                                           const float* __restrict__ Sint, const float* __restrict__ X0int,
                                                           int64_t closed_from, double coef, float* __restrict__ S,
                                                           float* __restrict__ H) {
@@ -675,7 +676,7 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(int64_t n, int64_t F, 
   double s[VEC];
   double part = 0.0;
   if (active) {
-    load_vec<VEC>((closed ? X0int : Sint) + row * F + fs * VEC, x);
+    load_vec<VEC>((closed ? X0int : Sint) + row * ldi + fs * VEC, x);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       s[j] = closed ? coef * (double)x[j] : (double)x[j];
@@ -695,7 +696,8 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(int64_t n, int64_t F, 
 }
 
 // wide-F fallback (F > 64*VEC): wave per row.
-__global__ __launch_bounds__(kBlock) void finalize_wide_kernel(int64_t n, int64_t F, const int32_t* __restrict__ perm,
+__global__ __launch_bounds__(kBlock) void finalize_wide_kernel(int64_t n, int64_t F, int64_t ldi,
+                                                               const int32_t* __restrict__ perm,
                                                                const float* __restrict__ Sint,
                                                                const float* __restrict__ X0int, int64_t closed_from,
                                                                double coef, float* __restrict__ S,
@@ -708,11 +710,11 @@ __global__ __launch_bounds__(kBlock) void finalize_wide_kernel(int64_t n, int64_
   const float* src = closed ? X0int : Sint;
   const double c = closed ? coef : 1.0;
   double part = 0.0;
-  for (int64_t f = lane; f < F; f += 64) part += fabs(c * (double)src[row * F + f]);
+  for (int64_t f = lane; f < F; f += 64) part += fabs(c * (double)src[row * ldi + f]);
   for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off, 64);
   const double den = part + 1e-8;
   for (int64_t f = lane; f < F; f += 64) {
-    const double s = c * (double)src[row * F + f];
+    const double s = c * (double)src[row * ldi + f];
     if (S) S[r * F + f] = (float)s;
     if (H) H[r * F + f] = (float)(s / den);
   }
@@ -737,6 +739,16 @@ __global__ __launch_bounds__(kBlock) void permute_kernel(int64_t n, int64_t F, i
 #pragma unroll
   for (int j = 0; j < VEC; ++j) y[j] = x[j];
   store_vec<VEC>(dst + di, y);
+}
+
+// caller rows (stride F) -> internal rows (stride Fp > F), the Fp - F pad columns zeroed
+__global__ void permute_pad_kernel(int64_t n, int64_t F, int64_t Fp, const int32_t* __restrict__ perm,
+                                   const float* __restrict__ src, float* __restrict__ dst) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * Fp) return;
+  const int64_t i = idx / Fp;
+  const int64_t f = idx - i * Fp;
+  dst[idx] = f < F ? src[(int64_t)perm[i] * F + f] : 0.0f;
 }
 
 __global__ void permute_wide_kernel(int64_t n, int64_t F, const int32_t* __restrict__ perm, int direction,
@@ -1106,27 +1118,29 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
 }
 
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef, float* S,
-                    float* H, hipStream_t stream) {
+                    float* H, hipStream_t stream, int64_t ldi) {
   const int64_t closed_from = X0int ? L->n_active : L->n_rows;
   const int64_t n = L->n_rows;
   if (n == 0) return WG_OK;
-  const int vec = pick_vec(F, {Sint, X0int, S, H});
+  if (ldi <= 0) ldi = F;
+  int vec = pick_vec(F, {Sint, X0int, S, H});
+  while (vec > 1 && ldi % vec) vec >>= 1;
   if (F <= 64 * vec) {
     const int LF = (int)(F / vec);
     const int G = 64 / LF;
     const dim3 grid((unsigned)ceil_div(n, 4 * G));
     if (vec == 4)
-      hipLaunchKernelGGL(finalize_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, X0int, closed_from,
-                         closed_coef, S, H);
+      hipLaunchKernelGGL(finalize_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, ldi, LF, L->perm, Sint, X0int,
+                         closed_from, closed_coef, S, H);
     else if (vec == 2)
-      hipLaunchKernelGGL(finalize_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, X0int, closed_from,
-                         closed_coef, S, H);
+      hipLaunchKernelGGL(finalize_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, ldi, LF, L->perm, Sint, X0int,
+                         closed_from, closed_coef, S, H);
     else
-      hipLaunchKernelGGL(finalize_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, Sint, X0int, closed_from,
-                         closed_coef, S, H);
+      hipLaunchKernelGGL(finalize_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, ldi, LF, L->perm, Sint, X0int,
+                         closed_from, closed_coef, S, H);
   } else {
-    hipLaunchKernelGGL(finalize_wide_kernel, dim3(ceil_div(n, 4)), dim3(kBlock), 0, stream, n, F, L->perm, Sint, X0int,
-                       closed_from, closed_coef, S, H);
+    hipLaunchKernelGGL(finalize_wide_kernel, dim3(ceil_div(n, 4)), dim3(kBlock), 0, stream, n, F, ldi, L->perm, Sint,
+                       X0int, closed_from, closed_coef, S, H);
   }
   WG_LAUNCH_CHECK();
   return WG_OK;
@@ -1150,6 +1164,18 @@ int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src
   WG_LAUNCH_CHECK();
   return WG_OK;
 }
+
+int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream) {
+  const int64_t n = L->n_rows;
+  if (n == 0) return WG_OK;
+  if (Fp == F) return launch_permute(L, 0, F, src, dst, stream);
+  hipLaunchKernelGGL(permute_pad_kernel, dim3((unsigned)ceil_div(n * Fp, 256)), dim3(256), 0, stream, n, F, Fp, L->perm,
+                     src, dst);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
+int padded_features(int64_t F) { return (int)((F >= 3 && F % 4) ? (F + 3) / 4 * 4 : F); }
 
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream) {
   hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(n, 4)), dim3(kBlock), 0, stream, n, F, S, H);
