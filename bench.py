@@ -193,6 +193,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     sw.profile_start()
     run()
     prof = sw.profile_collect()
+    kat = _eigen_kat_sharded(sw, indptr, r0, r1, F, K, s_heat, world, device)
     if world > 1:
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
     nnz_lhat = _allreduce(float(sw.L.nnz), dist.ReduceOp.SUM, device) if world > 1 else float(sw.L.nnz)
@@ -233,6 +234,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                      "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
                      "nominal_8d_bytes": b_8d,
+                     "eigen_kat": kat,
                      "nominal_8d_frac": (b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None},
     }
 
@@ -299,6 +301,34 @@ def f1_companion(lib, L, K, s_heat, steps, device):
             "unit": "edges*K/s", "ms_per_step": ms, "avg_launch_us": avg_ms * 1e3,
             "kernel": lds_kernel_name(info),
             "algorithmic_bytes_per_launch": b_step, "frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
+def _kat_signal(deg: np.ndarray, F: int) -> np.ndarray:
+    """Columns that are multiples of v = sqrt(w): for a symmetric graph without
+    self loops w = degree, and L_hat v = -v (eigenvector
+    KAT), so T_k = (-1)^k X0 and S = X0 * sum_k (-1)^k exp(-s k) exactly."""
+    v = np.sqrt(deg.astype(np.float64))
+    return (v[:, None] * (1.0 + 0.125 * np.arange(F))[None, :]).astype(np.float32)
+
+
+def _kat_coef(K: int, s_heat: float) -> float:
+    return float(sum(((-1.0) ** i) * np.exp(-s_heat * i) for i in range(K + 1)))
+
+
+def _eigen_kat_sharded(sw, indptr, r0, r1, F, K, s_heat, world, device) -> dict:
+    """Full-size parity check of the sharded chain (no oracle can run at this
+    size): the eigenvector KAT on every rank's rows, max error over ranks."""
+    X = torch.from_numpy(_kat_signal(np.diff(indptr)[r0:r1], F)).to(device)
+    _, S = sw.wavelet_features(X, k=K, s=s_heat)
+    expect = X.double() * _kat_coef(K, s_heat)
+    err = float((S.double() - expect).abs().max()) if S.numel() else 0.0
+    scale = float(expect.abs().max()) if S.numel() else 0.0
+    if world > 1:
+        err = _allreduce(err, dist.ReduceOp.MAX, device)
+        scale = _allreduce(scale, dist.ReduceOp.MAX, device)
+    rel = err / scale if scale else 0.0
+    return {"max_rel_err": rel, "tol": 1e-5, "ok": rel <= 1e-5,
+            "what": "X0 = sqrt(degree) x column scales; S must equal X0 * sum_k (-1)^k e^{-sk} (every rank, max)"}
 
 
 def sharded_main(args, world, rank, device):
@@ -395,6 +425,13 @@ def main():
     elapsed_prof, prof, _ = timed(True)
     _log(f"main: timed {args.steps} passes in {elapsed:.3f} s; cold / F=1 companion")
     cold = cold_chains(step, L, args.cold_reps, device) if args.cold_reps > 0 else None
+    # full-size parity check of the benchmarked pass (eigenvector KAT, all F columns)
+    Xk = torch.from_numpy(_kat_signal(np.diff(g.indptr), F)).to(device)
+    wats_hip._lib.check(lib.wg_wavelet_features(L.handle, Xk.data_ptr(), F, K, args.s, S.data_ptr(), H.data_ptr(),
+                                                stream), "wavelet_features")
+    expect = Xk.double() * _kat_coef(K, args.s)
+    kat_rel = float((S.double() - expect).abs().max() / expect.abs().max())
+    del Xk, expect
     f1 = None
     if args.f1_companion and F > 1:
         f1 = f1_companion(lib, L, K, args.s, args.steps, device)
@@ -461,6 +498,9 @@ def main():
             "timing": "value / ms_per_step: K passes without per-launch events; roofline: the same K passes "
                       "timed right after with HIP events around every step-kernel launch (ms_per_step_profiled)",
             "edges_K_F_per_s": edges_k * F / elapsed,
+            "eigen_kat": {"max_rel_err": kat_rel, "tol": 1e-5, "ok": kat_rel <= 1e-5,
+                          "what": "the benchmarked graph, K and F with X0 = sqrt(degree) x column scales: "
+                                  "S must equal X0 * sum_k (-1)^k e^{-sk}"},
         }
         if cold is not None:
             cold["edges_K_per_s"] = float(nnz) * K / (cold["step_ms"] * 1e-3)
