@@ -41,10 +41,12 @@ if [ "${RUN_PMC:-0}" = 1 ]; then
   for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
     tag=$(echo $ctr | cut -d' ' -f1)
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/$OUT/pmc_$tag" -o run -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --sharded-extra none > "$OUT/pmc_$tag.log" 2>&1
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --sharded-extra none --cold-reps 0 --f1-companion 0 \
+        > "$OUT/pmc_$tag.log" 2>&1
     stop_if_fatal $? "pmc $tag"
   done
-  python tools/pmc_traffic.py "$OUT"/pmc_* --out "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
+  python tools/pmc_traffic.py --kernel "cheb_step_kernel<4, true" "$OUT"/pmc_* --out "$OUT/traffic.json" \
+      > "$OUT/traffic.log" 2>&1
   timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --sharded-extra none --traffic-json "$OUT/traffic.json" \
       --out "$OUT/bench_traffic.json" > "$OUT/bench_traffic.log" 2>&1
   stop_if_fatal $? bench_traffic

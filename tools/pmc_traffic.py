@@ -1,6 +1,8 @@
 """Per-launch HBM traffic of one kernel from rocprofv3 --pmc passes.
 
-Usage: python tools/pmc_traffic.py --kernel cheb_step_kernel DIR [DIR ...] [--out traffic.json]
+Usage: python tools/pmc_traffic.py --kernel "cheb_step_kernel<4, true" DIR [DIR ...] [--out traffic.json]
+(--kernel is a substring of the kernel name: make it specific enough to pick
+one instantiation -- the bench's F = 1 companion runs cheb_step_kernel<1, ...>)
 
 Each DIR is the -d output of one `rocprofv3 --pmc <counters> --output-format csv`
 pass (FETCH_SIZE and WRITE_SIZE must be collected in separate passes on gfx950:
