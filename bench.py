@@ -58,8 +58,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
-    ap.add_argument("--traffic-json", default=None,
-                    help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py)")
+    ap.add_argument("--traffic-json", default="auto",
+                    help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py); "
+                         "'auto': the committed PMC summary of the default workload (profiles/r01/s17_traffic.json, "
+                         "tools/gpu_session.sh RUN_PMC=1) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--sharded-extra", default="reddit,rmat-8m",
                     help="comma-separated configs also measured row-sharded over all ranks (RCCL halo exchange), "
@@ -450,9 +452,14 @@ def main():
         lds_info = L.lds_plan_info(active_only=True) if F == 1 else None
         b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
         achieved = b_step / (avg_ms * 1e-3) / 1e9
-        traffic = None
-        if args.traffic_json and os.path.exists(args.traffic_json):
-            traffic = json.load(open(args.traffic_json)).get("bytes_per_launch")
+        traffic, traffic_src = None, None
+        tj = args.traffic_json
+        if tj == "auto":
+            tj = os.path.join(REPO, "profiles", "r01", "s17_traffic.json") \
+                if (args.config == "ogbn-arxiv" and F == 40 and K == 16) else None
+        if tj and tj != "none" and os.path.exists(tj):
+            traffic = json.load(open(tj)).get("bytes_per_launch")
+            traffic_src = os.path.relpath(tj, REPO) if os.path.isabs(tj) else tj
         line = {
             "metric": "Chebyshev SpMM-chain edges*K/s (ogbn-arxiv-size, K=16) + %HBM roofline",
             "value": edges_k / elapsed,
@@ -481,6 +488,9 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction: "
+                                   f"an upper bound) + WRITE_SIZE per launch of this kernel on this workload"
+                                   if traffic is not None else None),
                 "kernel": lds_kernel_name(lds_info),
                 "byte_model": _byte_model(lds_info),
                 "algorithmic_bytes_per_launch": b_step,
