@@ -890,7 +890,9 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
       mode = 1;
     } else if (n > 0 && nnz_rows / n >= 64) {
       mode = 2;
-    } else if (hub_auto >= 16384) {
+    } else if (hub_auto >= 16384 && L->n_cols == L->n_rows) {
+      // (row shards: the hub would be the shard's own highest-degree columns, but most
+      // gathers go to halo columns, which are not degree-ordered -> gather kernel)
       mode = 4;
       hub = (int32_t)hub_auto;
     } else {
