@@ -392,6 +392,13 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
 int wg_dist_destroy(wg_dist_t D) {
   if (!D) return WG_OK;
   (void)hipDeviceSynchronize();
+  if (D->ipc && D->world > 1 && D->cap) {
+    // peers may still pull from this rank's region in their last phase: wait until
+    // every peer has completed as many phases as this rank (its last write here is
+    // its final signal), then unmap and free.  A lost peer times out (60 s).
+    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, D->cap, D->pull);
+    (void)hipStreamSynchronize(D->cap);
+  }
   delete D;
   return WG_OK;
 }
