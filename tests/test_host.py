@@ -164,3 +164,23 @@ def test_sparse_gcn_state_dict_matches_reference_layout():
     assert set(a.state_dict()) == set(b.state_dict())
     b.load_state_dict(a.state_dict())
     assert wats_hip.SparseCompatibleGCN(4, dataset_name="ogbn-arxiv").gc2.out_features == 40
+
+
+def test_c_abi_header_is_plain_c_and_links(tmp_path):
+    """The boundary as a C99 program sees it: include/wats_hip.h compiles with
+    gcc -std=c99 -Wall -Werror (and as C++), the program links against the
+    library and its argument-validation paths run without a GPU."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    src = os.path.join(REPO, "tests", "c", "abi_check.c")
+    exe = str(tmp_path / "abi_check")
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"), src,
+                    "-L", libdir, "-lwats_hip", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-fsyntax-only", "-x", "c++", "-I",
+                    os.path.join(REPO, "include"), src], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.startswith("ok")
