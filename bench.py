@@ -407,24 +407,27 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-        evs[0].record()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if profile else None
+        if evs:
+            evs[0].record()
         for i in range(args.steps):
             step()
-            evs[i + 1].record()
+            if evs:
+                evs[i + 1].record()
         torch.cuda.synchronize(device)
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
         prof = L.profile_collect() if profile else None
         L.profile_enable(False)
-        ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+        ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) if evs else []
         return t1 - t0, prof, ms[len(ms) // 2] if ms else None
 
-    # value: the passes alone (per-launch events add ~4.5 us of gap each, 10 % of
-    # an arxiv F=40 pass); roofline: the same K passes again, with the events
-    elapsed, _, median_ms = timed(False)
-    elapsed_prof, prof, _ = timed(True)
+    # value: the passes alone, no events at all (per-launch events add ~4.5 us of
+    # gap each, 10 % of an arxiv F=40 pass); roofline and the per-pass median:
+    # the same K passes again, with events around every step launch and pass
+    elapsed, _, _ = timed(False)
+    elapsed_prof, prof, median_ms = timed(True)
     _log(f"main: timed {args.steps} passes in {elapsed:.3f} s; cold / F=1 companion")
     cold = cold_chains(step, L, args.cold_reps, device) if args.cold_reps > 0 else None
     # full-size parity check of the benchmarked pass (eigenvector KAT, all F columns)
@@ -503,7 +506,7 @@ def main():
                 "launches": prof["launches"],
             },
             "chain_ms": prof["sum_ms"] / args.steps,
-            "median_step_ms": median_ms,
+            "median_step_ms_profiled": median_ms,
             "ms_per_step_profiled": elapsed_prof / args.steps * 1e3,
             "timing": "value / ms_per_step: K passes without per-launch events; roofline: the same K passes "
                       "timed right after with HIP events around every step-kernel launch (ms_per_step_profiled)",
