@@ -131,6 +131,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "lds_maxnb")) {
     L->tune.lds_maxnb = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 64));
+  } else if (!strcmp(key, "fuse_finalize")) {
+    L->tune.fuse_finalize = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hub_iter")) {
     L->tune.hub_iter = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
   } else if (!strcmp(key, "lds_perm")) {
@@ -250,13 +253,18 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   float* b0 = L->ws;               // T_0, then T_2, T_4, ... (in place)
   float* b1 = L->ws + stride;      // T_1, T_3, ...
   float* sint = L->ws + 2 * stride;
-  int rc = launch_permute_pad(L, F, Fp, X0, b0, stream);
-  if (rc) return rc;
-  if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * Fp, hipMemcpyDeviceToDevice, stream));
   // purely isolated rows (internal rows >= n_active) never enter the chain:
   // T_k = (-1)^k X0 exactly, so S = X0 * sum_k (-1)^k alpha_k (WATS.py:65-68)
   double coef = 0.0;
   for (int32_t k = 0; k <= K; ++k) coef += ((k & 1) ? -1.0 : 1.0) * std::exp(-s * (double)k);
+  // finalize fused: the permute-in finishes the closed-form rows, the last step
+  // writes S and H in the caller's order (no separate finalize pass)
+  const bool fuse_fin = !lp && L->tune.fuse_finalize && Fp == F && K >= 1 && S && H &&
+                        step_single_tile(L, F, {b0, b1, sint, S, H});
+  int rc = fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, stream)
+                    : launch_permute_pad(L, F, Fp, X0, b0, stream);
+  if (rc) return rc;
+  if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * Fp, hipMemcpyDeviceToDevice, stream));
   if (lp) {
     float* u[2] = {L->ws + 3 * stride, L->ws + 3 * stride + ustride};  // u_{k-1} = T_{k-1} * dinv
     rc = launch_scale_dinv(L, lp->n, b0, u[0], stream);
@@ -276,9 +284,12 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
     float* xk = (k == K) ? nullptr : ((k & 1) ? b1 : b0);  // T_K itself is never re-read
     const double ak = std::exp(-s * (double)k);             // WATS.py:65
-    rc = launch_step(L, k, Fp, xm1, xm2, xk, sint, nullptr, 1.0, ak, stream, /*active_only=*/true);
+    const bool last_fused = fuse_fin && k == K;
+    rc = launch_step(L, k, Fp, xm1, xm2, xk, sint, last_fused ? H : nullptr, 1.0, ak, stream, /*active_only=*/true,
+                     last_fused ? S : nullptr);
     if (rc) return rc;
   }
+  if (fuse_fin) return WG_OK;
   return launch_finalize(L, F, sint, b0, coef, S, H, stream, Fp);
 }
 

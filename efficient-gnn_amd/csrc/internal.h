@@ -136,6 +136,7 @@ struct Tuning {
   int32_t lds_maxnb = 16;    // largest block count the LDS kernel takes (else the gather kernel)
   int32_t lds_depth = 2;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
   int32_t lds_k = 4;         // windows: chunks per lane (1 = cheb_lds2_kernel, 2 / 4 = cheb_lds3_kernel)
+  int32_t fuse_finalize = 1;  // wavelet_features: closed rows in the permute-in, S / H from the last step
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
 };
@@ -185,14 +186,22 @@ int sort_row_columns(wg_laplacian_s* L, hipStream_t stream);
 // step.hip
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out);
+// S_out (finalize fused into the last step; needs S, H and F within one tile):
+// the rows' final S and H go to caller row perm[row] of S_out / H
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
-                float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false);
+                float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
+                float* S_out = nullptr);
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef,
                     float* S, float* H, hipStream_t stream, int64_t ldi = 0);  // ldi: internal row stride (0 = F)
 // the internal signal width of an F-column chain: odd / 4-unaligned F >= 3 is
 // padded to a multiple of 4 (zero columns), so the step kernel runs float4
 // lanes (Reddit-size F = 41: 5383 -> 1878 us per step as F = 44)
 int padded_features(int64_t F);
+// launch_step would run F columns as one tile (the condition for a fused H / finalize)
+bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const void*> ptrs);
+// permute-in that also writes the closed-form rows' S and H in the caller's order
+int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
+                             float* H, hipStream_t stream);
 // caller rows (stride F) -> internal rows (stride Fp), pad columns zeroed
 int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);

@@ -40,6 +40,8 @@ struct StepArgs {
   float* xk;          // T_k (nullable)
   float* S;           // heat-kernel sum (nullable)
   float* H;           // normalised output (nullable; only when the tile covers all F)
+  const int32_t* out_perm;  // last step, finalize fused: S / H rows go to caller row out_perm[row] ...
+  float* S_out;             // ... of S_out / H (internal S is only read)
   int64_t ld;         // row stride (floats) of every vector
   int32_t LF;         // lanes across the tile's columns (tile width = LF * VEC)
   int32_t k;          // step index (1 or >= 2)
@@ -105,12 +107,14 @@ struct EpiIn {
   float prev[VEC];  // k == 1: T_0 own row (for S); k >= 2: T_{k-2} own row
   float sold[VEC];  // S own row (k >= 2)
   int iso;
+  int32_t orow;     // out_perm[row] (finalize fused into the last step)
 };
 
 template <int VEC>
 __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int fs, EpiIn<VEC>& in) {
   const int64_t off = row * a.ld + (int64_t)fs * VEC;
   in.iso = a.iso[row];
+  in.orow = a.out_perm ? a.out_perm[row] : (int32_t)row;
   load_vec<VEC>((a.k == 1 ? a.xm1 : a.xm2) + off, in.prev);
   if (a.S && a.k >= 2) load_vec<VEC>(a.S + off, in.sold);
 }
@@ -146,8 +150,11 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
 #pragma unroll
     for (int j = 0; j < VEC; ++j)  // k == 1: S = alpha0*T_0 + alpha1*T_1
       s[j] = (a.k == 1) ? a.alpha0 * (double)in.prev[j] + a.alpha_k * t[j] : (double)in.sold[j] + a.alpha_k * t[j];
-    if (nt_st) store_vec_nt<VEC>(a.S + off, s);
-    else store_vec<VEC>(a.S + off, s);
+    // finalize fused (last step): the rows go straight to the caller's order
+    const int64_t oo = a.out_perm ? (int64_t)in.orow * a.ld + (int64_t)fs * VEC : off;
+    float* Sd = a.out_perm ? a.S_out : a.S;
+    if (nt_st) store_vec_nt<VEC>(Sd + oo, s);
+    else store_vec<VEC>(Sd + oo, s);
     if (a.H) {
       double part = 0.0;
 #pragma unroll
@@ -158,7 +165,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
       double h[VEC];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) h[j] = s[j] / den;
-      store_vec<VEC>(a.H + off, h);
+      store_vec<VEC>(a.H + oo, h);
     }
   }
 }
@@ -741,6 +748,50 @@ __global__ __launch_bounds__(kBlock) void permute_kernel(int64_t n, int64_t F, i
   store_vec<VEC>(dst + di, y);
 }
 
+// Permute-in with the closed-form rows finished on the spot (finalize fused
+// into the chain): internal rows < closed_from get T_0 = X0 (internal order);
+// purely isolated rows >= closed_from never enter the chain, so their
+// S = coef * X0 and H = S / (|S|_1 + 1e-8) are written to the caller's row
+// directly (the finalize_kernel arithmetic, same order of the row sum).
+template <int VEC>
+__global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, int64_t F, int LF,
+                                                                   const int32_t* __restrict__ perm,
+                                                                   const float* __restrict__ src,
+                                                                   float* __restrict__ dst, int64_t closed_from,
+                                                                   double coef, float* __restrict__ S,
+                                                                   float* __restrict__ H) {
+  const int lane = threadIdx.x & 63;
+  const int G = 64 / LF;
+  const int sg = lane / LF;
+  const int fs = lane - sg * LF;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + sg;
+  const bool active = sg < G && row < n;
+  const bool closed = row >= closed_from;
+  int64_t r = 0;
+  float x[VEC];
+  double sv[VEC];
+  double part = 0.0;
+  if (active) {
+    r = perm[row];
+    load_vec<VEC>(src + r * F + fs * VEC, x);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      sv[j] = closed ? coef * (double)x[j] : (double)x[j];
+      part += fabs(sv[j]);
+    }
+    if (!closed) store_vec<VEC>(dst + row * F + fs * VEC, sv);
+  }
+  double tot = 0.0;
+  for (int q = 0; q < LF; ++q) tot += __shfl(part, sg * LF + q, 64);
+  if (!active || !closed) return;
+  const double den = tot + 1e-8;
+  double h[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) h[j] = sv[j] / den;
+  store_vec<VEC>(S + r * F + fs * VEC, sv);
+  store_vec<VEC>(H + r * F + fs * VEC, h);
+}
+
 // caller rows (stride F) -> internal rows (stride Fp > F), the Fp - F pad columns zeroed
 __global__ void permute_pad_kernel(int64_t n, int64_t F, int64_t Fp, const int32_t* __restrict__ perm,
                                    const float* __restrict__ src, float* __restrict__ dst) {
@@ -1061,13 +1112,14 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start) {
 }
 
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
-                float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only) {
+                float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out) {
   if (L->n_rows == 0) return WG_OK;
   if (int rc = prof_mark(L, stream, true)) return rc;
-  const int vec = pick_vec(F, {xm1, xm2, xk, S, H});
+  const int vec = pick_vec(F, {xm1, xm2, xk, S, H, S_out});
   int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
   if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
   const bool fuse_h = (H != nullptr) && F <= max_tile;
+  if (S_out && !(fuse_h && S)) return fail(WG_ERR_INVALID, "launch_step: fused finalize needs one tile and S");
   for (int64_t f0 = 0; f0 < F; f0 += max_tile) {
     const int64_t fw = std::min<int64_t>(max_tile, F - f0);
     const int LF = (int)(fw / vec);
@@ -1084,6 +1136,8 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.xk = xk ? xk + f0 : nullptr;
     a.S = S ? S + f0 : nullptr;
     a.H = fuse_h ? H + f0 : nullptr;
+    a.out_perm = S_out ? L->perm : nullptr;
+    a.S_out = S_out;
     a.ld = F;
     a.LF = LF;
     a.k = k;
@@ -1171,6 +1225,35 @@ int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* sr
   if (Fp == F) return launch_permute(L, 0, F, src, dst, stream);
   hipLaunchKernelGGL(permute_pad_kernel, dim3((unsigned)ceil_div(n * Fp, 256)), dim3(256), 0, stream, n, F, Fp, L->perm,
                      src, dst);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
+bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const void*> ptrs) {
+  const int vec = pick_vec(F, ptrs);
+  int64_t max_tile = 64 * (int64_t)vec;
+  if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
+  return F <= max_tile;
+}
+
+int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
+                             float* H, hipStream_t stream) {
+  const int64_t n = L->n_rows;
+  if (n == 0) return WG_OK;
+  const int vec = pick_vec(F, {src, dst, S, H});
+  if (F > 64 * vec) return fail(WG_ERR_INVALID, "permute_in_closed: F too wide");
+  const int LF = (int)(F / vec);
+  const int G = 64 / LF;
+  const dim3 grid((unsigned)ceil_div(n, 4 * G));
+  if (vec == 4)
+    hipLaunchKernelGGL(permute_in_closed_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
+                       L->n_active, coef, S, H);
+  else if (vec == 2)
+    hipLaunchKernelGGL(permute_in_closed_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
+                       L->n_active, coef, S, H);
+  else
+    hipLaunchKernelGGL(permute_in_closed_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
+                       L->n_active, coef, S, H);
   WG_LAUNCH_CHECK();
   return WG_OK;
 }

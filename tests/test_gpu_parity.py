@@ -253,7 +253,8 @@ def test_wats_dropin_on_gpu_matches_reference():
                                    dict(inkernel_combine=0, iter=2, block_iter=1, chunk_iter=1),
                                    dict(gbuf=1), dict(hubf=64), dict(hubf=700, waves=16, chunk_iter=2, block_iter=2),
                                    dict(hubf=5000, waves=8), dict(gbuf=1, iter=2, block_iter=1, chunk_iter=1),
-                                   dict(inkernel_combine=1, iter=2, block_iter=1, chunk_iter=2, waves=8)])
+                                   dict(inkernel_combine=1, iter=2, block_iter=1, chunk_iter=2, waves=8),
+                                   dict(fuse_finalize=0), dict(fuse_finalize=0, tile_f=8)])
 def test_tuning_knobs_preserve_results(knobs):
     _check_knobs(knobs, F=12)
 
