@@ -500,6 +500,9 @@ def main():
                 "rows_per_launch": n_active,
                 "closed_form_rows": n - n_active,
                 "algorithmic_bytes_all_rows": algorithmic_bytes(n, nnz, F),
+                "all_rows_frac": algorithmic_bytes(n, nnz, F) / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "frac_note": "frac counts the rows each launch processes (purely isolated rows are closed-form "
+                             "and never launched); all_rows_frac is SURVEY 8(d)'s B_step with N = all nodes",
                 "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "avg_launch_us": avg_ms * 1e3,
                 "max_launch_us": prof["max_ms"] * 1e3,
