@@ -146,6 +146,27 @@ def build_halo_plan(indptr_local: np.ndarray, indices_global, bounds: np.ndarray
     return plan
 
 
+def gather_rows(X_local: torch.Tensor, bounds: np.ndarray, group=None) -> torch.Tensor:
+    """The full (N, F) matrix on every rank from each rank's row block
+    ``[bounds[q], bounds[q+1])`` (the optional final H gather
+    for a caller -- the WATS head -- that needs every row on one device).
+    One all_gather of row blocks padded to the largest block; collective."""
+    rank, world = _rank_world(group)
+    if world == 1:
+        return X_local
+    b = np.asarray(bounds, dtype=np.int64)
+    sizes = np.diff(b)
+    mx = int(sizes.max())
+    F = X_local.shape[1] if X_local.dim() == 2 else 1
+    dev = _device_for(group)
+    pad = torch.zeros(mx, F, dtype=X_local.dtype, device=dev)
+    pad[: X_local.shape[0]] = X_local.reshape(-1, F).to(dev)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    out = torch.cat([parts[q][: int(sizes[q])] for q in range(world)])
+    return out.to(X_local.device)
+
+
 def global_column_degree(partial_colsum: torch.Tensor, partial_diag: torch.Tensor, plan: HaloPlan,
                          group=None) -> torch.Tensor:
     """``w = colsum(A) - diag(A)`` for the columns [own | halo] of this rank:

@@ -287,3 +287,34 @@ def test_native_chain_loopback_exchange(F, lds, graph):
         assert cnt.value == K and tot.value > 0
     finally:
         lib.wg_dist_destroy(h)
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from wats_hip.dist import gather_rows
+        g = rmat_graph(700, 5000, seed=2)
+        b = partition_rows(g.indptr, world)
+        full = np.arange(g.n * 3, dtype=np.float32).reshape(g.n, 3)
+        got = gather_rows(torch.from_numpy(full[b[rank]:b[rank + 1]].copy()), b)
+        q.put((rank, bool(np.array_equal(got.numpy(), full))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_rows_cpu_gloo(world):
+    """The optional final gather of row-sharded outputs."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)
