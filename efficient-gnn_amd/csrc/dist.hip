@@ -489,6 +489,7 @@ int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
 int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src) {
   if (!D || !blobs || (D->n_halo > 0 && !halo_src)) return fail(WG_ERR_INVALID, "wg_dist_ipc_connect: bad arguments");
   if (!D->region) return fail(WG_ERR_INVALID, "wg_dist_ipc_connect: call wg_dist_ipc_local first");
+  if (D->ipc || !D->peer_region.empty()) return fail(WG_ERR_INVALID, "wg_dist_ipc_connect: already connected");
   const char* b = static_cast<const char*>(blobs);
   D->peer_region.assign(D->world, nullptr);
   std::vector<int64_t*> pf(D->world, nullptr);
