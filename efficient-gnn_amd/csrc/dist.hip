@@ -49,15 +49,32 @@ struct IpcPull {
   const float* slot_base[kMaxPeers];  // peer q's slot 0 (mapped); slot 1 at + slot_floats[q]
   int64_t slot_floats[kMaxPeers];
   const int64_t* flags;               // mine: flags[q] = phases peer q completed
-  const int64_t* count;               // phases this rank completed
+  int64_t* count;                     // phases this rank completed
+  int64_t* const* peer_flags;         // peer q's flags (mapped), device array [world]
   int32_t* err;
   int32_t world, rank;
 };
 
-__device__ __forceinline__ void ipc_wait(const IpcPull& p) {
+// signal: first record that this rank completed one more phase (count += 1,
+// stored into every peer's flag for this rank, after a system-scope release);
+// then wait until every peer has completed as many phases as this rank
+__device__ __forceinline__ void ipc_wait(const IpcPull& p, bool signal) {
+  __shared__ int64_t s_target;
+  if (threadIdx.x == 0) {
+    int64_t c = *p.count;
+    if (signal) {
+      __threadfence_system();
+      c += 1;
+      *p.count = c;
+      for (int q = 0; q < p.world; ++q)
+        if (q != p.rank) __hip_atomic_store(p.peer_flags[q] + p.rank, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    s_target = c;
+  }
+  __syncthreads();
   if (threadIdx.x < 64) {
     const int q = threadIdx.x;
-    const int64_t target = *p.count;
+    const int64_t target = s_target;
     bool ok = true;
     if (q < p.world && q != p.rank) {
       const uint64_t t0 = wall_clock64();
@@ -92,8 +109,8 @@ __global__ __launch_bounds__(256) void ipc_pull_kernel(IpcPull p, int slot, int6
   }
 }
 
-// wait only (before a phase that writes a slot but pulls nothing: the chain's first vector)
-__global__ void ipc_wait_kernel(IpcPull p) { ipc_wait(p); }
+// (signal the previous phase and) wait for the peers; one workgroup
+__global__ void ipc_wait_kernel(IpcPull p, int signal) { ipc_wait(p, signal != 0); }
 
 // this rank completed one more phase: count += 1, then tell every peer
 __global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, int64_t* const* peer_flags) {
@@ -194,22 +211,23 @@ struct wg_dist_s {
     return WG_OK;
   }
 
-  int ipc_wait_only(hipStream_t st) {
-    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, st, pull);
+  int ipc_wait_only(hipStream_t st, bool signal_first = false) {
+    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, st, pull, signal_first ? 1 : 0);
     WG_LAUNCH_CHECK();
     return WG_OK;
   }
 
   // refresh the halo rows ext[n_own ...] (F floats per row) from their owners.
   // ipc: `slot` is the region slot ext lives in (the owners' rows are read from
-  // the same slot of their regions)
+  // the same slot of their regions); the previous phase's completion is
+  // signalled by the same one-workgroup kernel that then waits for the peers
   int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot = 0) {
     if (ipc && world == 1) return WG_OK;  // no peers: nothing to wait for or pull
     if (ipc) {
       if (int rc = mark(st, true)) return rc;
-      // one spinning workgroup waits for the peers (ranks sharing a GPU in tests must not
+      // one spinning workgroup signals and waits (ranks sharing a GPU in tests must not
       // starve each other's kernels), then a full grid pulls the halo rows
-      if (int rc = ipc_wait_only(st)) return rc;
+      if (int rc = ipc_wait_only(st, /*signal_first=*/true)) return rc;
       const int64_t total = n_halo * F;
       if (total > 0) {
         const int blocks = (int)std::min<int64_t>(65535, ceil_div(total, 256));
@@ -289,15 +307,14 @@ struct wg_dist_s {
       int rc = launch_permute(L, 0, 1, X0, T[0], st);
       if (!rc && sig) rc = ipc_wait_only(st);
       if (!rc) rc = launch_scale_dinv(L, n_own, T[0], U[0], st);
-      if (!rc && sig) rc = ipc_signal(st);
-      for (int32_t k = 1; k <= K && !rc; ++k) {
+      for (int32_t k = 1; k <= K && !rc; ++k) {  // the exchange signals phase k-1, then waits
         rc = exchange(U[(k - 1) & 1], sendbuf, 1, st, (k - 1) & 1);
         if (!rc)
           rc = launch_lds1_step(L, lp, k, U[(k - 1) & 1], T[(k - 1) & 1], k >= 2 ? T[k & 1] : nullptr,
                                 k == K ? nullptr : T[k & 1], k == K ? nullptr : U[k & 1], sint, 1.0,
                                 std::exp(-s * (double)k), st);
-        if (!rc && sig) rc = ipc_signal(st);
       }
+      if (!rc && sig) rc = ipc_signal(st);  // phase K
       if (!rc) rc = launch_finalize(L, 1, sint, nullptr, 0.0, S, H, st);
       return rc;
     }
@@ -307,7 +324,6 @@ struct wg_dist_s {
     int rc = WG_OK;
     if (sig) rc = ipc_wait_only(st);
     if (!rc) rc = launch_permute_pad(L, F, Fp, X0, A[0], st);
-    if (!rc && sig) rc = ipc_signal(st);
     if (!rc && K == 0)
       rc = hipMemcpyAsync(sint, A[0], sizeof(float) * n_own * Fp, hipMemcpyDeviceToDevice, st) == hipSuccess
                ? WG_OK
@@ -318,8 +334,8 @@ struct wg_dist_s {
       if (!rc)
         rc = launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
                          std::exp(-s * (double)k), st);
-      if (!rc && sig) rc = ipc_signal(st);
     }
+    if (!rc && sig) rc = ipc_signal(st);  // phase K
     if (!rc) rc = launch_finalize(L, F, sint, nullptr, 0.0, S, H, st, Fp);
     return rc;
   }
@@ -396,7 +412,7 @@ int wg_dist_destroy(wg_dist_t D) {
     // peers may still pull from this rank's region in their last phase: wait until
     // every peer has completed as many phases as this rank (its last write here is
     // its final signal), then unmap and free.  A lost peer times out (60 s).
-    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, D->cap, D->pull);
+    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, D->cap, D->pull, 0);
     (void)hipStreamSynchronize(D->cap);
   }
   delete D;
@@ -523,6 +539,7 @@ int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src)
   }
   p.flags = reinterpret_cast<const int64_t*>(D->region + 2 * D->slot_floats);
   p.count = D->count;
+  p.peer_flags = D->peer_flags;
   p.err = D->err;
   p.world = D->world;
   p.rank = D->rank;
