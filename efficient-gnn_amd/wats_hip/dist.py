@@ -319,8 +319,22 @@ class ShardedWavelet:
         assert sum(len(x) for x in src) == p.n_halo
         allb = (ctypes.c_uint8 * (128 * p.world)).from_buffer_copy(b"".join(blobs))
         _trace("handles exchanged; mapping the peers' regions")
+        err = None
         with torch.cuda.device(self.device):
-            check(lib.wg_dist_ipc_connect(h, allb, ptr(halo_src)), "dist_ipc_connect")
+            try:
+                check(lib.wg_dist_ipc_connect(h, allb, ptr(halo_src)), "dist_ipc_connect")
+            except Exception as exc:  # noqa: BLE001 -- made collective below
+                err = exc
+        if p.world > 1:
+            # every rank must be connected before any enters a chain (a rank waiting on
+            # peers that gave up would spin until its 60 s timeout)
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=_device_for(self.group))
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
+            if not int(ok.item()) and err is None:
+                err = RuntimeError("wats_hip: IPC exchange setup failed on another rank")
+        if err is not None:
+            lib.wg_dist_destroy(h)
+            raise err
         return h
 
     def check_exchange(self) -> None:
