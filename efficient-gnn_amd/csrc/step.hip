@@ -781,6 +781,8 @@ __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, in
     }
     if (!closed) store_vec<VEC>(dst + row * F + fs * VEC, sv);
   }
+  // closed rows are the internal tail: most waves hold none and skip the row sums
+  if (!__ballot(active && closed)) return;
   double tot = 0.0;
   for (int q = 0; q < LF; ++q) tot += __shfl(part, sg * LF + q, 64);
   if (!active || !closed) return;

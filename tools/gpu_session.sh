@@ -34,7 +34,7 @@ timeout -k 10 400 python bench.py --steps ${STEPS:-20} --warmup 3 --out "$OUT/be
 stop_if_fatal $? bench
 if [ "${RUN_PROF:-1}" = 1 ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- \
-      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sharded-extra none > "$OUT/prof.log" 2>&1
+      python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sharded-extra none --cold-reps 0 > "$OUT/prof.log" 2>&1
   stop_if_fatal $? rocprof
 fi
 if [ "${RUN_PMC:-0}" = 1 ]; then
