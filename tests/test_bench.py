@@ -1,0 +1,43 @@
+"""The bench.py contract the driver parses: one JSON line on stdout with the
+required keys, a roofline object (bound, achieved, peak, unit, frac,
+traffic) and, at N = 1, a cpu_baseline object -- run on a small workload."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+
+def _run(args, timeout=600):
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                         timeout=timeout, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, f"stdout must be exactly one JSON line, got {len(lines)}: {out.stdout[:2000]}"
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_line_schema_small():
+    d = _run(["--config", "pubmed", "--F", "8", "--steps", "3", "--warmup", "1", "--cpu-seconds", "1",
+              "--sharded-extra", "pubmed", "--sharded-steps", "2", "--exchange", "ipc,rccl", "--cold-reps", "1"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["higher_is_better"] is True and d["value"] > 0
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1.5
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    c = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in c, k
+    assert d["eigen_kat"]["ok"], d["eigen_kat"]
+    for key in ("sharded", "sharded_pubmed_rccl"):
+        sh = d[key]
+        assert "error" not in sh, sh
+        assert sh["value"] > 0 and sh["roofline"]["eigen_kat"]["ok"]
