@@ -956,11 +956,16 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // Defaults measured on MI355X (profiles/r01 sweeps): wide signals (G = 64/LF
 // small, e.g. F = 40 -> G = 6) want long per-sub-group runs; F = 1 (G = 64)
 // shorter ones.
-void default_knobs(const Tuning& t, int G, int* iter, int* block_iter, int* chunk_iter) {
+// Wide tiles (F >= 16) on large graphs: one sub-group per row up to 96 entries per
+// lane (ogbn-arxiv-size F=40: 41.8 vs 45.5 us per step with iter 24; F=64 56.3 vs
+// 64.9; Reddit-size F=44 1732 vs 1817 us); small graphs keep more lanes per row
+// for latency (PubMed-size F=40: 9.3 us with iter 24, 17.2 with 96).
+void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter) {
   const bool wide = G <= 16;
-  *iter = t.iter > 0 ? t.iter : (wide ? 24 : 16);
+  const bool big = nnz >= (int64_t)1 << 20;
+  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 96 : 24) : 16);
   *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
-  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? 32 : 16);
+  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (big ? 64 : 32) : 16);
 }
 
 // Build (once per tile shape) the segment table and the split-row chunk table.
@@ -988,7 +993,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   for (int b = 0; b < kBuckets; ++b) bucket[b] = L->bucket[b];
   bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
   int iter, block_iter, chunk_iter;
-  default_knobs(L->tune, G, &iter, &block_iter, &chunk_iter);
+  default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter);
   const int64_t team_max = (int64_t)G * iter;
   const int64_t block_max = (int64_t)NW * G * block_iter;
   const int64_t CH = (int64_t)NW * G * chunk_iter;
