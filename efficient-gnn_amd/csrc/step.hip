@@ -1155,7 +1155,11 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.rowchunks = plan->rowchunks;
     a.arrivals = (L->tune.inkernel_combine && plan->n_split > 0) ? plan->arrivals : nullptr;
     a.seg_mask = L->tune.seg_mask;
-    a.nt = L->tune.nt;
+    // non-temporal T_k / S stores only for large per-step streams (ogbn-arxiv F=40, 30 MB of
+    // T_k + S per step: 40.6 us plain vs 42.0 nt; F=64, 48 MB: 55.3 vs 56.5; Reddit-size F=44,
+    // 82 MB: 1773 plain vs 1738 nt)
+    const int64_t stream_rows = (active_only && L->reordered) ? L->n_active : L->n_rows;
+    a.nt = L->tune.nt >= 0 ? L->tune.nt : ((stream_rows * F * 8 <= ((int64_t)64 << 20)) ? 0 : 4);
     a.bcast = L->tune.bcast;
     a.vidx = L->tune.vidx;
     a.xm1_bytes = (L->n_cols * F - f0) * (int64_t)sizeof(float);
