@@ -958,14 +958,16 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // shorter ones.
 // Wide tiles (F >= 16) on large graphs: one sub-group per row up to 96 entries per
 // lane (ogbn-arxiv-size F=40: 41.8 vs 45.5 us per step with iter 24; F=64 56.3 vs
-// 64.9; Reddit-size F=44 1732 vs 1817 us); small graphs keep more lanes per row
-// for latency (PubMed-size F=40: 9.3 us with iter 24, 17.2 with 96).
+// 64.9; Reddit-size F=44 1732 vs 1817 us) and long split-row chunks (Reddit-size
+// F=44: 1625 us with chunk_iter 128 vs 1729 with 64; arxiv neutral); small graphs
+// keep more lanes per row for latency (PubMed-size F=40: 9.3 us with iter 24, 17.2
+// with 96).
 void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter) {
   const bool wide = G <= 16;
   const bool big = nnz >= (int64_t)1 << 20;
   *iter = t.iter > 0 ? t.iter : (wide ? (big ? 96 : 24) : 16);
   *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
-  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (big ? 64 : 32) : 16);
+  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (big ? 128 : 32) : 16);
 }
 
 // Build (once per tile shape) the segment table and the split-row chunk table.
