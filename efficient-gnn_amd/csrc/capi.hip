@@ -87,7 +87,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "hot")) {
     L->tune.hot = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 40000));
   } else if (!strcmp(key, "vidx")) {
-    L->tune.vidx = value ? 1 : 0;
+    L->tune.vidx = value < 0 ? -1 : (value ? 1 : 0);
     return WG_OK;
   } else if (!strcmp(key, "bcast")) {
     L->tune.bcast = value ? 1 : 0;

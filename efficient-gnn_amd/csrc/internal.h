@@ -123,7 +123,7 @@ struct Tuning {
                              // streams exceed 64 MB, else 0: the next steps re-read them)
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
   int32_t bcast = 1;         // F > 1: sub-group cooperative index loads (ds_bpermute broadcast)
-  int32_t vidx = 0;          // F == 1: 16-B aligned int4/float4 index loads
+  int32_t vidx = -1;         // F == 1: 16-B aligned int4/float4 index loads; -1 = auto (on for nnz >= 16 M)
   int32_t waves = 4;         // waves per step-kernel workgroup: 4, 8 or 16
   int32_t hot = 0;           // F == 1: LDS hot-column cache size (columns), 0 = off
   int64_t seg_mask = -1;     // timing attribution only: launch only these segments

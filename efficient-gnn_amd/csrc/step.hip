@@ -965,7 +965,7 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter) {
   const bool wide = G <= 16;
   const bool big = nnz >= (int64_t)1 << 20;
-  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 96 : 24) : 16);
+  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 96 : 24) : (G == 64 && nnz >= ((int64_t)16 << 20) ? 8 : 16));
   *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
   *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (big ? 128 : 32) : 16);
 }
@@ -1163,7 +1163,10 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     const int64_t stream_rows = (active_only && L->reordered) ? L->n_active : L->n_rows;
     a.nt = L->tune.nt >= 0 ? L->tune.nt : ((stream_rows * F * 8 <= ((int64_t)64 << 20)) ? 0 : 4);
     a.bcast = L->tune.bcast;
-    a.vidx = L->tune.vidx;
+    // F == 1 gathers on large graphs: int4 index loads and narrower teams (8M R-MAT 8-way
+    // shard: 275.7 us per step with vidx + iter 8 vs 296.9 without; ogbn-arxiv-size F=1:
+    // vidx 12.3 vs 11.5, so only from 16 M nonzeros)
+    a.vidx = L->tune.vidx >= 0 ? L->tune.vidx : (L->nnz >= ((int64_t)16 << 20) ? 1 : 0);
     a.xm1_bytes = (L->n_cols * F - f0) * (int64_t)sizeof(float);
     a.gbuf = (L->tune.gbuf && a.xm1_bytes < ((int64_t)1 << 31)) ? 1 : 0;
     // hub rows: LDS = (hubf + 1) * tile + the block-mode buffer (NW*64*VEC doubles) <= 160 KiB
