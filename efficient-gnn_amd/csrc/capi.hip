@@ -134,6 +134,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "fuse_finalize")) {
     L->tune.fuse_finalize = value ? 1 : 0;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "hub_vidx")) {
+    L->tune.hub_vidx = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hub_iter")) {
     L->tune.hub_iter = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
   } else if (!strcmp(key, "lds_perm")) {

@@ -157,6 +157,9 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_lds1_kernel(Lds1Args a) {
 // columns, and the two are added (one of them is 0, so the sum is exact).
 // Row teams, row groups and the LDS counter as cheb_lds1_kernel; one column
 // block, so the epilogue runs in place.
+// VIDX: each lane takes 4 consecutive entries with one 16-B column load
+// (groups aligned to 4 entries in the padded CSR, masked to the row).
+template <bool VIDX>
 __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   __shared__ int s_next;
   constexpr uint32_t kDrop = 0x80000000u;
@@ -196,7 +199,23 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
     const int32_t row = gd.x + team;
     const bool act = team < nrows;
     double acc = 0.0;
-    if (act) {
+    if (act && VIDX) {
+      const int32_t e0 = rp[row], e1 = rp[row + 1];
+      for (int32_t qq = (e0 & ~3) + 4 * q; qq < e1; qq += 4 * ln) {
+        const int4 c4 = *reinterpret_cast<const int4*>(col + qq);
+        const int32_t cc[4] = {c4.x, c4.y, c4.z, c4.w};
+        float x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = qq + j >= e0 && qq + j < e1;
+          const float xl = u[ok ? min(cc[j], H) : H];
+          const uint32_t off = (ok && cc[j] >= H) ? (uint32_t)cc[j] * 4u : kDrop;
+          x[j] = xl + __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += (double)x[j];
+      }
+    } else if (act) {
       const int32_t e1 = rp[row + 1];
       int32_t e = rp[row] + q;
       for (; e + 3 * ln < e1; e += 4 * ln) {
@@ -1032,17 +1051,19 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
   a.alpha0 = alpha0;
   a.alpha_k = alpha_k;
   if (p->mode == 4) {
-    static bool attr4 = false;
-    if (!attr4) {
-      WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_hub1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024 - 64));
-      attr4 = true;
+    static bool attr4[2] = {false, false};
+    const bool vx = L->tune.hub_vidx != 0;
+    if (!attr4[vx]) {
+      WG_HIP_TRY(hipFuncSetAttribute(vx ? (const void*)cheb_hub1_kernel<true> : (const void*)cheb_hub1_kernel<false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
+      attr4[vx] = true;
     }
     a.brp = L->rowptr;
     a.gcol = L->col;
     a.hub = p->hub;
     a.u_bytes = (int32_t)(p->ulen * 4);
-    hipLaunchKernelGGL(cheb_hub1_kernel, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
+    if (vx) hipLaunchKernelGGL(cheb_hub1_kernel<true>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
+    else hipLaunchKernelGGL(cheb_hub1_kernel<false>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
     WG_LAUNCH_CHECK();
     return prof_mark(L, stream, false);
   }
