@@ -143,8 +143,9 @@ def cpu_baseline(g, K, F, s, X, seconds):
 
 def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl"):
     """One graph (generated identically on every rank, on the GPU) split into
-    nnz-balanced row blocks; per Chebyshev step one all_to_all_single halo
-    exchange (RCCL) + the step kernel.  Strong scaling (fixed graph).
+    nnz-balanced row blocks; per Chebyshev step one halo exchange (`exchange`:
+    IPC pull or RCCL send/recv in the native chain, or torch all_to_all_single)
+    + the step kernel.  Strong scaling (fixed graph).
     Returns the result dict (meaningful on rank 0)."""
     from wats_hip.dist import ShardedWavelet, partition_rows
     from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
