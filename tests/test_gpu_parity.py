@@ -200,6 +200,28 @@ def test_eigenvector_kat_full_size(name, k):
     assert_parity(_np(S), X0.astype(np.float64) * coef, what=f"{name} eigen KAT")
 
 
+@pytest.mark.parametrize("F", [40, 41, 1])
+def test_eigenvector_kat_large_wide(F):
+    """The large-graph defaults (one sub-group per row up to 576 entries,
+    long split-row chunks, plain / non-temporal stores by stream size, padded
+    odd widths, fused finalize, F = 1 kernel selection) on a 20 M-nonzero
+    R-MAT graph from the GPU generator, checked with the eigenvector KAT:
+    X0 = sqrt(degree) x column scales -> S = X0 * sum_k (-1)^k e^{-sk}."""
+    from wats_hip.graphgen import rmat_graph_device
+    ip, ix = rmat_graph_device(400_000, 20_000_000, seed=3)
+    L = NormalizedLaplacian(400_000, ip, ix)
+    deg = torch.diff(ip).to(torch.float64)
+    X0 = (deg.sqrt()[:, None] * (1.0 + 0.125 * torch.arange(F, dtype=torch.float64, device=deg.device))[None, :])
+    X0 = X0.to(torch.float32).contiguous()
+    k = 16
+    coef = sum(((-1.0) ** i) * np.exp(-0.8 * i) for i in range(k + 1))
+    H, S = wats_hip.graph_wavelet_features(L, k=k, X0=X0, return_S=True)
+    assert_parity(_np(S), _np(X0).astype(np.float64) * coef, what=f"20M R-MAT F={F} eigen KAT")
+    Sd = X0.double() * coef
+    Hd = Sd / (Sd.abs().sum(dim=1, keepdim=True) + 1e-8)
+    assert float((H.double() - Hd).abs().max()) <= 1e-5
+
+
 def test_deterministic_and_reorder_invariant():
     g = named_graph("ogbn-arxiv")
     X = torch.randn(g.n, 8, generator=torch.Generator().manual_seed(0))
