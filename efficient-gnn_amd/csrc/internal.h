@@ -138,7 +138,7 @@ struct Tuning {
   int32_t lds_depth = 2;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
   int32_t lds_k = 4;         // windows: chunks per lane (1 = cheb_lds2_kernel, 2 / 4 = cheb_lds3_kernel)
   int32_t fuse_finalize = 1;  // wavelet_features: closed rows in the permute-in, S / H from the last step
-  int32_t hub_vidx = 1;      // hub teams: 16-B column loads, 4 consecutive entries per lane (8M: 1199 vs 1210 us)
+  int32_t hub_vidx = 0;      // hub teams: 1 = 16-B column loads, 4 consecutive entries per lane (s26, 8M R-MAT: 1725 vs 1299 us, off)
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
 };
