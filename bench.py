@@ -89,6 +89,14 @@ def algorithmic_bytes(n: int, nnz: int, F: int) -> int:
     return 8 * nnz + 4 * (n + 1) + 20 * n * F
 
 
+def clenshaw_bytes(n: int, nnz: int, F: int) -> int:
+    """The wavelet chain's heat sum by Clenshaw's recurrence:
+    CSR 8 B/nnz, int32 row pointers, gather b_{k+1} once, read b_{k+2} and X0,
+    write b_k (fp32) -- no S stream.  SURVEY 8(d)'s forward-recurrence model
+    (algorithmic_bytes) is reported beside it as nominal_8d_frac."""
+    return 8 * nnz + 4 * (n + 1) + 16 * n * F
+
+
 def _byte_model(info) -> str:
     if not info:
         return "SURVEY 8(d)"
@@ -454,7 +462,7 @@ def main():
         n_active = n - int(L.info["n_closed_form"])
         b_8d = algorithmic_bytes(n_active, nnz, F)
         lds_info = L.lds_plan_info(active_only=True) if F == 1 else None
-        b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
+        b_step = lds_algorithmic_bytes(lds_info) if lds_info else clenshaw_bytes(n_active, nnz, F)
         achieved = b_step / (avg_ms * 1e-3) / 1e9
         traffic, traffic_src = None, None
         tj = args.traffic_json
@@ -496,14 +504,17 @@ def main():
                                    f"an upper bound) + WRITE_SIZE per launch of this kernel on this workload"
                                    if traffic is not None else None),
                 "kernel": lds_kernel_name(lds_info),
-                "byte_model": _byte_model(lds_info),
+                "byte_model": _byte_model(lds_info) if lds_info else
+                              "Clenshaw heat sum (DESIGN.md 4.1): 8 B/nnz + 4(N+1) + 16 N F",
                 "algorithmic_bytes_per_launch": b_step,
                 "rows_per_launch": n_active,
                 "closed_form_rows": n - n_active,
                 "algorithmic_bytes_all_rows": algorithmic_bytes(n, nnz, F),
                 "all_rows_frac": algorithmic_bytes(n, nnz, F) / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "frac_note": "frac counts the rows each launch processes (purely isolated rows are closed-form "
-                             "and never launched); all_rows_frac is SURVEY 8(d)'s B_step with N = all nodes",
+                "frac_note": "frac: the bytes this kernel's algorithm needs (Clenshaw: no S stream) over the "
+                             "rows each launch processes (purely isolated rows are closed-form and never "
+                             "launched); nominal_8d_frac: SURVEY 8(d)'s forward-recurrence B_step over the same "
+                             "rows; all_rows_frac: SURVEY 8(d)'s B_step with N = all nodes",
                 "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "avg_launch_us": avg_ms * 1e3,
                 "max_launch_us": prof["max_ms"] * 1e3,

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "internal.h"
 
@@ -113,6 +114,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
       WG_HIP_TRY(hipDeviceSynchronize());
       if (int rc = sort_row_columns(L, nullptr)) return rc;
     }
+  } else if (!strcmp(key, "clenshaw")) {
+    L->tune.clenshaw = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hubf")) {
     L->tune.hubf = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 4096));
     return WG_OK;  // launch-time choice
@@ -282,15 +286,47 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     }
     return launch_finalize(L, F, sint, b0, coef, S, H, stream);
   }
-  for (int32_t k = 1; k <= K; ++k) {
-    const float* xm1 = (k & 1) ? b0 : b1;
-    const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
-    float* xk = (k == K) ? nullptr : ((k & 1) ? b1 : b0);  // T_K itself is never re-read
-    const double ak = std::exp(-s * (double)k);             // WATS.py:65
-    const bool last_fused = fuse_fin && k == K;
-    rc = launch_step(L, k, Fp, xm1, xm2, xk, sint, last_fused ? H : nullptr, 1.0, ak, stream, /*active_only=*/true,
-                     last_fused ? S : nullptr);
+  if (L->tune.clenshaw && K >= 1) {
+    // Clenshaw's recurrence for S = sum_k c_k T_k(L_hat) X0, c_k = exp(-s k) (WATS.py:65-68):
+    //   b_K = c_K X0 (never stored), b_k = c_k X0 + 2 L_hat b_{k+1} - b_{k+2} (k = K-1 .. 1),
+    //   S = c_0 X0 + L_hat b_1 - b_2.
+    // K SpMM steps as in the forward recurrence, but no S stream: each step reads X0 instead of
+    // reading and writing S.  b_k is written in place over b_{k+2} (own rows only); the buffers
+    // alternate so that b_1 sits in b1 and the final step may overwrite b_2 in sint.
+    std::vector<double> c(K + 1);
+    for (int32_t k = 0; k <= K; ++k) c[k] = std::exp(-s * (double)k);
+    const float* bk1 = b0;           // b_{k+1} (b_K is implicit: c_K X0)
+    float* bk2 = nullptr;            // b_{k+2} (nullptr: implicit, b_K, or 0)
+    double cacc = 2.0 * c[K];        // the implicit b_K = c_K X0 enters through the SpMM scale
+    float* bufs[2] = {(K & 1) ? sint : b1, (K & 1) ? b1 : sint};
+    int nb = 0;
+    for (int32_t k = K - 1; k >= 1; --k) {
+      float* out = bk2 ? bk2 : bufs[nb++];
+      const double ck = c[k] - (bk2 == nullptr && k + 2 == K ? c[K] : 0.0);  // implicit b_{k+2} = c_K X0
+      ClenArgs cl{b0, ck, cacc, 0};
+      rc = launch_step(L, 2, Fp, bk1, bk2, out, nullptr, nullptr, 1.0, 0.0, stream, /*active_only=*/true, nullptr, &cl);
+      if (rc) return rc;
+      bk2 = const_cast<float*>(bk1 == b0 ? nullptr : bk1);
+      bk1 = out;
+      cacc = 2.0;
+    }
+    // final: S = c_0 X0 + L_hat b_1 - b_2 (K == 1: L_hat b_1 = c_1 L_hat X0; K == 2: b_2 = c_2 X0)
+    const double c0 = c[0] - (K == 2 ? c[2] : 0.0);
+    ClenArgs cl{b0, c0, K == 1 ? c[1] : 1.0, 1};
+    rc = launch_step(L, 2, Fp, bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
+                     1.0, 0.0, stream, /*active_only=*/true, fuse_fin ? S : nullptr, &cl);
     if (rc) return rc;
+  } else {
+    for (int32_t k = 1; k <= K; ++k) {
+      const float* xm1 = (k & 1) ? b0 : b1;
+      const float* xm2 = (k == 1) ? nullptr : ((k & 1) ? b1 : b0);
+      float* xk = (k == K) ? nullptr : ((k & 1) ? b1 : b0);  // T_K itself is never re-read
+      const double ak = std::exp(-s * (double)k);             // WATS.py:65
+      const bool last_fused = fuse_fin && k == K;
+      rc = launch_step(L, k, Fp, xm1, xm2, xk, sint, last_fused ? H : nullptr, 1.0, ak, stream,
+                       /*active_only=*/true, last_fused ? S : nullptr);
+      if (rc) return rc;
+    }
   }
   if (fuse_fin) return WG_OK;
   return launch_finalize(L, F, sint, b0, coef, S, H, stream, Fp);

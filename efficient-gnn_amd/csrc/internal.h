@@ -138,6 +138,7 @@ struct Tuning {
   int32_t lds_depth = 2;     // windows: 64-chunk windows in flight per wave (2, 4 or 8)
   int32_t lds_k = 4;         // windows: chunks per lane (1 = cheb_lds2_kernel, 2 / 4 = cheb_lds3_kernel)
   int32_t fuse_finalize = 1;  // wavelet_features: closed rows in the permute-in, S / H from the last step
+  int32_t clenshaw = 1;      // wavelet_features (F > 1 / weighted): heat sum by Clenshaw's recurrence (no S stream)
   int32_t hub_vidx = 0;      // hub teams: 1 = 16-B column loads, 4 consecutive entries per lane (s26, 8M R-MAT: 1725 vs 1299 us, off)
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
@@ -190,9 +191,18 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out);
 // S_out (finalize fused into the last step; needs S, H and F within one tile):
 // the rows' final S and H go to caller row perm[row] of S_out / H
+// Clenshaw form of the heat sum (wavelet_features): a step computes
+//   out = ck * X0 + cacc * (L_hat . xm1) - xm2      (xm2 NULL = 0)
+// into xk (final == 0), or into S [S_out / H] as the finished sum (final == 1).
+struct ClenArgs {
+  const float* x0;  // X0, internal order, same width / stride as the chain
+  double ck;
+  double cacc;
+  int final_;
+};
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
-                float* S_out = nullptr);
+                float* S_out = nullptr, const ClenArgs* cl = nullptr);
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef,
                     float* S, float* H, hipStream_t stream, int64_t ldi = 0);  // ldi: internal row stride (0 = F)
 // the internal signal width of an F-column chain: odd / 4-unaligned F >= 3 is

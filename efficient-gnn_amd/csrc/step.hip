@@ -58,6 +58,9 @@ struct StepArgs {
   int32_t gbuf;        // F > 1 bcast gathers as raw buffer loads (accumulate_bcast_buf)
   int32_t hubf;        // F > 1, hub kernel: rows [0, hubf) of the tile from LDS
   int64_t xm1_bytes;   // extent of T_{k-1} from xm1 (gbuf: < 2^31)
+  int32_t clen;        // 0 = forward recurrence + heat sum; 1 / 2 = Clenshaw step / final (ClenArgs)
+  const float* x0;     // Clenshaw: X0 rows (internal order, stride ld)
+  double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc - xm2
 };
 
 template <int VEC>
@@ -105,7 +108,7 @@ __device__ __forceinline__ void store_vec(float* p, const double (&x)[VEC]) {
 template <int VEC>
 struct EpiIn {
   float prev[VEC];  // k == 1: T_0 own row (for S); k >= 2: T_{k-2} own row
-  float sold[VEC];  // S own row (k >= 2)
+  float sold[VEC];  // S own row (k >= 2); Clenshaw: X0 own row
   int iso;
   int32_t orow;     // out_perm[row] (finalize fused into the last step)
 };
@@ -115,6 +118,16 @@ __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int
   const int64_t off = row * a.ld + (int64_t)fs * VEC;
   in.iso = a.iso[row];
   in.orow = a.out_perm ? a.out_perm[row] : (int32_t)row;
+  if (a.clen) {
+    if (a.xm2) {
+      load_vec<VEC>(a.xm2 + off, in.prev);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) in.prev[j] = 0.0f;
+    }
+    load_vec<VEC>(a.x0 + off, in.sold);
+    return;
+  }
   load_vec<VEC>((a.k == 1 ? a.xm1 : a.xm2) + off, in.prev);
   if (a.S && a.k >= 2) load_vec<VEC>(a.S + off, in.sold);
 }
@@ -139,8 +152,13 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
     for (int j = 0; j < VEC; ++j) acc[j] -= (double)x[j];
   }
   double t[VEC];
+  if (a.clen) {  // Clenshaw: b = ck * X0 + cacc * (L_hat b') - b''
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) t[j] = (a.k == 1) ? acc[j] : 2.0 * acc[j] - (double)in.prev[j];
+    for (int j = 0; j < VEC; ++j) t[j] = a.ck * (double)in.sold[j] + a.cacc * acc[j] - (double)in.prev[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) t[j] = (a.k == 1) ? acc[j] : 2.0 * acc[j] - (double)in.prev[j];
+  }
   if (a.xk) {
     if (nt_st) store_vec_nt<VEC>(a.xk + off, t);
     else store_vec<VEC>(a.xk + off, t);
@@ -148,8 +166,10 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
   if (a.S) {
     double s[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j)  // k == 1: S = alpha0*T_0 + alpha1*T_1
-      s[j] = (a.k == 1) ? a.alpha0 * (double)in.prev[j] + a.alpha_k * t[j] : (double)in.sold[j] + a.alpha_k * t[j];
+    for (int j = 0; j < VEC; ++j)  // k == 1: S = alpha0*T_0 + alpha1*T_1; Clenshaw final: S = t
+      s[j] = a.clen ? t[j]
+                    : (a.k == 1) ? a.alpha0 * (double)in.prev[j] + a.alpha_k * t[j]
+                                 : (double)in.sold[j] + a.alpha_k * t[j];
     // finalize fused (last step): the rows go straight to the caller's order
     const int64_t oo = a.out_perm ? (int64_t)in.orow * a.ld + (int64_t)fs * VEC : off;
     float* Sd = a.out_perm ? a.S_out : a.S;
@@ -1121,7 +1141,8 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start) {
 }
 
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
-                float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out) {
+                float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out,
+                const ClenArgs* cl) {
   if (L->n_rows == 0) return WG_OK;
   if (int rc = prof_mark(L, stream, true)) return rc;
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H, S_out});
@@ -1152,6 +1173,14 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.k = k;
     a.alpha0 = alpha0;
     a.alpha_k = alpha_k;
+    if (cl) {  // Clenshaw: the generic (k >= 2) paths, S written only by the final step
+      a.k = 2;
+      a.clen = cl->final_ ? 2 : 1;
+      a.x0 = cl->x0 + f0;
+      a.ck = cl->ck;
+      a.cacc = cl->cacc;
+      if (!cl->final_) a.S = nullptr;
+    }
     a.chunks = plan->chunks;
     a.partial = plan->partial;
     a.rowchunks = plan->rowchunks;

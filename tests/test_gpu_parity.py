@@ -306,6 +306,29 @@ def _check_knobs(knobs, F):
         assert torch.equal(S0, S1), "same plan must give bitwise-identical results"
 
 
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 7, 16])
+@pytest.mark.parametrize("F,fuse", [(4, 1), (40, 1), (40, 0), (6, 1), (130, 1)])
+def test_clenshaw_heat_sum_vs_forward_and_oracle(k, F, fuse):
+    """wavelet_features' default heat sum (Clenshaw's recurrence: no S stream,
+    b_k written over b_{k+2}) against the oracle's forward recurrence and the
+    forward chain (clenshaw = 0), for every K parity / small-K special case,
+    fused and unfused finalize, padded (F = 6) and multi-tile (F = 130) widths,
+    on a weighted directed graph with self loops and isolated nodes."""
+    g = random_graph(700, 0.02, seed=k * 7 + F, directed=True, weighted=True, self_loop_frac=0.05,
+                     isolated_frac=0.08)
+    A = g.to_scipy()
+    X = np.random.default_rng(k + F).standard_normal((g.n, F)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=k, s=0.8, X0=X, return_all=True)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(fuse_finalize=fuse, clenshaw=1)
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=k, X0=torch.from_numpy(X), return_S=True)
+    L.tune(clenshaw=0)
+    H0, S0 = wats_hip.graph_wavelet_features(L, k=k, X0=torch.from_numpy(X), return_S=True)
+    for S, H, tag in ((S1, H1, "clenshaw"), (S0, H0, "forward")):
+        assert_parity(_np(S), ref["S"], what=f"K={k} F={F} {tag} S")
+        assert_parity(_np(H), ref["H"], what=f"K={k} F={F} {tag} H")
+
+
 # ----------------------------------------------------------------- F == 1 column-blocked LDS kernel
 @pytest.mark.parametrize("knobs", [dict(lds=0), dict(lds=1), dict(lds=1, lds_cb=2048), dict(lds=1, lds_cb=1024, lds_iter=2),
                                    dict(lds=1, lds_cb=4096, lds_iter=64, lds_wg=7),
