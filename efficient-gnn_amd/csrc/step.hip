@@ -981,11 +981,12 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // 64.9; Reddit-size F=44 1732 vs 1817 us) and long split-row chunks (Reddit-size
 // F=44: 1625 us with chunk_iter 128 vs 1729 with 64; arxiv neutral); small graphs
 // keep more lanes per row for latency (PubMed-size F=40: 9.3 us with iter 24, 17.2
-// with 96).
+// with 96).  F = 1 from 1 M nonzeros: 8 entries per lane (ogbn-arxiv-size: 10.7 us per
+// step vs 11.6 with 16, s34).
 void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter) {
   const bool wide = G <= 16;
   const bool big = nnz >= (int64_t)1 << 20;
-  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 96 : 24) : (G == 64 && nnz >= ((int64_t)16 << 20) ? 8 : 16));
+  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 96 : 24) : (G == 64 && big ? 8 : 16));
   *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
   *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (big ? 128 : 32) : 16);
 }

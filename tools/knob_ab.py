@@ -2,7 +2,7 @@
 per set, the mean step-kernel time and the max relative difference of S and H
 against the first set (the reference numbering is unchanged by any knob).
 
-    python tools/knob_ab.py --config ogbn-arxiv --sets "hubf=0;hubf=800,hubw=1" [--rounds 2]
+    python tools/knob_ab.py --config ogbn-arxiv --sets "clenshaw=0;clenshaw=1" [--rounds 2]
 """
 import argparse
 import json
@@ -35,12 +35,12 @@ def main():
     X = torch.randn(L.n, F, device="cuda") if F > 1 else L.log1p_degree()
     sets = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in s.split(",") if kv) for s in a.sets.split(";")]
     keys = sorted({k for s in sets for k in s})
+    if any(set(s) != set(keys) for s in sets):
+        raise SystemExit("every set must name the same knobs (the handle keeps the last value of a knob)")
     ref = None
     for rnd in range(a.rounds):
         for s in sets:
-            knobs = {k: 0 for k in keys}
-            knobs.update(s)
-            L.tune(**knobs)
+            L.tune(**s)
             H, S = wats_hip.graph_wavelet_features(L, X0=X, k=K, s=0.8, return_S=True)
             torch.cuda.synchronize()
             if ref is None:
