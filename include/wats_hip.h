@@ -181,6 +181,8 @@ int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float*
  * a7: graph_wavelet_features (calibration/WATS.py:39-74), fused:
  *   T_0 = X0 (N,F) -> K Chebyshev steps -> S = sum_k exp(-s k) T_k ->
  *   H = S / (||S||_1,row + 1e-8).
+ * F > 1 or weighted: the sum is evaluated by Clenshaw's recurrence (K SpMM
+ * steps, no S stream; tuning key "clenshaw" 0 = forward recurrence).
  * X0, S, H in the caller's row order, row stride F.  S and H nullable (at
  * least one non-NULL).  K >= 0.  Uses the handle's workspace (grown on first
  * use for a given F -- call once untimed before capturing into a graph).
@@ -188,10 +190,13 @@ int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float*
 int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s,
                         float* S, float* H, void* stream);
 
-/* Tuning: key "iter" (team-mode nonzeros per lane sub-group, default 8),
- * "chunk_iter" (chunk-mode nonzeros per sub-group, default 16), "seg_mask"
- * (bitmask of plan segments to launch -- timing attribution only; results
- * are wrong unless all bits are set).  Synchronous (drops cached plans). */
+/* Tuning: key "iter" (team-mode nonzeros per lane sub-group; default by
+ * shape), "chunk_iter" (chunk-mode nonzeros per sub-group),
+ * "seg_mask" (bitmask of plan segments to launch -- timing attribution only;
+ * results are wrong unless all bits are set), "clenshaw" (wavelet_features'
+ * heat sum, default 1), and the kernel-variant keys listed in
+ * efficient-gnn_amd/csrc/internal.h (struct Tuning).  Plan-shaping keys are
+ * synchronous (they drop cached plans); launch-time keys are not. */
 int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value);
 /* Human-readable launch plan of the step kernel for an F-column signal
  * (thread-local string, valid until the next call on this thread). */
