@@ -307,11 +307,14 @@ def f1_companion(lib, L, K, s_heat, steps, device):
     avg_ms = p["sum_ms"] / max(1, p["launches"])
     n_active = n - int(L.info["n_closed_form"])
     info = L.lds_plan_info(active_only=True)
-    b_step = lds_algorithmic_bytes(info) if info else algorithmic_bytes(n_active, L.nnz, 1)
+    b_step = lds_algorithmic_bytes(info) if info else clenshaw_bytes(n_active, L.nnz, 1)
+    b_8d = algorithmic_bytes(n_active, L.nnz, 1)
     return {"F": 1, "signal": "log1p(rowsum) (WATS.py:58-59)", "value": float(L.nnz) * K / (ms * 1e-3),
             "unit": "edges*K/s", "ms_per_step": ms, "avg_launch_us": avg_ms * 1e3,
             "kernel": lds_kernel_name(info),
-            "algorithmic_bytes_per_launch": b_step, "frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            "byte_model": _byte_model(info) if info else "Clenshaw heat sum (DESIGN.md 4.1)",
+            "algorithmic_bytes_per_launch": b_step, "frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def _kat_signal(deg: np.ndarray, F: int) -> np.ndarray:
