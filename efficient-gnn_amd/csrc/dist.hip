@@ -275,7 +275,9 @@ struct wg_dist_s {
     const size_t snd = ((size_t)std::max<int64_t>(n_send, 1) * Fp + 63) / 64 * 64;
     const size_t ulen = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
     // lds: T ping-pong (own rows) + u ping-pong (padded column space); else T ping-pong over [own | halo]
-    const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd;
+    // F > 1 / weighted: heat sum by Clenshaw's recurrence (as wg_wavelet_features), X0 kept in its own buffer
+    const bool clen = !lp && L->tune.clenshaw && K >= 1;
+    const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd + (clen ? own : 0);
     if (ws_floats < need) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       WG_HIP_TRY(hipStreamIsCapturing(st, &cs));
@@ -328,12 +330,35 @@ struct wg_dist_s {
       rc = hipMemcpyAsync(sint, A[0], sizeof(float) * n_own * Fp, hipMemcpyDeviceToDevice, st) == hipSuccess
                ? WG_OK
                : fail(WG_ERR_HIP, "wg_dist: copy");
-    for (int32_t k = 1; k <= K && !rc; ++k) {
-      float* cur = A[(k - 1) & 1];
-      rc = exchange(cur, sendbuf, Fp, st, (k - 1) & 1);
-      if (!rc)
-        rc = launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
-                         std::exp(-s * (double)k), st);
+    if (clen) {
+      // b_K = c_K X0 implicit; b_k = c_k X0 + 2 L_hat b_{k+1} - b_{k+2} written over b_{k+2} (own rows)
+      // in the slot the forward chain would write; S = c_0 X0 + L_hat b_1 - b_2 (capi.hip).
+      // Phase j = 1..K exchanges slot (j-1)&1, exactly as the forward chain's step j.
+      float* x0 = take(own);
+      if (!rc && hipMemcpyAsync(x0, A[0], sizeof(float) * n_own * Fp, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        rc = fail(WG_ERR_HIP, "wg_dist: copy X0");
+      std::vector<double> c(K + 1);
+      for (int32_t k = 0; k <= K; ++k) c[k] = std::exp(-s * (double)k);
+      for (int32_t j = 1; j <= K && !rc; ++j) {
+        const int32_t k = K - j;  // this phase computes b_k (k = 0: the final S)
+        float* cur = A[(j - 1) & 1];
+        rc = exchange(cur, sendbuf, Fp, st, (j - 1) & 1);
+        if (rc) break;
+        const bool prev_stored = j >= 3;  // b_{k+2} in slot j&1 (j == 2: the implicit b_K; j == 1: zero)
+        const double ck = c[k] - (j == 2 ? c[K] : 0.0);
+        const double cacc = (j == 1) ? (k == 0 ? c[K] : 2.0 * c[K]) : (k == 0 ? 1.0 : 2.0);
+        ClenArgs cl{x0, ck, cacc, k == 0 ? 1 : 0};
+        rc = launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr, k == 0 ? nullptr : A[j & 1],
+                         k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, st, false, nullptr, &cl);
+      }
+    } else {
+      for (int32_t k = 1; k <= K && !rc; ++k) {
+        float* cur = A[(k - 1) & 1];
+        rc = exchange(cur, sendbuf, Fp, st, (k - 1) & 1);
+        if (!rc)
+          rc = launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr,
+                           1.0, std::exp(-s * (double)k), st);
+      }
     }
     if (!rc && sig) rc = ipc_signal(st);  // phase K
     if (!rc) rc = launch_finalize(L, F, sint, nullptr, 0.0, S, H, st, Fp);

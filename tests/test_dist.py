@@ -225,6 +225,26 @@ def test_native_chain_world1(kind, F, lds):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 2, 3, 5])
+def test_native_chain_clenshaw_small_orders(K):
+    """The sharded chain's Clenshaw heat sum (F > 1) at the orders whose
+    first / second phases carry the implicit b_K: against the oracle and
+    against the forward recurrence (clenshaw = 0)."""
+    from wats_hip.dist import ShardedWavelet
+    g = _native_graph("weighted")
+    sw = ShardedWavelet(g.indptr, g.indices, g.values, g.n, np.array([0, g.n]), exchange="rccl", device="cuda:0")
+    X = torch.from_numpy(np.random.default_rng(K).standard_normal((g.n, 6)).astype(np.float32)).cuda()
+    ref = O.graph_wavelet_features(g.to_scipy(), k=K, s=0.8, X0=X.cpu().numpy(), return_all=True)
+    H1, S1 = sw.wavelet_features(X, k=K, s=0.8)
+    sw.L.tune(clenshaw=0)
+    H0, S0 = sw.wavelet_features(X, k=K, s=0.8)
+    for S, H, tag in ((S1, H1, "clenshaw"), (S0, H0, "forward")):
+        assert_parity(S.cpu().numpy(), ref["S"], what=f"native K={K} {tag} S")
+        assert_parity(H.cpu().numpy(), ref["H"], what=f"native K={K} {tag} H")
+    sw.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("F,lds,graph", [(1, 2, 1), (1, 0, 1), (8, 3, 1), (8, 3, 0), (40, 3, 1)])
 def test_native_chain_loopback_exchange(F, lds, graph):
     """The native exchange with real RCCL traffic on one GPU: a one-rank shard
