@@ -41,3 +41,15 @@ def test_bench_line_schema_small():
         sh = d[key]
         assert "error" not in sh, sh
         assert sh["value"] > 0 and sh["roofline"]["eigen_kat"]["ok"]
+
+
+def test_byte_models_cpu():
+    """bench.py's byte models (no GPU): SURVEY 8(d)'s forward-recurrence B_step
+    and the Clenshaw form, which drops the S read + write (8 B) and adds the
+    X0 read (4 B) per row and column."""
+    sys.path.insert(0, REPO)
+    import bench
+    n, nnz, F = 93_861, 2_315_600, 40
+    assert bench.algorithmic_bytes(n, nnz, F) == 8 * nnz + 4 * (n + 1) + 20 * n * F
+    assert bench.algorithmic_bytes(n, nnz, F) - bench.clenshaw_bytes(n, nnz, F) == 4 * n * F
+    assert bench.algorithmic_bytes(n, nnz, F) == 93_989_048   # the active-row B_step quoted in DESIGN.md 4.1
