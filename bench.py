@@ -89,11 +89,15 @@ def algorithmic_bytes(n: int, nnz: int, F: int) -> int:
     return 8 * nnz + 4 * (n + 1) + 20 * n * F
 
 
-def clenshaw_bytes(n: int, nnz: int, F: int) -> int:
+def clenshaw_bytes(n: int, nnz: int, F: int, unit: bool = False) -> int:
     """The wavelet chain's heat sum by Clenshaw's recurrence:
     CSR 8 B/nnz, int32 row pointers, gather b_{k+1} once, read b_{k+2} and X0,
-    write b_k (fp32) -- no S stream.  SURVEY 8(d)'s forward-recurrence model
+    write b_k (fp32) -- no S stream.  On an unweighted graph (`unit`) the chain
+    carries u = b * dinv and reads no CSR values: 4 B/nnz plus the float64
+    dinv of each row.  SURVEY 8(d)'s forward-recurrence model
     (algorithmic_bytes) is reported beside it as nominal_8d_frac."""
+    if unit:
+        return 4 * nnz + 4 * (n + 1) + 16 * n * F + 8 * n
     return 8 * nnz + 4 * (n + 1) + 16 * n * F
 
 
@@ -276,7 +280,7 @@ def cold_chains(step, L, reps, device):
             "protocol": "512 MiB scratch write before each pass; median pass time"}
 
 
-def f1_companion(lib, L, K, s_heat, steps, device):
+def f1_companion(lib, L, K, s_heat, steps, device, unit=False):
     """The same graph with the reference's own F = 1 signal log1p(rowsum)
     (WATS.py:58-59): the kernel auto-selection's choice and its step time."""
     import wats_hip
@@ -307,7 +311,7 @@ def f1_companion(lib, L, K, s_heat, steps, device):
     avg_ms = p["sum_ms"] / max(1, p["launches"])
     n_active = n - int(L.info["n_closed_form"])
     info = L.lds_plan_info(active_only=True)
-    b_step = lds_algorithmic_bytes(info) if info else clenshaw_bytes(n_active, L.nnz, 1)
+    b_step = lds_algorithmic_bytes(info) if info else clenshaw_bytes(n_active, L.nnz, 1, unit)
     b_8d = algorithmic_bytes(n_active, L.nnz, 1)
     return {"F": 1, "signal": "log1p(rowsum) (WATS.py:58-59)", "value": float(L.nnz) * K / (ms * 1e-3),
             "unit": "edges*K/s", "ms_per_step": ms, "avg_launch_us": avg_ms * 1e3,
@@ -389,6 +393,7 @@ def main():
     F = args.F if args.F is not None else F_def
     g = named_graph(args.config, seed=args.seed + rank)   # independent graph per rank
     st = g.stats()
+    unit = g.values is None or bool(np.all(g.values == 1))   # the value-free Clenshaw chain applies
     L = wats_hip.NormalizedLaplacian.from_graph(g, device=device)
     rng = np.random.default_rng(1 + rank)
     if F == 1:
@@ -451,7 +456,7 @@ def main():
     del Xk, expect
     f1 = None
     if args.f1_companion and F > 1:
-        f1 = f1_companion(lib, L, K, args.s, args.steps, device)
+        f1 = f1_companion(lib, L, K, args.s, args.steps, device, unit)
     edges_k = float(nnz) * K * args.steps
     if world > 1:
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
@@ -465,7 +470,7 @@ def main():
         n_active = n - int(L.info["n_closed_form"])
         b_8d = algorithmic_bytes(n_active, nnz, F)
         lds_info = L.lds_plan_info(active_only=True) if F == 1 else None
-        b_step = lds_algorithmic_bytes(lds_info) if lds_info else clenshaw_bytes(n_active, nnz, F)
+        b_step = lds_algorithmic_bytes(lds_info) if lds_info else clenshaw_bytes(n_active, nnz, F, unit)
         achieved = b_step / (avg_ms * 1e-3) / 1e9
         traffic, traffic_src = None, None
         tj = args.traffic_json
@@ -508,7 +513,8 @@ def main():
                                    if traffic is not None else None),
                 "kernel": lds_kernel_name(lds_info),
                 "byte_model": _byte_model(lds_info) if lds_info else
-                              "Clenshaw heat sum (DESIGN.md 4.1): 8 B/nnz + 4(N+1) + 16 N F",
+                              ("Clenshaw heat sum on u = b dinv (DESIGN.md 4.1): 4 B/nnz + 4(N+1) + 16 N F + 8 N"
+                               if unit else "Clenshaw heat sum (DESIGN.md 4.1): 8 B/nnz + 4(N+1) + 16 N F"),
                 "algorithmic_bytes_per_launch": b_step,
                 "rows_per_launch": n_active,
                 "closed_form_rows": n - n_active,

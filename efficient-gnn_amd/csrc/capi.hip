@@ -117,6 +117,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "clenshaw")) {
     L->tune.clenshaw = value ? 1 : 0;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "uscale")) {
+    L->tune.uscale = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hubf")) {
     L->tune.hubf = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 4096));
     return WG_OK;  // launch-time choice
@@ -300,10 +303,16 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     double cacc = 2.0 * c[K];        // the implicit b_K = c_K X0 enters through the SpMM scale
     float* bufs[2] = {(K & 1) ? sint : b1, (K & 1) ? b1 : sint};
     int nb = 0;
+    // unweighted graphs: every stored b_k as u_k = b_k * dinv, so the gathers read no CSR values
+    // (L_hat b = -dinv_i sum_j u_j); X0 itself stays unscaled (the first step reads the values)
+    const int useu = (L->unit && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 && L->tune.hot == 0) ? 1 : 0;
     for (int32_t k = K - 1; k >= 1; --k) {
       float* out = bk2 ? bk2 : bufs[nb++];
       const double ck = c[k] - (bk2 == nullptr && k + 2 == K ? c[K] : 0.0);  // implicit b_{k+2} = c_K X0
       ClenArgs cl{b0, ck, cacc, 0};
+      cl.uin = useu && bk1 != b0;
+      cl.uprev = useu && bk2 != nullptr;
+      cl.uout = useu;
       rc = launch_step(L, 2, Fp, bk1, bk2, out, nullptr, nullptr, 1.0, 0.0, stream, /*active_only=*/true, nullptr, &cl);
       if (rc) return rc;
       bk2 = const_cast<float*>(bk1 == b0 ? nullptr : bk1);
@@ -313,6 +322,8 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     // final: S = c_0 X0 + L_hat b_1 - b_2 (K == 1: L_hat b_1 = c_1 L_hat X0; K == 2: b_2 = c_2 X0)
     const double c0 = c[0] - (K == 2 ? c[2] : 0.0);
     ClenArgs cl{b0, c0, K == 1 ? c[1] : 1.0, 1};
+    cl.uin = useu && bk1 != b0;
+    cl.uprev = useu && K >= 3;
     rc = launch_step(L, 2, Fp, bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
                      1.0, 0.0, stream, /*active_only=*/true, fuse_fin ? S : nullptr, &cl);
     if (rc) return rc;

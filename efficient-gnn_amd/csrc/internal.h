@@ -139,6 +139,7 @@ struct Tuning {
   int32_t lds_k = 4;         // windows: chunks per lane (1 = cheb_lds2_kernel, 2 / 4 = cheb_lds3_kernel)
   int32_t fuse_finalize = 1;  // wavelet_features: closed rows in the permute-in, S / H from the last step
   int32_t clenshaw = 1;      // wavelet_features (F > 1 / weighted): heat sum by Clenshaw's recurrence (no S stream)
+  int32_t uscale = 1;        // Clenshaw on unweighted graphs: carry u = b * dinv, gathers read no CSR values
   int32_t hub_vidx = 0;      // hub teams: 1 = 16-B column loads, 4 consecutive entries per lane (s26, 8M R-MAT: 1725 vs 1299 us, off)
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
@@ -199,6 +200,9 @@ struct ClenArgs {
   double ck;
   double cacc;
   int final_;
+  // unweighted graphs (L->unit): the chain vectors as u = b * dinv (no CSR values read);
+  // uin: xm1 is u, uprev: xm2 is u, uout: write u (not on the final step)
+  int uin = 0, uprev = 0, uout = 0;
 };
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,

@@ -61,6 +61,11 @@ struct StepArgs {
   int32_t clen;        // 0 = forward recurrence + heat sum; 1 / 2 = Clenshaw step / final (ClenArgs)
   const float* x0;     // Clenshaw: X0 rows (internal order, stride ld)
   double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc - xm2
+  // Clenshaw on unweighted graphs (L_hat_ij = -dinv_i dinv_j): the chain carries u = b * dinv, so the
+  // gathers need no values (val == nullptr: every value 1).  uin: xm1 holds u; uprev: xm2 holds u;
+  // uout: xk gets u.
+  const double* dinv;
+  int32_t uin, uprev, uout;
 };
 
 template <int VEC>
@@ -111,6 +116,7 @@ struct EpiIn {
   float sold[VEC];  // S own row (k >= 2); Clenshaw: X0 own row
   int iso;
   int32_t orow;     // out_perm[row] (finalize fused into the last step)
+  double dinv;      // Clenshaw on u = b * dinv: dinv of the row
 };
 
 template <int VEC>
@@ -119,6 +125,7 @@ __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int
   in.iso = a.iso[row];
   in.orow = a.out_perm ? a.out_perm[row] : (int32_t)row;
   if (a.clen) {
+    in.dinv = (a.uin | a.uprev | a.uout) ? a.dinv[row] : 1.0;
     if (a.xm2) {
       load_vec<VEC>(a.xm2 + off, in.prev);
     } else {
@@ -140,6 +147,10 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
                                               const EpiIn<VEC>& in, int lane0) {
   const int64_t off = row * a.ld + (int64_t)fs * VEC;
   const bool nt_st = (a.nt & 4) != 0;
+  if (a.clen && a.uin) {  // sum of u_j over the row: L_hat b = -dinv_i * sum (off-diagonal part)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] *= -in.dinv;
+  }
   if (in.iso) {  // L_hat_ii = -1 (scipy setdiag(1 - iso), then "- identity")
     float x[VEC];
     if (a.k == 1) {
@@ -148,13 +159,24 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
     } else {
       load_vec<VEC>(a.xm1 + off, x);
     }
+    const double xs = (a.clen && a.uin) ? 1.0 / in.dinv : 1.0;  // own row of u -> b
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] -= (double)x[j];
+    for (int j = 0; j < VEC; ++j) acc[j] -= (double)x[j] * xs;
   }
   double t[VEC];
   if (a.clen) {  // Clenshaw: b = ck * X0 + cacc * (L_hat b') - b''
+    const double ps = a.uprev ? 1.0 / in.dinv : 1.0;
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) t[j] = a.ck * (double)in.sold[j] + a.cacc * acc[j] - (double)in.prev[j];
+    for (int j = 0; j < VEC; ++j)
+      t[j] = a.ck * (double)in.sold[j] + a.cacc * acc[j] - (double)in.prev[j] * ps;
+    if (a.uout && a.xk) {
+      double u[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) u[j] = t[j] * in.dinv;
+      if (nt_st) store_vec_nt<VEC>(a.xk + off, u);
+      else store_vec<VEC>(a.xk + off, u);
+      return;  // never the final step (S is written only there)
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) t[j] = (a.k == 1) ? acc[j] : 2.0 * acc[j] - (double)in.prev[j];
@@ -214,7 +236,7 @@ __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       c[u] = col[e + u * stride];
-      v[u] = val[e + u * stride];
+      v[u] = val ? val[e + u * stride] : 1.0f;
     }
     float x[4][VEC];
 #pragma unroll
@@ -226,7 +248,7 @@ __device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t
   }
   for (; e < e1; e += stride) {
     const int32_t c = col[e];
-    const float v = val[e];
+    const float v = val ? val[e] : 1.0f;
     float x[VEC];
     load_vec<VEC>(xb + (int64_t)c * ld, x);
 #pragma unroll
@@ -298,7 +320,7 @@ __device__ __forceinline__ void accumulate_hot1(const StepArgs& a, int32_t e, in
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       c[u] = col[e + u * stride];
-      v[u] = val[e + u * stride];
+      v[u] = val ? val[e + u * stride] : 1.0f;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) x[u] = hot_or_global(hot, xb, c[u], H, ld);
@@ -334,7 +356,7 @@ __device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, i
     if (tt < n) {
       const int32_t idx = e + tt * stride;
       myc = a.col[idx];
-      myv = a.val[idx];
+      myv = a.val ? a.val[idx] : 1.0f;
     }
     const int cnt = min(LF, n - t0);
     for (int j = 0; j < cnt; j += U) {
@@ -447,7 +469,7 @@ __device__ __forceinline__ void accumulate_vidx1(const StepArgs& a, int32_t e0, 
   const int32_t eb = e0 & ~3;
   for (int32_t q = eb + 4 * ns; q < e1; q += 4 * stride) {
     const int4 c = *reinterpret_cast<const int4*>(a.col + q);
-    const float4 v = *reinterpret_cast<const float4*>(a.val + q);
+    const float4 v = a.val ? *reinterpret_cast<const float4*>(a.val + q) : make_float4(1.f, 1.f, 1.f, 1.f);
     const int32_t cc[4] = {c.x, c.y, c.z, c.w};
     const float vv[4] = {v.x, v.y, v.z, v.w};
     float x[4];
@@ -1181,6 +1203,11 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       a.ck = cl->ck;
       a.cacc = cl->cacc;
       if (!cl->final_) a.S = nullptr;
+      a.dinv = L->dinv;
+      a.uin = cl->uin;
+      a.uprev = cl->uprev;
+      a.uout = cl->final_ ? 0 : cl->uout;
+      if (a.uin) a.val = nullptr;  // unweighted: the gathered u needs no values
     }
     a.chunks = plan->chunks;
     a.partial = plan->partial;

@@ -53,3 +53,5 @@ def test_byte_models_cpu():
     assert bench.algorithmic_bytes(n, nnz, F) == 8 * nnz + 4 * (n + 1) + 20 * n * F
     assert bench.algorithmic_bytes(n, nnz, F) - bench.clenshaw_bytes(n, nnz, F) == 4 * n * F
     assert bench.algorithmic_bytes(n, nnz, F) == 93_989_048   # the active-row B_step quoted in DESIGN.md 4.1
+    # unweighted: no CSR values (4 B/nnz), plus the float64 dinv of each row
+    assert bench.clenshaw_bytes(n, nnz, F) - bench.clenshaw_bytes(n, nnz, F, unit=True) == 4 * nnz - 8 * n

@@ -329,6 +329,30 @@ def test_clenshaw_heat_sum_vs_forward_and_oracle(k, F, fuse):
         assert_parity(_np(H), ref["H"], what=f"K={k} F={F} {tag} H")
 
 
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 16])
+@pytest.mark.parametrize("F,knobs", [(4, {}), (40, {}), (40, dict(fuse_finalize=0)), (130, {}), (6, {}),
+                                     (1, dict(lds=0)), (1, dict(lds=0, vidx=1)), (40, dict(bcast=0)),
+                                     (40, dict(iter=2, block_iter=1, chunk_iter=1))])
+def test_clenshaw_value_free_unweighted(k, F, knobs):
+    """Unweighted graphs: the Clenshaw chain carries u = b * dinv and gathers
+    no CSR values (L_hat_ij = -dinv_i dinv_j); isolated rows, split / block /
+    team rows, every gather variant, against the oracle and against the
+    valued form (uscale = 0)."""
+    g = rmat_graph(3000, 30000, seed=k + F)
+    A = g.to_scipy()
+    X = np.random.default_rng(k * F).standard_normal((g.n, F)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=k, s=0.8, X0=X, return_all=True)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(uscale=1, **knobs)
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=k, X0=torch.from_numpy(X), return_S=True)
+    L.tune(uscale=0)
+    H0, S0 = wats_hip.graph_wavelet_features(L, k=k, X0=torch.from_numpy(X), return_S=True)
+    for S, H, tag in ((S1, H1, "u-scaled"), (S0, H0, "valued")):
+        assert_parity(_np(S), ref["S"], what=f"K={k} F={F} {knobs} {tag} S")
+        if F > 1:
+            assert_parity(_np(H), ref["H"], what=f"K={k} F={F} {knobs} {tag} H")
+
+
 # ----------------------------------------------------------------- F == 1 column-blocked LDS kernel
 @pytest.mark.parametrize("knobs", [dict(lds=0), dict(lds=1), dict(lds=1, lds_cb=2048), dict(lds=1, lds_cb=1024, lds_iter=2),
                                    dict(lds=1, lds_cb=4096, lds_iter=64, lds_wg=7),
