@@ -3,8 +3,9 @@
 
 One "step" = one full ``graph_wavelet_features`` pass (reference
 calibration/WATS.py:39-74) over a device-resident graph: permute the signal
-into the internal order, K fused Chebyshev steps (T_k = 2 L_hat T_{k-1} -
-T_{k-2}, S += alpha_k T_k), then S / H back to caller order.  The Laplacian
+into the internal order, K fused SpMM steps evaluating S = sum_k alpha_k
+T_k(L_hat) X0 by Clenshaw's recurrence (value-free gathers on
+an unweighted graph), the last one writing S / H in caller order.  The Laplacian
 prologue (a1-a3) is built once before timing, as the reference builds it once
 per WATS construction.
 
@@ -21,9 +22,10 @@ ONE graph (e.g. --config reddit / rmat-8m) into row blocks over the ranks with a
 per-step RCCL halo exchange (strong scaling), see DESIGN.md section 7.
 
 Also printed in the same JSON line:
-  roofline      -- the step kernel's algorithmic bytes (SURVEY.md 8(d):
-                   B_step = 8 nnz + 4 (N+1) + 20 N F) / its mean duration from
-                   HIP events recorded live around every step launch;
+  roofline      -- the step kernel's algorithmic bytes (clenshaw_bytes; SURVEY.md
+                   8(d)'s B_step = 8 nnz + 4 (N+1) + 20 N F beside it as
+                   nominal_8d_frac) / its mean duration from HIP events
+                   recorded live around every step launch;
   cpu_baseline  -- the oracle (scipy/numpy restatement of the reference, one
                    thread) on the same graph, rank 0 at N=1 only.
 """
