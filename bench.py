@@ -22,10 +22,11 @@ ONE graph (e.g. --config reddit / rmat-8m) into row blocks over the ranks with a
 per-step RCCL halo exchange (strong scaling), see DESIGN.md section 7.
 
 Also printed in the same JSON line:
-  roofline      -- the step kernel's algorithmic bytes (clenshaw_bytes; SURVEY.md
-                   8(d)'s B_step = 8 nnz + 4 (N+1) + 20 N F beside it as
-                   nominal_8d_frac) / its mean duration from HIP events
-                   recorded live around every step launch;
+  roofline      -- SURVEY.md 8(d)'s algorithmic bytes per launch (B_step =
+                   8 nnz + 4 (N+1) + 20 N F over the launched rows) / the step
+                   kernel's mean duration from HIP events recorded live around
+                   every step launch; kernel_bytes_frac: the fewer bytes the
+                   kernel's own algorithm needs (clenshaw_bytes);
   cpu_baseline  -- the oracle (scipy/numpy restatement of the reference, one
                    thread) on the same graph, rank 0 at N=1 only.
 """
@@ -96,8 +97,8 @@ def clenshaw_bytes(n: int, nnz: int, F: int, unit: bool = False) -> int:
     CSR 8 B/nnz, int32 row pointers, gather b_{k+1} once, read b_{k+2} and X0,
     write b_k (fp32) -- no S stream.  On an unweighted graph (`unit`) the chain
     carries u = b * dinv and reads no CSR values: 4 B/nnz plus the float64
-    dinv of each row.  SURVEY 8(d)'s forward-recurrence model
-    (algorithmic_bytes) is reported beside it as nominal_8d_frac."""
+    dinv of each row.  Reported as kernel_bytes_frac beside the roofline's
+    SURVEY 8(d) forward-recurrence model (algorithmic_bytes)."""
     if unit:
         return 4 * nnz + 4 * (n + 1) + 16 * n * F + 8 * n
     return 8 * nnz + 4 * (n + 1) + 16 * n * F
