@@ -353,6 +353,21 @@ def test_clenshaw_value_free_unweighted(k, F, knobs):
             assert_parity(_np(H), ref["H"], what=f"K={k} F={F} {knobs} {tag} H")
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_clenshaw_value_free_directed_selfloops(seed):
+    """The value-free chain on unweighted DIRECTED graphs with self loops and
+    isolated nodes (w = column sum minus the diagonal, WATS.py:26 -> scipy
+    _laplacian.py:467): L_hat_ij = -dinv_i dinv_j still holds off the diagonal."""
+    g = random_graph(900, 0.01, seed=seed, directed=True, weighted=False, self_loop_frac=0.1, isolated_frac=0.1)
+    A = g.to_scipy()
+    X = np.random.default_rng(seed).standard_normal((g.n, 8)).astype(np.float32)
+    for k in (3, 8):
+        ref = O.graph_wavelet_features(A, k=k, s=0.8, X0=X, return_all=True)
+        H, S = wats_hip.graph_wavelet_features(A, k=k, s=0.8, X0=torch.from_numpy(X), return_S=True)
+        assert_parity(_np(S), ref["S"], what=f"directed unweighted seed={seed} K={k} S")
+        assert_parity(_np(H), ref["H"], what=f"directed unweighted seed={seed} K={k} H")
+
+
 # ----------------------------------------------------------------- F == 1 column-blocked LDS kernel
 @pytest.mark.parametrize("knobs", [dict(lds=0), dict(lds=1), dict(lds=1, lds_cb=2048), dict(lds=1, lds_cb=1024, lds_iter=2),
                                    dict(lds=1, lds_cb=4096, lds_iter=64, lds_wg=7),
