@@ -998,9 +998,11 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // Defaults measured on MI355X (profiles/r01 sweeps): wide signals (G = 64/LF
 // small, e.g. F = 40 -> G = 6) want long per-sub-group runs; F = 1 (G = 64)
 // shorter ones.
-// Wide tiles (F >= 16) on large graphs: one sub-group per row up to 96 entries per
-// lane (ogbn-arxiv-size F=40: 41.8 vs 45.5 us per step with iter 24; F=64 56.3 vs
-// 64.9; Reddit-size F=44 1732 vs 1817 us) and long split-row chunks (Reddit-size
+// Wide tiles (F >= 16) on large graphs: one sub-group per row up to 192 entries per
+// lane (ogbn-arxiv-size F=40: 41.8 vs 45.5 us per step with iter 96 vs 24; F=64 56.3
+// vs 64.9; Reddit-size F=44 1732 vs 1817 us; with the value-free Clenshaw chain,
+// s47-s49: 192 vs 96 -- arxiv F=40 37.3 vs 38.2, F=64 49.9 vs 51.8, Reddit-size F=44
+// 1497 vs 1522; 256 jumps to 55 us) and long split-row chunks (Reddit-size
 // F=44: 1625 us with chunk_iter 128 vs 1729 with 64; arxiv neutral); small graphs
 // keep more lanes per row for latency (PubMed-size F=40: 9.3 us with iter 24, 17.2
 // with 96).  F = 1 from 1 M nonzeros: 8 entries per lane (ogbn-arxiv-size: 10.7 us per
@@ -1008,7 +1010,7 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter) {
   const bool wide = G <= 16;
   const bool big = nnz >= (int64_t)1 << 20;
-  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 96 : 24) : (G == 64 && big ? 8 : 16));
+  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 192 : 24) : (G == 64 && big ? 8 : 16));
   *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
   *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (big ? 128 : 32) : 16);
 }
