@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle-s", type=float, default=0.5,
+                    help="seconds of untimed passes after the W warmup passes (clock ramp); reported as settle_s")
     ap.add_argument("--config", default="ogbn-arxiv")
     ap.add_argument("--K", type=int, default=None)
     ap.add_argument("--F", type=int, default=None)
@@ -63,7 +65,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--traffic-json", default="auto",
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py); "
-                         "'auto': the committed PMC summary of the default workload (profiles/r01/s44_traffic.json, "
+                         "'auto': the committed PMC summary of the default workload (profiles/r01/s50_traffic.json, "
                          "tools/gpu_session.sh RUN_PMC=1) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--sharded-extra", default="reddit,rmat-8m",
@@ -421,6 +423,14 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(device)
+    # Clock settle (untimed, reported as settle_s): W passes are ~2 ms of load at the
+    # defaults, short of the clock ramp (profiles/r01/s51_iter_sweep.log: the first
+    # measurement of a fresh process reads 2-3 us/step slow on arxiv F=40).
+    t_settle = time.perf_counter() + args.settle_s
+    while time.perf_counter() < t_settle:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize(device)
 
     def timed(profile: bool):
         """K passes bracketed by barrier + synchronize; with `profile`, HIP
@@ -485,7 +495,7 @@ def main():
         traffic, traffic_src = None, None
         tj = args.traffic_json
         if tj == "auto":
-            tj = os.path.join(REPO, "profiles", "r01", "s44_traffic.json") \
+            tj = os.path.join(REPO, "profiles", "r01", "s50_traffic.json") \
                 if (args.config == "ogbn-arxiv" and F == 40 and K == 16) else None
         if tj and tj != "none" and os.path.exists(tj):
             traffic = json.load(open(tj)).get("bytes_per_launch")
@@ -497,6 +507,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_s": args.settle_s,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",

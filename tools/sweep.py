@@ -53,6 +53,7 @@ def main():
                     help="knob grid, e.g. 'iter=16,24;chunk_iter=64,128;nt=0,7'")
     ap.add_argument("--segments", action="store_true")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--warm-s", type=float, default=1.0, help="seconds of untimed chains before the grid")
     ap.add_argument("--keep-order", action="store_true", help="WG_FLAG_KEEP_COLUMN_ORDER (no per-row column sort)")
     a = ap.parse_args()
     global REPS
@@ -74,6 +75,11 @@ def main():
     bstep = 8 * L.nnz + 4 * (n_act + 1) + 20 * n_act * F
     grid = [(kv.split("=")[0], [int(v) for v in kv.split("=")[1].split(",")]) for kv in a.grid.split(";") if kv]
     names = [k for k, _ in grid]
+    # Clock ramp: without ~1 s of load first, the first grid entry reads 2-3 us slow
+    # on arxiv F=40 (profiles/r01/s48_ab.log round 0, s51_iter_sweep.log).
+    t_end = time.perf_counter() + a.warm_s
+    while time.perf_counter() < t_end:
+        time_chain(L, X, K, reps=2)
     first = None
     for combo in itertools.product(*[v for _, v in grid]):
         knobs = dict(zip(names, combo))
