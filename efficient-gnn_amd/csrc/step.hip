@@ -1003,7 +1003,8 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // vs 64.9; Reddit-size F=44 1732 vs 1817 us; with the value-free Clenshaw chain,
 // s47-s49: 192 vs 96 -- arxiv F=40 37.3 vs 38.2, F=64 49.9 vs 51.8, Reddit-size F=44
 // 1497 vs 1522; 256 jumps to 55 us) and long split-row chunks (Reddit-size
-// F=44: 1625 us with chunk_iter 128 vs 1729 with 64; arxiv neutral); small graphs
+// F=44: 1625 us with chunk_iter 128 vs 1729 with 64) above 16 M nonzeros, 64 below
+// (arxiv F=40 36.5 vs 37.1 us, F=64 neutral; profiles/r01/s55_chunk_sweep.log); small graphs
 // keep more lanes per row for latency (PubMed-size F=40: 9.3 us with iter 24, 17.2
 // with 96).  F = 1 from 1 M nonzeros: 8 entries per lane (ogbn-arxiv-size: 10.7 us per
 // step vs 11.6 with 16, s34).
@@ -1012,7 +1013,8 @@ void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_it
   const bool big = nnz >= (int64_t)1 << 20;
   *iter = t.iter > 0 ? t.iter : (wide ? (big ? 192 : 24) : (G == 64 && big ? 8 : 16));
   *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
-  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (big ? 128 : 32) : 16);
+  const bool huge = nnz >= (int64_t)1 << 24;
+  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (huge ? 128 : big ? 64 : 32) : 16);
 }
 
 // Build (once per tile shape) the segment table and the split-row chunk table.
