@@ -70,6 +70,10 @@ int wg_laplacian_get_info(wg_laplacian_t L, wg_laplacian_info* info) {
 
 int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   if (!L || !key) return fail(WG_ERR_INVALID, "wg_laplacian_tune: NULL argument");
+  // any knob -- plan-shaping or launch-time -- invalidates a chain captured into a
+  // hipGraph (dist.hip keys its exec on this counter): plan buffers are freed below,
+  // and launch-time knobs are baked into the captured kernel arguments
+  ++L->tune_gen;
   if (!strcmp(key, "iter")) {
     if (value < 1) return fail(WG_ERR_INVALID, "iter must be >= 1");
     L->tune.iter = (int32_t)value;

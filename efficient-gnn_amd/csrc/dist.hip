@@ -134,8 +134,9 @@ struct GraphKey {
   int64_t F;
   int32_t K;
   double s;
+  int64_t gen;  // the handle's tune_gen: wg_laplacian_tune frees plans and changes launch knobs
   bool operator==(const GraphKey& o) const {
-    return X0 == o.X0 && S == o.S && H == o.H && F == o.F && K == o.K && s == o.s;
+    return X0 == o.X0 && S == o.S && H == o.H && F == o.F && K == o.K && s == o.s && gen == o.gen;
   }
 };
 
@@ -457,7 +458,7 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   if (!D->comm && !D->ipc && (D->n_send > 0 || D->n_halo > 0 || D->world > 1))
     return fail(WG_ERR_INVALID, "wg_dist_wavelet_features: no exchange (no RCCL id given and IPC not connected)");
   hipStream_t st = as_stream(stream_);
-  const GraphKey key{X0, S, H, F, K, s};
+  const GraphKey key{X0, S, H, F, K, s, D->L->tune_gen};
   if (!(key == D->key)) {
     if (D->exec) {
       WG_HIP_TRY(hipStreamSynchronize(D->cap));

@@ -163,6 +163,7 @@ struct wg_laplacian_s {
   int64_t n_active = 0;       // rows [0, n_active) enter the chain in wg_wavelet_features
   int64_t n_closed = 0;       // purely isolated rows at the end: T_k = (-1)^k X0 (closed form)
   wg::Tuning tune;
+  int64_t tune_gen = 0;       // bumped by every wg_laplacian_tune: captured chains (dist.hip) re-capture
   std::map<int, wg::Plan> plans;  // key: (LF * 8 + VEC) * 2 + active_only
   // unweighted graph (every off-diagonal a_ij == 1): L_hat_ij = -dinv_i dinv_j
   // up to scipy's float32 rounding, so the F == 1 LDS kernel reads no values

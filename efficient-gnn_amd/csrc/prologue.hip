@@ -596,6 +596,39 @@ int wg_laplacian_create(int64_t n_rows, int64_t n_cols, int64_t nnz, const int64
   return WG_OK;
 }
 
+// A literal operator (every stored entry kept with its value, diagonal included,
+// nothing normalised): what chebyshev_polynomials(L, k, X0) applies when the
+// caller hands it an explicit matrix (reference calibration/WATS.py:29-37 is
+// called with L_rescaled, a float64 scipy CSR, at WATS.py:62).
+int wg_operator_create(int64_t n, int64_t nnz, const int64_t* indptr, const int32_t* indices, const float* values,
+                       uint32_t flags, void* stream_, wg_laplacian_t* out) {
+  if (!out) return fail(WG_ERR_INVALID, "wg_operator_create: out is NULL");
+  *out = nullptr;
+  if (n < 0 || nnz < 0 || !indptr || (nnz > 0 && (!indices || !values)))
+    return fail(WG_ERR_INVALID, "wg_operator_create: bad shape (n=%lld nnz=%lld)", (long long)n, (long long)nnz);
+  if (nnz > INT32_MAX || n > INT32_MAX) return fail(WG_ERR_UNSUPPORTED, "wg_operator_create: nnz/n exceed int32");
+  auto* L = new wg_laplacian_s();
+  if (hipGetDevice(&L->device) != hipSuccess) {
+    delete L;
+    return fail(WG_ERR_HIP, "wg_operator_create: no HIP device");
+  }
+  L->n_rows = n;
+  L->n_cols = n;
+  L->nnz_input = nnz;
+  L->reordered = !(flags & WG_FLAG_NO_REORDER);
+  int rc = build_operator(L, indptr, indices, values, nullptr, /*raw=*/true, as_stream(stream_));
+  if (rc == WG_OK && !(flags & WG_FLAG_KEEP_COLUMN_ORDER)) rc = sort_row_columns(L, as_stream(stream_));
+  if (rc == WG_OK && hipStreamSynchronize(as_stream(stream_)) != hipSuccess)
+    rc = fail(WG_ERR_HIP, "wg_operator_create: sync");
+  if (rc != WG_OK) {
+    (void)hipStreamSynchronize(as_stream(stream_));
+    delete L;
+    return rc;
+  }
+  *out = L;
+  return WG_OK;
+}
+
 int wg_laplacian_destroy(wg_laplacian_t L) {
   if (!L) return WG_OK;
   int cur = 0;

@@ -15,8 +15,8 @@ Differences: the features are computed on the GPU from the dense ``adj``
 ``k``/``s`` (defaults 3 / 0.8 as hard-coded at WATS.py:99), ``X0`` (signal),
 ``graph`` (a sparse graph to use instead of the dense ``adj`` for the
 features), ``wavelet_feats`` (precomputed features, e.g. a cache),
-``fused_head`` (default on: the temperature head + log_softmax as the fused
-HIP kernels of ``head.py``; off: the reference's torch ops) and
+``fused_head`` (default off: the reference's torch ops; on: the temperature
+head + log_softmax as the fused HIP kernels of ``head.py``) and
 ``verbose``; ``fit()`` is an alias of ``calib_train``.
 """
 from __future__ import annotations
@@ -43,7 +43,7 @@ def accuracy(outputs: torch.Tensor, labels: torch.Tensor) -> float:
 
 class WATS(torch.nn.Module):
     def __init__(self, base_model, features, labels, adj, val_mask, *, k: int = 3, s: float = 0.8, X0=None,
-                 graph=None, wavelet_feats=None, verbose: bool = True, fused_head: bool = True):
+                 graph=None, wavelet_feats=None, verbose: bool = True, fused_head: bool = False):
         super().__init__()
         self.fused_head = bool(fused_head) and torch.cuda.is_available()
         # WATS.py:91 picks cuda when available; the HIP feature path requires it.

@@ -51,6 +51,7 @@ SIGNATURES = {
     "wg_column_degree": (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wg_laplacian_create": (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_u32, c_vp,
                                            ctypes.POINTER(c_vp)]),
+    "wg_operator_create": (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_vp, ctypes.POINTER(c_vp)]),
     "wg_laplacian_destroy": (ctypes.c_int, [c_vp]),
     "wg_laplacian_get_info": (ctypes.c_int, [c_vp, ctypes.POINTER(LaplacianInfo)]),
     "wg_laplacian_export": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

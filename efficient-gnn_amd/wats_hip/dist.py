@@ -54,7 +54,13 @@ def partition_rows(indptr: np.ndarray, world: int) -> np.ndarray:
     targets = (np.arange(1, world) * total) // world
     cuts = np.searchsorted(weight, targets, side="left")
     bounds = np.concatenate([[0], np.clip(cuts, 0, n), [n]]).astype(np.int64)
-    return np.maximum.accumulate(bounds)
+    bounds = np.maximum.accumulate(bounds)
+    if n >= world:
+        # hub rows can swallow several targets: keep every shard non-empty
+        # (shard q keeps >= 1 row and leaves >= world - q - 1 rows to the rest)
+        for q in range(1, world):
+            bounds[q] = min(max(bounds[q], bounds[q - 1] + 1), n - (world - q))
+    return bounds
 
 
 @dataclass
@@ -474,7 +480,9 @@ class ShardedWavelet:
             self.close()
             self._ipc_F = F
             self._dist = self._create_ipc(F)
-        if self._dist is not None and p.n_own:
+        if self._dist is not None:
+            # native chain on every rank, empty shards included: a rank with no rows must
+            # still take part in every phase of the exchange (RCCL groups / IPC flags)
             return self._wavelet_features_native(X, k, s, out)
         if F == 1 and k >= 1 and p.n_own and self.u_len() > 0:
             S = self._wavelet_features_u(X, k, s)

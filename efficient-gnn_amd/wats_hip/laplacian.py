@@ -103,8 +103,42 @@ class NormalizedLaplacian:
         self.info = info.as_dict()
         self.n = int(n_rows)
         self.n_cols = n_cols
+        self.is_literal = False
 
     # ------------------------------------------------------------------ builders
+    @classmethod
+    def literal(cls, indptr, indices, values, n: int, reorder: bool = True, sort_columns: bool = True, device=None):
+        """A LITERAL operator: every stored entry applied with its value
+        (float32), diagonal included, nothing normalised (``wg_operator_create``).
+        What :func:`chebyshev_polynomials` applies to an explicit matrix, e.g.
+        the reference's ``L_rescaled`` (calibration/WATS.py:55,62)."""
+        to_t = lambda a, dt: a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a, dtype=dt))
+        device = require_gpu(device)
+        indptr = to_t(indptr, np.int64).to(device=device, dtype=torch.int64).contiguous()
+        indices = to_t(indices, np.int32).to(device=device, dtype=torch.int32).contiguous()
+        values = to_t(values, np.float32).to(device=device, dtype=torch.float32).contiguous()
+        if indptr.numel() != n + 1:
+            raise ValueError("indptr must have n + 1 entries")
+        nnz = int(indices.numel())
+        flags = _lib.WG_FLAG_NONE if reorder else _lib.WG_FLAG_NO_REORDER
+        if not sort_columns:
+            flags |= _lib.WG_FLAG_KEEP_COLUMN_ORDER
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            check(_lib.load().wg_operator_create(n, nnz, ptr(indptr), ptr(indices) if nnz else None,
+                                                 ptr(values) if nnz else None, flags, stream_handle(device),
+                                                 ctypes.byref(handle)), "operator_create")
+        self = cls.__new__(cls)
+        self.device = device
+        self._h = handle
+        info = LaplacianInfo()
+        check(_lib.load().wg_laplacian_get_info(self._h, ctypes.byref(info)), "laplacian_get_info")
+        self.info = info.as_dict()
+        self.n = int(n)
+        self.n_cols = int(n)
+        self.is_literal = True
+        return self
+
     @classmethod
     def from_csr(cls, indptr, indices, values=None, n: int | None = None, **kw):
         if n is None:
@@ -239,5 +273,11 @@ class NormalizedLaplacian:
         except Exception:
             pass
 
+    @property
+    def shape(self):
+        return (self.n, self.n_cols)
+
     def __repr__(self):
+        if self.is_literal:
+            return f"NormalizedLaplacian.literal(n={self.n}, nnz={self.nnz}, device={self.device})"
         return f"NormalizedLaplacian(n={self.n}, nnz={self.nnz}, isolated={self.info['n_isolated']}, device={self.device})"

@@ -2,7 +2,8 @@
 
 Same names, argument meaning and defaults as ``calibration/WATS.py``:
 
-* :func:`compute_normalized_laplacian` -- WATS.py:24-27 (+ the rescale of :55);
+* :func:`compute_normalized_laplacian` -- WATS.py:24-27 (``L_sym``; the
+  rescale of :55 is the reference's own arithmetic on the returned object);
 * :func:`chebyshev_polynomials`        -- WATS.py:29-37;
 * :func:`graph_wavelet_features`       -- WATS.py:39-74 (``k=3, s=0.8``).
 
@@ -16,6 +17,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -26,6 +28,8 @@ from .laplacian import NormalizedLaplacian, require_gpu, stream_handle
 def as_laplacian(adj, **kw) -> NormalizedLaplacian:
     if isinstance(adj, NormalizedLaplacian):
         return adj
+    if isinstance(adj, SymNormalizedLaplacian):
+        return adj.laplacian_hat()
     if isinstance(adj, torch.Tensor):
         if adj.is_sparse or adj.layout == torch.sparse_csr:
             a = adj.to_sparse_csr()
@@ -43,13 +47,186 @@ def as_laplacian(adj, **kw) -> NormalizedLaplacian:
     return NormalizedLaplacian.from_dense(torch.as_tensor(np.asarray(adj, dtype=np.float32)), **kw)
 
 
-def compute_normalized_laplacian(adj, **kw) -> NormalizedLaplacian:
-    """Device ``L_hat = (2/2.0)*laplacian(adj, normed=True) - I`` (WATS.py:24-27, :55)."""
-    return as_laplacian(adj, **kw)
+def _scalar(c):
+    import numbers
+    if isinstance(c, numbers.Real) and not isinstance(c, bool):
+        return float(c)
+    if isinstance(c, (np.floating, np.integer)) or (isinstance(c, np.ndarray) and c.ndim == 0):
+        return float(c)
+    return None
+
+
+def _identity_multiple(other, n: int):
+    """``d`` if ``other`` is ``d * identity(n)`` (scipy sparse, numpy or torch), else None."""
+    import scipy.sparse as sp
+    if sp.issparse(other):
+        if other.shape != (n, n):
+            return None
+        o = sp.csr_matrix(other)
+        o.sum_duplicates()
+        o.eliminate_zeros()
+        diag = o.diagonal()
+        if o.nnz != np.count_nonzero(diag) or (n and not np.all(diag == diag[0])):
+            return None
+        return float(diag[0]) if n else 0.0
+    return None
+
+
+class SymNormalizedLaplacian:
+    """``scale * L_sym - shift * I`` of an adjacency, with
+    ``L_sym = I - D^{-1/2} A D^{-1/2}`` exactly as scipy's
+    ``csgraph.laplacian(adj, normed=True)`` builds it (the value
+    :func:`compute_normalized_laplacian` returns, reference
+    calibration/WATS.py:24-27).
+
+    Supports the reference's own arithmetic on it -- ``(2 / 2.0) * L -
+    identity(N)`` (WATS.py:55) -- and ``@`` with a signal.  Nothing touches the
+    GPU until the operator is used: the rescale the reference performs maps to
+    the device L_hat handle (:class:`NormalizedLaplacian`, the fused step
+    kernels); any other scale / shift is applied literally (a valued CSR,
+    ``wg_operator_create``)."""
+
+    def __init__(self, adj, scale: float = 1.0, shift: float = 0.0, _base=None):
+        self.adj = adj
+        self.scale = float(scale)
+        self.shift = float(shift)
+        self._base = _base if _base is not None else {}   # shared: the built L_hat handle
+        n = adj.n if (isinstance(adj, NormalizedLaplacian) or not hasattr(adj, "shape")) else adj.shape[0]
+        self.shape = (int(n), int(n))
+
+    # ---- the reference's arithmetic (WATS.py:55): scalar * L, L -/+ d * identity(N)
+    def _with(self, scale, shift):
+        return SymNormalizedLaplacian(self.adj, scale, shift, self._base)
+
+    def __mul__(self, c):
+        c = _scalar(c)
+        if c is None:
+            return NotImplemented
+        return self._with(self.scale * c, self.shift * c)
+
+    __rmul__ = __mul__
+
+    def __truediv__(self, c):
+        c = _scalar(c)
+        if c is None:
+            return NotImplemented
+        return self._with(self.scale / c, self.shift / c)
+
+    def __neg__(self):
+        return self._with(-self.scale, -self.shift)
+
+    def __sub__(self, other):
+        d = _identity_multiple(other, self.shape[0])
+        if d is None:
+            raise NotImplementedError("wats_hip: only scalar multiples of identity(N) can be subtracted from L")
+        return self._with(self.scale, self.shift + d)
+
+    def __add__(self, other):
+        d = _identity_multiple(other, self.shape[0])
+        if d is None:
+            raise NotImplementedError("wats_hip: only scalar multiples of identity(N) can be added to L")
+        return self._with(self.scale, self.shift - d)
+
+    __radd__ = __add__
+
+    @property
+    def is_rescaled(self) -> bool:
+        """True for ``L_sym - I`` = L_hat, the operator of the fused chain."""
+        return self.scale == 1.0 and self.shift == 1.0
+
+    # ---- device operators
+    def laplacian_hat(self) -> NormalizedLaplacian:
+        """The device handle of ``L_hat = L_sym - I`` (built once, shared by
+        every scaled copy of this object)."""
+        L = self._base.get("L_hat")
+        if L is None:
+            L = self.adj if isinstance(self.adj, NormalizedLaplacian) else as_laplacian(self.adj)
+            self._base["L_hat"] = L
+        return L
+
+    def operator(self) -> NormalizedLaplacian:
+        """The handle :func:`chebyshev_polynomials` applies: the L_hat handle
+        for the reference's rescale, else a literal ``scale * L_sym - shift * I``."""
+        if self.is_rescaled:
+            return self.laplacian_hat()
+        key = ("literal", self.scale, self.shift)
+        op = self._base.get(key)
+        if op is None:
+            L = self.laplacian_hat()
+            indptr, indices, values, iso = L.export()
+            n = L.n
+            # off-diagonal: scale * L_sym_ij (= scale * L_hat_ij); diagonal: scale * (1 - iso) - shift
+            rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+            diag = self.scale * (1.0 - iso.astype(np.float64)) - self.shift
+            r = np.concatenate([rows, np.arange(n, dtype=np.int64)])
+            c = np.concatenate([indices.astype(np.int64), np.arange(n, dtype=np.int64)])
+            v = np.concatenate([self.scale * values.astype(np.float64), diag])
+            order = np.lexsort((c, r))
+            r, c, v = r[order], c[order], v[order].astype(np.float32)
+            ip = np.zeros(n + 1, dtype=np.int64)
+            np.cumsum(np.bincount(r, minlength=n), out=ip[1:])
+            op = NormalizedLaplacian.literal(ip, c.astype(np.int32), v, n=n, device=L.device)
+            self._base[key] = op
+        return op
+
+    def __matmul__(self, X):
+        """``(scale L_sym - shift I) X`` on the GPU (float32 (N, F) tensor)."""
+        op = self.operator()
+        return chebyshev_polynomials(op, 1, X)[1]
+
+    def to_scipy(self):
+        """float64 scipy CSR of this operator (caller numbering), for checks."""
+        import scipy.sparse as sp
+        L_hat = self.laplacian_hat().to_scipy()          # L_sym - I
+        n = self.shape[0]
+        return (self.scale * L_hat + (self.scale - self.shift) * sp.identity(n)).tocsr()
+
+    def __repr__(self):
+        return f"SymNormalizedLaplacian(n={self.shape[0]}, scale={self.scale}, shift={self.shift})"
+
+
+def compute_normalized_laplacian(adj, **kw) -> SymNormalizedLaplacian:
+    """``L_sym = I - D^{-1/2} A D^{-1/2}`` (reference calibration/WATS.py:24-27,
+    scipy ``csgraph.laplacian(adj, normed=True)``, ``_laplacian.py:467-475``).
+
+    Returns a :class:`SymNormalizedLaplacian`; the reference's next line,
+    ``L_rescaled = (2 / 2.0) * L - identity(N)`` (WATS.py:55), works on it
+    unchanged and yields the device ``L_hat`` operator that
+    :func:`chebyshev_polynomials` runs on the fused step kernel."""
+    if kw:
+        return SymNormalizedLaplacian(as_laplacian(adj, **kw))
+    return SymNormalizedLaplacian(adj)
+
+
+def as_operator(L) -> NormalizedLaplacian:
+    """What :func:`chebyshev_polynomials` applies, taken LITERALLY (the
+    reference applies whatever matrix it is given, WATS.py:32-36): a
+    :class:`SymNormalizedLaplacian` expression, a device handle, or an
+    explicit scipy / numpy / torch matrix (uploaded as a valued CSR, no
+    normalisation)."""
+    if isinstance(L, SymNormalizedLaplacian):
+        return L.operator()
+    if isinstance(L, NormalizedLaplacian):
+        return L
+    import scipy.sparse as sp
+    if isinstance(L, torch.Tensor):
+        L = L.detach().to_dense().cpu().numpy() if (L.is_sparse or L.layout != torch.strided) else L.detach().cpu().numpy()
+    if not sp.issparse(L):
+        L = np.asarray(L)
+        if L.ndim != 2:
+            raise ValueError("chebyshev_polynomials: L must be a 2-D operator")
+    A = sp.csr_matrix(L)
+    if A.shape[0] != A.shape[1]:
+        raise ValueError("chebyshev_polynomials: L must be square")
+    A.sum_duplicates()
+    return NormalizedLaplacian.literal(A.indptr.astype(np.int64), A.indices.astype(np.int32),
+                                       A.data.astype(np.float32), n=A.shape[0])
 
 
 def _signal(L: NormalizedLaplacian, X0) -> torch.Tensor:
     if X0 is None:
+        if L.is_literal:
+            raise ValueError("X0 is required with an explicit operator (the reference passes it, WATS.py:62)")
         return L.log1p_degree()
     X0 = torch.as_tensor(X0)
     if X0.dim() == 1:
@@ -65,11 +242,13 @@ def heat_coefficients(k: int, s: float) -> list:
 
 
 def chebyshev_polynomials(L, k: int, X0) -> list:
-    """``[T_0, ..., T_k]`` with ``T_0 = X0``, ``T_1 = L_hat X0``,
-    ``T_i = 2 L_hat T_{i-1} - T_{i-2}`` (WATS.py:29-37); float32 device tensors
-    in the caller's row order.  ``L`` is the rescaled operator (what the
-    reference passes at WATS.py:62), or anything :func:`as_laplacian` accepts."""
-    L = as_laplacian(L)
+    """``[T_0, ..., T_k]`` with ``T_0 = X0``, ``T_1 = L X0``,
+    ``T_i = 2 L T_{i-1} - T_{i-2}`` (WATS.py:29-37); float32 device tensors
+    in the caller's row order.  ``L`` is applied as given (see
+    :func:`as_operator`): the reference's ``L_rescaled = (2/2.0) *
+    compute_normalized_laplacian(adj) - identity(N)`` (WATS.py:55,62) runs on
+    the device L_hat handle; an explicit matrix runs as a literal CSR."""
+    L = as_operator(L)
     X0 = _signal(L, X0)
     T = [X0]
     if k <= 0:

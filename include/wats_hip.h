@@ -123,6 +123,17 @@ int wg_laplacian_get_info(wg_laplacian_t L, wg_laplacian_info* info_host);
 int wg_laplacian_export(wg_laplacian_t L, int64_t* indptr, int32_t* indices,
                         float* values, uint8_t* iso, void* stream);
 
+/* A literal CSR operator for chebyshev_polynomials(L, k, X0)
+ * (calibration/WATS.py:29-37) called with an explicit matrix -- the reference
+ * passes `L_rescaled = (2/2.0)*L - identity(N)`, a float64 scipy CSR
+ * (WATS.py:55,62).  Every stored entry is kept with its value (float32),
+ * diagonal entries included; nothing is normalised and no row is isolated.
+ * Square n x n; the handle is a wg_laplacian_t of the same step kernel
+ * (wg_cheb_step / wg_permute_rows; freed by wg_laplacian_destroy).
+ * Synchronous. */
+int wg_operator_create(int64_t n, int64_t nnz, const int64_t* indptr, const int32_t* indices,
+                       const float* values, uint32_t flags, void* stream, wg_laplacian_t* out);
+
 /* -------------------------------------------------------------------------
  * a3: input signal.  Replaces `X0 = log1p(adj.sum(axis=1))`
  * (calibration/WATS.py:58-59): row sums INCLUDING self loops, float32 (N,1),

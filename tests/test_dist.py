@@ -338,3 +338,73 @@ def test_gather_rows_cpu_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+@pytest.mark.gpu
+def test_native_chain_recaptures_after_tune():
+    """the captured hipGraph must not outlive wg_laplacian_tune
+    (which frees the plans its kernels point at and changes launch knobs).
+    Three calls (eager, captured, replayed), a plan-shaping tune, then more
+    calls: every result equals the oracle."""
+    from wats_hip.dist import ShardedWavelet
+    g = _native_graph("rmat")
+    sw = ShardedWavelet(g.indptr, g.indices, g.values, g.n, np.array([0, g.n]), exchange="rccl", device="cuda:0")
+    X = torch.from_numpy(np.random.default_rng(6).standard_normal((g.n, 8)).astype(np.float32)).cuda()
+    ref = O.graph_wavelet_features(g.to_scipy(), k=6, s=0.8, X0=X.cpu().numpy(), return_all=True)
+    for _ in range(3):
+        H, S = sw.wavelet_features(X, k=6, s=0.8)
+    assert_parity(S.cpu().numpy(), ref["S"], what="before tune")
+    for knobs in ({"iter": 3, "block_iter": 2, "chunk_iter": 2}, {"clenshaw": 0}, {"waves": 8}):
+        sw.L.tune(**knobs)
+        for _ in range(3):
+            H, S = sw.wavelet_features(X, k=6, s=0.8)
+            assert_parity(S.cpu().numpy(), ref["S"], what=f"after tune {knobs}")
+    sw.close()
+
+
+def _empty_shard_worker(rank, world, port, bounds, F, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "efficient-gnn_amd"))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from wats_hip.dist import ShardedWavelet
+        g = _graph("rmat")
+        r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+        lo, hi = g.indptr[r0], g.indptr[r1]
+        sw = ShardedWavelet(g.indptr[r0:r1 + 1] - lo, g.indices[lo:hi], None, g.n, np.asarray(bounds),
+                            exchange="ipc", device="cuda:0", max_features=F)
+        X = np.random.default_rng(0).standard_normal((g.n, F)).astype(np.float32)
+        outs = [sw.wavelet_features(torch.from_numpy(X[r0:r1]), k=5, s=0.8) for _ in range(3)]
+        sw.check_exchange()
+        sw.close()
+        q.put((rank, outs[0][1].cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F", [1, 4])
+def test_ipc_chain_with_an_empty_shard(F):
+    """a rank that owns no rows runs the native chain too (it must
+    take part in every exchange phase); before, it took the Python path and
+    its peers hung.  Bounds [0, 600, 600, 1100, n]: rank 1 is empty."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = _graph("rmat")
+    bounds = [0, 600, 600, 1100, g.n]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_shard_worker, args=(r, 4, port, bounds, F, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(4)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1][1].shape == (0, F)
+    X = np.random.default_rng(0).standard_normal((g.n, F)).astype(np.float32)
+    ref = O.graph_wavelet_features(g.to_scipy(), k=5, s=0.8, X0=X, return_all=True)
+    assert_parity(np.concatenate([r[1] for r in res]), ref["S"], what=f"empty shard F={F}")

@@ -184,3 +184,43 @@ def test_c_abi_header_is_plain_c_and_links(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.startswith("ok")
+
+
+def test_compute_normalized_laplacian_reference_arithmetic_cpu():
+    """compute_normalized_laplacian returns L_sym (calibration/WATS.py:24-27);
+    the reference's own rescale `(2 / 2.0) * L - identity(N)` (WATS.py:55)
+    works on it and selects the fused L_hat operator.  Pure host arithmetic:
+    nothing touches the GPU until the operator is applied."""
+    from scipy.sparse import diags, identity
+    g = random_graph(30, 0.2, seed=1)
+    A = g.to_scipy()
+    N = A.shape[0]
+    L = wats_hip.compute_normalized_laplacian(A)
+    assert L.shape == (N, N) and (L.scale, L.shift) == (1.0, 0.0)
+    R = (2 / 2.0) * L - identity(N)
+    assert isinstance(R, wats_hip.SymNormalizedLaplacian) and R.is_rescaled
+    assert R._base is L._base                      # one device handle shared by every expression
+    h = 0.5 * L - 2 * identity(N)
+    assert (h.scale, h.shift) == (0.5, 2.0) and not h.is_rescaled
+    assert ((L - identity(N)) * 2.0).shift == 2.0
+    assert (L + identity(N)).shift == -1.0
+    with pytest.raises(NotImplementedError):
+        L - diags(np.arange(N, dtype=np.float64))  # not a multiple of identity
+    with pytest.raises(NotImplementedError):
+        L - A
+
+
+def test_partition_rows_never_empty_when_rows_suffice():
+    """A hub-heavy graph (star) used to leave empty shards; every shard now
+    gets >= 1 row when n >= world (an empty shard took the Python
+    path and hung its peers)."""
+    from wats_hip.dist import partition_rows
+    n = 2000
+    src = np.zeros(n - 1, np.int64)
+    dst = np.arange(1, n)
+    g = coo_to_csr(n, np.r_[src, dst], np.r_[dst, src])
+    for world in (2, 4, 8, 16):
+        b = partition_rows(g.indptr, world)
+        assert b[0] == 0 and b[-1] == n and np.all(np.diff(b) >= 1), (world, b)
+    b = partition_rows(np.array([0, 5, 7]), 4)      # fewer rows than ranks: empty shards are unavoidable
+    assert b[0] == 0 and b[-1] == 2 and np.all(np.diff(b) >= 0)

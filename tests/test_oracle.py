@@ -84,3 +84,39 @@ def test_heat_coefficients():
     a = O.heat_coefficients(4, 0.8)
     assert a[0] == 1.0
     np.testing.assert_allclose(a, np.exp(-0.8 * np.arange(5)), rtol=0)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_c_oracle_matches_reference_golden(name):
+    """The C restatement (oracle/wats_chain.c, the checker for the Reddit / 8M
+    sizes) reproduces the reference's golden S and H -- the same float64 row
+    sums in the same order as scipy's sparsetools, so bit for bit on S."""
+    from oracle import wats_oracle_c as C
+    d = load_golden(name)
+    A = golden_csr(d)
+    A.sort_indices()
+    k, s = int(d["k"]), float(d["s"])
+    X0 = d["X0"].astype(np.float32)
+    S, H = C.graph_wavelet_features(A.indptr, A.indices, A.data, X0, k, s, threads=3)
+    np.testing.assert_array_equal(S, d["S"])
+    np.testing.assert_allclose(H, d["H"], rtol=1e-14, atol=1e-300)
+
+
+def test_c_oracle_matches_python_oracle_random_graphs():
+    """Wider inputs than the fixtures (unweighted R-MAT F=5 K=16; weighted
+    directed graph with self loops and isolated nodes): equal to the numpy
+    restatement bit for bit on S, for 1 and 4 threads."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "efficient-gnn_amd"))
+    from oracle import wats_oracle_c as C
+    from wats_hip.graphgen import random_graph, rmat_graph
+    for g, F, k in ((rmat_graph(3000, 40000, seed=3), 5, 16),
+                    (random_graph(500, 0.02, seed=4, directed=True, weighted=True, self_loop_frac=0.1,
+                                  isolated_frac=0.05), 3, 7)):
+        A = g.to_scipy()
+        X0 = np.random.default_rng(0).standard_normal((g.n, F)).astype(np.float32)
+        ref = O.graph_wavelet_features(A, k=k, s=0.8, X0=X0, return_all=True)
+        for th in (1, 4):
+            S, H = C.graph_wavelet_features(g.indptr, g.indices, g.values, X0, k, 0.8, threads=th)
+            np.testing.assert_array_equal(S, ref["S"])
+            np.testing.assert_allclose(H, ref["H"], rtol=1e-14, atol=1e-300)
