@@ -9,17 +9,19 @@ an unweighted graph), the last one writing S / H in caller order.  The Laplacian
 prologue (a1-a3) is built once before timing, as the reference builds it once
 per WATS construction.
 
-Default workload (BASELINE.json configs[2], the one the metric is quoted on):
-ogbn-arxiv-size synthetic R-MAT graph (N=169,343, nnz~2.32M symmetrised), K=16,
-F=40 random-normal signal columns, s=0.8.
-
+Headline workload by GPU count (BASELINE.json configs):
+  N = 1  configs[2], the one the metric is quoted on: ogbn-arxiv-size synthetic
+         R-MAT graph (N=169,343, nnz~2.32M symmetrised), K=16, F=40
+         random-normal signal columns, s=0.8.
+  N > 1  configs[3]: the Reddit-size graph (232,965 nodes / 114.6M nonzeros),
+         K=16, F=41 (the 41-class logit-shaped RHS of SURVEY 8(d)), ONE graph
+         row-sharded over the N ranks (nnz-balanced row blocks, [own | halo]
+         columns) with a halo exchange per Chebyshev step (RCCL grouped
+         send/recv by default) -- strong scaling.  The same Reddit run at one
+         rank is the N = 1 line's `sharded` object, so the Reddit curve is
+         complete across the driver's 1/2/4/8 lines.
 value = total edges*K processed by all ranks / max-over-ranks wall time, where
 edges = nnz of the off-diagonal L_hat (= symmetrised adjacency without loops).
-Multi-GPU (torchrun, one process per GPU): each rank runs its own
-independently generated graph of the same size -- weak scaling over
-independent graphs, no data-path collective.  `--mode sharded` instead splits
-ONE graph (e.g. --config reddit / rmat-8m) into row blocks over the ranks with a
-per-step RCCL halo exchange (strong scaling), see DESIGN.md section 7.
 
 Also printed in the same JSON line:
   roofline      -- SURVEY.md 8(d)'s algorithmic bytes per launch (B_step =
@@ -28,7 +30,11 @@ Also printed in the same JSON line:
                    every step launch; kernel_bytes_frac: the fewer bytes the
                    kernel's own algorithm needs (clenshaw_bytes);
   cpu_baseline  -- the oracle (scipy/numpy restatement of the reference, one
-                   thread) on the same graph, rank 0 at N=1 only.
+                   thread) on the same graph, rank 0 at N=1 only; its `check`
+                   compares the benchmarked pass's S (all columns) with the C
+                   restatement of the oracle (oracle/wats_chain.c);
+  sharded runs  -- `check`: every rank's rows of S for a random signal against
+                   the unsharded chain on the same GPU (max over ranks).
 """
 from __future__ import annotations
 
@@ -47,6 +53,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+CHECK_TOL = 1e-5       # north_star: <= 1e-5 relative (max|dS| / max|S| per column)
 
 
 def parse():
@@ -56,7 +63,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--settle-s", type=float, default=0.5,
                     help="seconds of untimed passes after the W warmup passes (clock ramp); reported as settle_s")
-    ap.add_argument("--config", default="ogbn-arxiv")
+    ap.add_argument("--config", default="ogbn-arxiv", help="the N = 1 headline workload")
+    ap.add_argument("--scale-config", default="reddit-f41",
+                    help="the N > 1 headline: this config row-sharded over all ranks (strong scaling)")
     ap.add_argument("--K", type=int, default=None)
     ap.add_argument("--F", type=int, default=None)
     ap.add_argument("--s", type=float, default=0.8)
@@ -68,23 +77,29 @@ def parse():
                          "'auto': the committed PMC summary of the default workload (profiles/r01/s56_traffic.json, "
                          "tools/gpu_session.sh RUN_PMC=1) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    ap.add_argument("--sharded-extra", default="reddit,rmat-8m",
-                    help="comma-separated configs also measured row-sharded over all ranks (RCCL halo exchange), "
-                         "attached as 'sharded' (first) and 'sharded_<config>' objects of the line; 'none' to skip")
+    ap.add_argument("--sharded-extra", default="reddit-f41,reddit,rmat-8m",
+                    help="comma-separated configs also measured row-sharded over all ranks (halo exchange), attached "
+                         "as 'sharded' (first) and 'sharded_<config>' objects of the line; 'none' to skip.  At N > 1 "
+                         "the --scale-config run is the headline and is not repeated here")
     ap.add_argument("--sharded-steps", type=int, default=5)
-    ap.add_argument("--sharded-timeout", type=float, default=360.0,
-                    help="seconds the sharded extra may take before the line is printed without it")
-    ap.add_argument("--exchange", default="ipc,rccl",
-                    help="comma-separated sharded halo exchanges: native chain with the one-sided IPC pull (ipc) or "
-                         "grouped ncclSend/ncclRecv (rccl), or torch all_to_all_single per step (nccl); the sharded "
-                         "extras run once per exchange (--mode sharded: the first one)")
+    ap.add_argument("--sharded-timeout", type=float, default=420.0,
+                    help="seconds the extras may take before the line is printed without the unfinished ones")
+    ap.add_argument("--exchange", default="rccl,ipc",
+                    help="comma-separated sharded halo exchanges: native chain with grouped ncclSend/ncclRecv "
+                         "(rccl) or the one-sided IPC pull (ipc), or torch all_to_all_single per step (nccl); the "
+                         "first is the headline's (N > 1) and the extras'; the others are timed for the first "
+                         "sharded config only, as 'sharded_<config>_<exchange>'")
     ap.add_argument("--cold-reps", type=int, default=5,
                     help="chains timed after writing a 512 MiB scratch buffer (cold Infinity Cache / L2); 0 = skip")
     ap.add_argument("--f1-companion", type=int, default=1,
                     help="also time the same graph with the F=1 log1p-degree signal (SURVEY 8(d) 'also report F=1')")
-    ap.add_argument("--mode", default="graphs", choices=["graphs", "sharded"],
-                    help="graphs: one independent graph per rank (default); sharded: one graph row-sharded over all "
-                         "ranks with a per-step RCCL halo exchange")
+    ap.add_argument("--connected-companion", type=int, default=1,
+                    help="N = 1: also time an arxiv-shaped graph without isolated rows (graphgen.connect_isolated)")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="N > 1: also time one independent arxiv-size graph per rank (no collective) as 'replicas'")
+    ap.add_argument("--mode", default="auto", choices=["auto", "graphs", "sharded"],
+                    help="auto: graphs at N = 1, sharded (--scale-config) at N > 1; graphs: one independent graph "
+                         "per rank; sharded: --config row-sharded over all ranks")
     return ap.parse_args()
 
 
@@ -138,8 +153,14 @@ def lds_algorithmic_bytes(info: dict) -> int:
     return 2 * nnz + 4 * (nb * n + 1) + (8 * nb * n if nb > 1 else 0) + 33 * n + 4 * cols
 
 
-def cpu_baseline(g, K, F, s, X, seconds):
+def cpu_baseline(g, K, F, s, X, seconds, S_gpu):
+    """The reference's CPU path, restated (oracle/wats_oracle.py: scipy
+    csgraph.laplacian + single-threaded sparsetools CSR mat-vecs, as
+    WATS.py:53-72 runs), timed on a bounded sample of passes; then the parity
+    check of the benchmarked pass: S_gpu (all columns) against the C
+    restatement of the oracle (oracle/wats_chain.c, 16 threads)."""
     from oracle import wats_oracle as O
+    from oracle import wats_oracle_c as C
     A = g.to_scipy()
     L_hat = O.rescaled_laplacian(A)  # prologue, untimed (as on the GPU)
     nnz = int(L_hat.nnz - np.count_nonzero(L_hat.diagonal()))
@@ -152,18 +173,37 @@ def cpu_baseline(g, K, F, s, X, seconds):
         t_total += time.perf_counter() - t0
         reps += 1
         del T, S
-    return dict(value=nnz * K * reps / t_total, unit="edges*K/s", cores=1, kind="port",
-                sample=f"{reps} full graph_wavelet_features passes (chain + heat sum + L1 norm, prologue excluded) "
-                       f"of the same graph/signal, scipy {__import__('scipy').__version__} single-threaded CSR "
-                       f"matvecs, {t_total:.1f} s")
+    out = dict(value=nnz * K * reps / t_total, unit="edges*K/s", cores=1, kind="port",
+               sample=f"{reps} full graph_wavelet_features passes (chain + heat sum + L1 norm, prologue excluded) "
+                      f"of the same graph/signal, scipy {__import__('scipy').__version__} single-threaded CSR "
+                      f"matvecs, {t_total:.1f} s")
+    t0 = time.perf_counter()
+    S_ref, _ = C.graph_wavelet_features(g.indptr, g.indices, g.values, X, K, s, threads=16, return_H=False)
+    err = _rel_err(S_gpu, S_ref)
+    out["check"] = {"max_rel_err": err, "tol": CHECK_TOL, "ok": bool(err <= CHECK_TOL),
+                    "what": f"the benchmarked pass's S (all {F} columns, this signal) vs the C restatement of the "
+                            f"oracle (oracle/wats_chain.c, float64, {time.perf_counter() - t0:.1f} s on 16 threads); "
+                            f"max over columns of max|dS| / max|S|"}
+    return out
 
 
-def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl"):
+def _rel_err(got, ref) -> float:
+    got = np.asarray(got, np.float64).reshape(ref.shape)
+    scale = np.abs(ref).max(axis=0)
+    err = np.abs(got - ref).max(axis=0)
+    ok = scale > 0
+    return float((err[ok] / scale[ok]).max()) if ok.any() else float(err.max(initial=0.0))
+
+
+# ----------------------------------------------------------------------------- row-sharded runs
+def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl",
+                median_reps: int = 0, check: bool = True):
     """One graph (generated identically on every rank, on the GPU) split into
     nnz-balanced row blocks; per Chebyshev step one halo exchange (`exchange`:
-    IPC pull or RCCL send/recv in the native chain, or torch all_to_all_single)
-    + the step kernel.  Strong scaling (fixed graph).
+    RCCL send/recv or IPC pull in the native chain, or torch
+    all_to_all_single) + the step kernel.  Strong scaling (fixed graph).
     Returns the result dict (meaningful on rank 0)."""
+    from wats_hip import NormalizedLaplacian, graph_wavelet_features
     from wats_hip.dist import ShardedWavelet, partition_rows
     from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
 
@@ -179,7 +219,8 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     lo, hi = int(indptr[r0]), int(indptr[r1])
     cols = indices_d[lo:hi].cpu().numpy()
     nnz_global = int(indptr[-1])
-    del indptr_d, indices_d
+    if not check:
+        del indptr_d, indices_d
     torch.cuda.empty_cache()
     with _stdout_to_stderr():   # RCCL prints its version banner at communicator init: keep stdout one JSON line
         sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device,
@@ -197,7 +238,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     for i in range(max(2, warmup)):   # the native chain is captured into a hipGraph on its 2nd call
         run()
         torch.cuda.synchronize(device)
-        _log(f"sharded {config} ({exchange}): warmup call {i + 1} done")
+    _log(f"sharded {config} ({exchange}): warm")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -208,12 +249,30 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    _log(f"sharded {config} ({exchange}): timed {steps} chains in {elapsed:.3f} s; profiling pass")
+    _log(f"sharded {config} ({exchange}): timed {steps} chains in {elapsed:.3f} s")
+    med = None
+    if median_reps > 0:   # per-chain times (HIP events on the launch stream), median over ranks' max
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(median_reps + 1)]
+        if world > 1:
+            dist.barrier()
+        evs[0].record()
+        for i in range(median_reps):
+            run()
+            evs[i + 1].record()
+        torch.cuda.synchronize(device)
+        per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(median_reps))
+        med = per[len(per) // 2]
+        if world > 1:
+            med = _allreduce(med, dist.ReduceOp.MAX, device)
     # kernel / exchange attribution: one more pass, eager, with HIP events (outside the timed region)
     sw.profile_start()
     run()
     prof = sw.profile_collect()
-    kat = _eigen_kat_sharded(sw, indptr, r0, r1, F, K, s_heat, world, device)
+    chk = None
+    if check:
+        chk = _check_vs_unsharded(sw, indptr_d, indices_d, n_t, r0, r1, F, K, s_heat, world, device,
+                                  NormalizedLaplacian, graph_wavelet_features)
+        del indptr_d, indices_d
     if world > 1:
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
     nnz_lhat = _allreduce(float(sw.L.nnz), dist.ReduceOp.SUM, device) if world > 1 else float(sw.L.nnz)
@@ -223,6 +282,9 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
     kernel = lds_kernel_name(lds_info) + " (rank 0 shard)"
     avg_ms = prof["step_ms"]
+    sw.close()
+    del sw
+    torch.cuda.empty_cache()
     return {
         "metric": f"Chebyshev SpMM-chain edges*K/s ({config}-size, K={K}, row-sharded)",
         "value": nnz_lhat * K * steps / elapsed,
@@ -231,6 +293,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         "steps": steps,
         "warmup": warmup,
         "ms_per_step": elapsed / steps * 1e3,
+        "median_step_ms": med,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -254,11 +317,36 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                      "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
                      "nominal_8d_bytes": b_8d,
-                     "eigen_kat": kat,
                      "nominal_8d_frac": (b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None},
+        "check": chk,
     }
 
 
+def _check_vs_unsharded(sw, indptr_d, indices_d, n, r0, r1, F, K, s_heat, world, device, NormalizedLaplacian,
+                        graph_wavelet_features) -> dict:
+    """Column-sensitive check of the sharded chain: a random signal (same on
+    every rank, seeded), the sharded S on this rank's rows against the
+    unsharded chain of the whole graph on this rank's GPU (the product path
+    twice: every halo row and gathered column must be right); max over ranks."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(12345)
+    X = torch.randn(n, F, generator=gen, device=device)
+    _, S_sh = sw.wavelet_features(X[r0:r1].contiguous(), k=K, s=s_heat)
+    L = NormalizedLaplacian(n, indptr_d, indices_d, device=device)
+    _, S_full = graph_wavelet_features(L, k=K, s=s_heat, X0=X, return_S=True)
+    L.close()
+    ref = S_full[r0:r1].double()
+    err = (S_sh.double() - ref).abs().amax(dim=0) if r1 > r0 else torch.zeros(F, dtype=torch.float64, device=device)
+    scale = S_full.double().abs().amax(dim=0)
+    rel = float((err / scale.clamp_min(1e-300)).max())
+    if world > 1:
+        rel = _allreduce(rel, dist.ReduceOp.MAX, device)
+    return {"max_rel_err": rel, "tol": CHECK_TOL, "ok": bool(rel <= CHECK_TOL),
+            "what": "random signal (all F columns): every rank's rows of the sharded S vs the unsharded chain on "
+                    "the same GPU; max over ranks and columns of max|dS| / max|S|"}
+
+
+# ----------------------------------------------------------------------------- single-GPU measurement
 def cold_chains(step, L, reps, device):
     """SURVEY.md 8(d) 'cold' protocol: before each timed pass, write a 512 MiB
     scratch buffer (evicts the 256 MiB Infinity Cache and every L2), then time
@@ -329,77 +417,11 @@ def f1_companion(lib, L, K, s_heat, steps, device, unit=False):
             "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
-def _kat_signal(deg: np.ndarray, F: int) -> np.ndarray:
-    """Columns that are multiples of v = sqrt(w): for a symmetric graph without
-    self loops w = degree, and L_hat v = -v (eigenvector
-    KAT), so T_k = (-1)^k X0 and S = X0 * sum_k (-1)^k exp(-s k) exactly."""
-    v = np.sqrt(deg.astype(np.float64))
-    return (v[:, None] * (1.0 + 0.125 * np.arange(F))[None, :]).astype(np.float32)
-
-
-def _kat_coef(K: int, s_heat: float) -> float:
-    return float(sum(((-1.0) ** i) * np.exp(-s_heat * i) for i in range(K + 1)))
-
-
-def _eigen_kat_sharded(sw, indptr, r0, r1, F, K, s_heat, world, device) -> dict:
-    """Full-size parity check of the sharded chain (no oracle can run at this
-    size): the eigenvector KAT on every rank's rows, max error over ranks."""
-    X = torch.from_numpy(_kat_signal(np.diff(indptr)[r0:r1], F)).to(device)
-    _, S = sw.wavelet_features(X, k=K, s=s_heat)
-    expect = X.double() * _kat_coef(K, s_heat)
-    err = float((S.double() - expect).abs().max()) if S.numel() else 0.0
-    scale = float(expect.abs().max()) if S.numel() else 0.0
-    if world > 1:
-        err = _allreduce(err, dist.ReduceOp.MAX, device)
-        scale = _allreduce(scale, dist.ReduceOp.MAX, device)
-    rel = err / scale if scale else 0.0
-    return {"max_rel_err": rel, "tol": 1e-5, "ok": rel <= 1e-5,
-            "what": "X0 = sqrt(degree) x column scales; S must equal X0 * sum_k (-1)^k e^{-sk} (every rank, max)"}
-
-
-def sharded_main(args, world, rank, device):
-    line = run_sharded(args.config, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
-                       args.exchange.split(",")[0])
-    if rank == 0:
-        js = json.dumps(line)
-        print(js, flush=True)
-        if args.out:
-            with open(args.out, "w") as f:
-                f.write(js + "\n")
-
-
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # WATS_BENCH_DEVICE pins every rank to one device (multi-rank tests on a 1-GPU box)
-    dev_idx = int(os.environ.get("WATS_BENCH_DEVICE", local_rank if world > 1 else 0))
-    device = torch.device("cuda", dev_idx)
-    torch.cuda.set_device(device)
-    if world > 1:
-        # WATS_BENCH_PG=gloo: rehearse several ranks on one GPU (RCCL refuses two
-        # ranks per device); with the IPC exchange the sharded path needs no RCCL
-        backend = os.environ.get("WATS_BENCH_PG", "nccl")
-        with _stdout_to_stderr():
-            if backend == "nccl":
-                dist.init_process_group("nccl", device_id=device)
-            else:
-                dist.init_process_group(backend)
-            dist.barrier()
-    if args.mode == "sharded":
-        sharded_main(args, world, rank, device)
-        if world > 1:
-            dist.destroy_process_group()
-        return
-
+def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
+    """One graph per rank (no collective): graph_wavelet_features passes timed
+    as the driver's contract says.  full=False: value / step / roofline only
+    (companion lines)."""
     import wats_hip
-    from wats_hip.graphgen import NAMED_CONFIGS, named_graph
-
-    n_target, nnz_target, K_def, F_def = NAMED_CONFIGS[args.config]
-    K = args.K if args.K is not None else K_def
-    F = args.F if args.F is not None else F_def
-    g = named_graph(args.config, seed=args.seed + rank)   # independent graph per rank
     st = g.stats()
     unit = g.values is None or bool(np.all(g.values == 1))   # the value-free Clenshaw chain applies
     L = wats_hip.NormalizedLaplacian.from_graph(g, device=device)
@@ -460,157 +482,236 @@ def main():
     # gap each, 10 % of an arxiv F=40 pass); roofline and the per-pass median:
     # the same K passes again, with events around every step launch and pass
     elapsed, _, _ = timed(False)
+    S_host = S.cpu().numpy() if (full and world == 1) else None   # the benchmarked pass's S (parity check)
     elapsed_prof, prof, median_ms = timed(True)
-    _log(f"main: timed {args.steps} passes in {elapsed:.3f} s; cold / F=1 companion")
-    cold = cold_chains(step, L, args.cold_reps, device) if args.cold_reps > 0 else None
-    # full-size parity check of the benchmarked pass (eigenvector KAT, all F columns)
-    Xk = torch.from_numpy(_kat_signal(np.diff(g.indptr), F)).to(device)
-    wats_hip._lib.check(lib.wg_wavelet_features(L.handle, Xk.data_ptr(), F, K, args.s, S.data_ptr(), H.data_ptr(),
-                                                stream), "wavelet_features")
-    expect = Xk.double() * _kat_coef(K, args.s)
-    kat_rel = float((S.double() - expect).abs().max() / expect.abs().max())
-    del Xk, expect
-    f1 = None
-    if args.f1_companion and F > 1:
-        f1 = f1_companion(lib, L, K, args.s, args.steps, device, unit)
+    _log(f"{config}: timed {args.steps} passes in {elapsed:.3f} s")
+    cold = cold_chains(step, L, args.cold_reps, device) if (full and args.cold_reps > 0) else None
+    f1 = f1_companion(lib, L, K, args.s, args.steps, device, unit) if (full and args.f1_companion and F > 1) else None
     edges_k = float(nnz) * K * args.steps
     if world > 1:
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
         edges_k = _allreduce(edges_k, dist.ReduceOp.SUM, device)
+    avg_ms = prof["sum_ms"] / max(1, prof["launches"])
+    # the step kernel processes the rows that enter the chain; purely
+    # isolated rows (closed form T_k = (-1)^k X0) are handled by finalize
+    n_active = n - int(L.info["n_closed_form"])
+    b_8d = algorithmic_bytes(n_active, nnz, F)
+    lds_info = L.lds_plan_info(active_only=True) if F == 1 else None
+    b_step = lds_algorithmic_bytes(lds_info) if lds_info else clenshaw_bytes(n_active, nnz, F, unit)
+    # roofline.achieved: SURVEY 8(d)'s per-row / per-nonzero figure x the rows and nonzeros one launch
+    # processes (the contract); the bytes this kernel's own algorithm needs are reported beside it.
+    # (F == 1 LDS formats: their own model -- SURVEY's 8 B/nnz would read above 1.0)
+    b_roof = b_step if lds_info else b_8d
+    achieved = b_roof / (avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = None, None
+    tj = args.traffic_json
+    if tj == "auto":
+        tj = os.path.join(REPO, "profiles", "r01", "s56_traffic.json") \
+            if (config == "ogbn-arxiv" and F == 40 and K == 16) else None
+    if tj and tj != "none" and os.path.exists(tj):
+        traffic = json.load(open(tj)).get("bytes_per_launch")
+        traffic_src = os.path.relpath(tj, REPO) if os.path.isabs(tj) else tj
+    line = {
+        "metric": f"Chebyshev SpMM-chain edges*K/s ({config}-size, K={K}) + %HBM roofline",
+        "value": edges_k / elapsed,
+        "unit": "edges*K/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "settle_s": args.settle_s,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{config}-size R-MAT graph (a=.57,b=c=.19), symmetrised, no self loops; "
+                        f"graph_wavelet_features K={K}, F={F} "
+                        f"{'log1p-degree signal' if F == 1 else 'randn signal columns'}, s={args.s}",
+            "N": n, "nnz": nnz, "isolated": st["isolated"], "max_degree": st["max_degree"],
+            "K": K, "F": F, "per_rank": "one graph per rank, no collective",
+            "parallelism": f"graphs x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "traffic_source": (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction: "
+                               f"an upper bound) + WRITE_SIZE per launch of this kernel on this workload"
+                               if traffic is not None else None),
+            "kernel": lds_kernel_name(lds_info),
+            "byte_model": _byte_model(lds_info) if lds_info else
+                          "SURVEY 8(d): 8 B/nnz + 4(N+1) + 20 N F over the launched rows",
+            "algorithmic_bytes_per_launch": b_roof,
+            "kernel_byte_model": _byte_model(lds_info) if lds_info else
+                                 ("Clenshaw heat sum on u = b dinv (DESIGN.md 4.1): 4 B/nnz + 4(N+1) + 16 N F + 8 N"
+                                  if unit else "Clenshaw heat sum (DESIGN.md 4.1): 8 B/nnz + 4(N+1) + 16 N F"),
+            "kernel_bytes_per_launch": b_step,
+            "kernel_bytes_frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "rows_per_launch": n_active,
+            "closed_form_rows": n - n_active,
+            "algorithmic_bytes_all_rows": algorithmic_bytes(n, nnz, F),
+            "all_rows_frac": algorithmic_bytes(n, nnz, F) / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frac_note": "frac: SURVEY 8(d)'s B_step over the rows each launch processes (purely isolated "
+                         "rows are closed-form and never launched); kernel_bytes_frac: the bytes this "
+                         "kernel's algorithm needs (Clenshaw: no S stream; unweighted: no CSR values); "
+                         "all_rows_frac: SURVEY 8(d)'s B_step with N = all nodes",
+            "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "avg_launch_us": avg_ms * 1e3,
+            "max_launch_us": prof["max_ms"] * 1e3,
+            "launches": prof["launches"],
+        },
+        "chain_ms": prof["sum_ms"] / args.steps,
+        "median_step_ms_profiled": median_ms,
+        "value_median": float(nnz) * K / (median_ms * 1e-3) * world if median_ms else None,
+        "ms_per_step_profiled": elapsed_prof / args.steps * 1e3,
+        "timing": "value / ms_per_step: K passes without per-launch events; roofline and median: the same K "
+                  "passes timed right after with HIP events around every step-kernel launch and every pass "
+                  "(ms_per_step_profiled, median_step_ms_profiled; value_median = nnz*K / that median)",
+        "edges_K_F_per_s": edges_k * F / elapsed,
+    }
+    if cold is not None:
+        cold["edges_K_per_s"] = float(nnz) * K / (cold["step_ms"] * 1e-3)
+        cold["achieved_GBs"] = b_roof / (cold["avg_launch_us"] * 1e-6) / 1e9
+        cold["frac"] = cold["achieved_GBs"] / HBM_PEAK_GBS
+        line["cold"] = cold
+    if f1 is not None:
+        line["f1_companion"] = f1
+    if full and world == 1 and not args.no_cpu_baseline:
+        if X_host is None:
+            X_host = L.log1p_degree().cpu().numpy()
+        line["cpu_baseline"] = cpu_baseline(g, K, F, args.s, X_host, args.cpu_seconds, S_host)
+        line["cpu_baseline"]["host_cpu"] = _cpu_model()
+    L.close()
+    del S, H, X
+    torch.cuda.empty_cache()
+    return line
+
+
+def _companion_summary(d: dict) -> dict:
+    """The fields of a companion line worth keeping in the main line."""
+    keep = ("metric", "value", "ms_per_step", "value_median", "median_step_ms_profiled", "config")
+    out = {k: d[k] for k in keep if k in d}
+    r = d.get("roofline", {})
+    out["roofline"] = {k: r.get(k) for k in ("achieved", "frac", "kernel_bytes_frac", "all_rows_frac",
+                                             "avg_launch_us", "rows_per_launch", "closed_form_rows")}
+    return out
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # WATS_BENCH_DEVICE pins every rank to one device (multi-rank tests on a 1-GPU box)
+    dev_idx = int(os.environ.get("WATS_BENCH_DEVICE", local_rank if world > 1 else 0))
+    device = torch.device("cuda", dev_idx)
+    torch.cuda.set_device(device)
+    if world > 1:
+        # WATS_BENCH_PG=gloo: rehearse several ranks on one GPU (RCCL refuses two
+        # ranks per device); with the IPC exchange the sharded path needs no RCCL
+        backend = os.environ.get("WATS_BENCH_PG", "nccl")
+        with _stdout_to_stderr():
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group(backend)
+            dist.barrier()
+    mode = args.mode if args.mode != "auto" else ("graphs" if world == 1 else "sharded")
+    exchanges = [x for x in args.exchange.split(",") if x]
+    from wats_hip.graphgen import NAMED_CONFIGS, connect_isolated, named_graph
 
     line = None
-    if rank == 0:
-        avg_ms = prof["sum_ms"] / max(1, prof["launches"])
-        # the step kernel processes the rows that enter the chain; purely
-        # isolated rows (closed form T_k = (-1)^k X0) are handled by finalize
-        n_active = n - int(L.info["n_closed_form"])
-        b_8d = algorithmic_bytes(n_active, nnz, F)
-        lds_info = L.lds_plan_info(active_only=True) if F == 1 else None
-        b_step = lds_algorithmic_bytes(lds_info) if lds_info else clenshaw_bytes(n_active, nnz, F, unit)
-        # roofline.achieved: SURVEY 8(d)'s per-row / per-nonzero figure x the rows and nonzeros one launch
-        # processes (the contract); the bytes this kernel's own algorithm needs are reported beside it.
-        # (F == 1 LDS formats: their own model -- SURVEY's 8 B/nnz would read above 1.0)
-        b_roof = b_step if lds_info else b_8d
-        achieved = b_roof / (avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = None, None
-        tj = args.traffic_json
-        if tj == "auto":
-            tj = os.path.join(REPO, "profiles", "r01", "s56_traffic.json") \
-                if (args.config == "ogbn-arxiv" and F == 40 and K == 16) else None
-        if tj and tj != "none" and os.path.exists(tj):
-            traffic = json.load(open(tj)).get("bytes_per_launch")
-            traffic_src = os.path.relpath(tj, REPO) if os.path.isabs(tj) else tj
-        line = {
-            "metric": "Chebyshev SpMM-chain edges*K/s (ogbn-arxiv-size, K=16) + %HBM roofline",
-            "value": edges_k / elapsed,
-            "unit": "edges*K/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "settle_s": args.settle_s,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic",
-            "config": {
-                "workload": f"{args.config}-size R-MAT graph (a=.57,b=c=.19), symmetrised, no self loops; "
-                            f"graph_wavelet_features K={K}, F={F} "
-                            f"{'log1p-degree signal' if F == 1 else 'randn signal columns'}, s={args.s}",
-                "N": n, "nnz": nnz, "isolated": st["isolated"], "max_degree": st["max_degree"],
-                "K": K, "F": F, "per_rank": "independent graph per rank (weak scaling, no collective)",
-                "parallelism": f"graphs x{world}",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_source": (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction: "
-                                   f"an upper bound) + WRITE_SIZE per launch of this kernel on this workload"
-                                   if traffic is not None else None),
-                "kernel": lds_kernel_name(lds_info),
-                "byte_model": _byte_model(lds_info) if lds_info else
-                              "SURVEY 8(d): 8 B/nnz + 4(N+1) + 20 N F over the launched rows",
-                "algorithmic_bytes_per_launch": b_roof,
-                "kernel_byte_model": _byte_model(lds_info) if lds_info else
-                                     ("Clenshaw heat sum on u = b dinv (DESIGN.md 4.1): 4 B/nnz + 4(N+1) + 16 N F + 8 N"
-                                      if unit else "Clenshaw heat sum (DESIGN.md 4.1): 8 B/nnz + 4(N+1) + 16 N F"),
-                "kernel_bytes_per_launch": b_step,
-                "kernel_bytes_frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "rows_per_launch": n_active,
-                "closed_form_rows": n - n_active,
-                "algorithmic_bytes_all_rows": algorithmic_bytes(n, nnz, F),
-                "all_rows_frac": algorithmic_bytes(n, nnz, F) / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "frac_note": "frac: SURVEY 8(d)'s B_step over the rows each launch processes (purely isolated "
-                             "rows are closed-form and never launched); kernel_bytes_frac: the bytes this "
-                             "kernel's algorithm needs (Clenshaw: no S stream; unweighted: no CSR values); "
-                             "all_rows_frac: SURVEY 8(d)'s B_step with N = all nodes",
-                "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "avg_launch_us": avg_ms * 1e3,
-                "max_launch_us": prof["max_ms"] * 1e3,
-                "launches": prof["launches"],
-            },
-            "chain_ms": prof["sum_ms"] / args.steps,
-            "median_step_ms_profiled": median_ms,
-            "ms_per_step_profiled": elapsed_prof / args.steps * 1e3,
-            "timing": "value / ms_per_step: K passes without per-launch events; roofline: the same K passes "
-                      "timed right after with HIP events around every step-kernel launch (ms_per_step_profiled)",
-            "edges_K_F_per_s": edges_k * F / elapsed,
-            "eigen_kat": {"max_rel_err": kat_rel, "tol": 1e-5, "ok": kat_rel <= 1e-5,
-                          "what": "the benchmarked graph, K and F with X0 = sqrt(degree) x column scales: "
-                                  "S must equal X0 * sum_k (-1)^k e^{-sk}"},
-        }
-        if cold is not None:
-            cold["edges_K_per_s"] = float(nnz) * K / (cold["step_ms"] * 1e-3)
-            cold["achieved_GBs"] = b_roof / (cold["avg_launch_us"] * 1e-6) / 1e9
-            cold["frac"] = cold["achieved_GBs"] / HBM_PEAK_GBS
-            line["cold"] = cold
-        if f1 is not None:
-            line["f1_companion"] = f1
-        if world == 1 and not args.no_cpu_baseline:
-            if X_host is None:
-                X_host = L.log1p_degree().cpu().numpy()
-            line["cpu_baseline"] = cpu_baseline(g, K, F, args.s, X_host, args.cpu_seconds)
-            line["cpu_baseline"]["host_cpu"] = _cpu_model()
+    if mode == "sharded":
+        # the N > 1 headline: one graph row-sharded over every rank (strong scaling)
+        cfg = args.scale_config if args.mode == "auto" else args.config
+        line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
+                           exchanges[0], median_reps=max(20, args.steps))
+        line["metric"] = (f"Chebyshev SpMM-chain edges*K/s ({cfg}-size, K={line['config']['K']}, F="
+                          f"{line['config']['F']}, row-sharded over {world} GPUs)")
+        line["headline_note"] = ("N > 1 headline: BASELINE.json configs[3] (Reddit-size, 1-D row-sharded, RCCL "
+                                 "halo exchange); the N = 1 line carries the same run at one rank as `sharded`")
+    else:
+        n_target, nnz_target, K_def, F_def = NAMED_CONFIGS[args.config]
+        K = args.K if args.K is not None else K_def
+        F = args.F if args.F is not None else F_def
+        g = named_graph(args.config, seed=args.seed + rank)   # independent graph per rank
+        line = single_gpu_line(args, g, args.config, K, F, world, rank, device, full=True)
+        if world == 1 and args.connected_companion and args.config == "ogbn-arxiv":
+            a = argparse.Namespace(**vars(args))
+            a.cold_reps = 0
+            line["connected_companion"] = _companion_summary(
+                single_gpu_line(a, connect_isolated(g, seed=7), "ogbn-arxiv-connected", K, F, world, rank, device,
+                                full=False))
+            line["connected_companion"]["what"] = ("the same R-MAT graph with every isolated node attached to one "
+                                                   "random node (graphgen.connect_isolated): no closed-form rows, "
+                                                   "as the real ogbn-arxiv")
+        del g
 
     extras = [c for c in (args.sharded_extra or "none").split(",") if c and c != "none"]
+    if mode == "sharded":
+        extras = [c for c in extras if c != (args.scale_config if args.mode == "auto" else args.config)]
     results = {}
-    if extras:
-        # BASELINE configs 3-4: one big graph row-sharded over all ranks with the
-        # per-step halo exchange.  Measured after the main line is complete; a
-        # Python-level failure is reported in the line instead of losing it, and
-        # a watchdog prints the line and ends the process if a sharded run (a
-        # collective on several GPUs) does not finish in time.
+    watchdog = None
+    if extras or (mode == "sharded" and args.replicas):
+        # Measured after the headline is complete; a Python-level failure is reported in
+        # the line instead of losing it, and a watchdog prints the line and ends the
+        # process if a run (a collective on several GPUs) does not finish in time.
         import threading
 
         def _expire():
             if rank == 0:
                 results["timeout"] = {"error": f"timeout after {args.sharded_timeout:.0f} s; the runs not "
                                                 f"listed did not finish"}
-                _attach(line, results)
+                _attach(line, results, mode)
                 _emit(line, args.out)
             os._exit(0)
         watchdog = threading.Timer(args.sharded_timeout, _expire)
         watchdog.daemon = True
         watchdog.start()
-        del S, H
-        exchanges = [x for x in args.exchange.split(",") if x]
-        for c in extras:
-            for j, x in enumerate(exchanges):
-                key = c if j == 0 else f"{c}_{x}"
-                try:
-                    torch.cuda.empty_cache()
-                    results[key] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
-                                               device, x)
-                except Exception as exc:  # noqa: BLE001
-                    results[key] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
+    if mode == "sharded" and args.replicas:
+        try:
+            n_target, nnz_target, K_def, F_def = NAMED_CONFIGS[args.config]
+            g = named_graph(args.config, seed=args.seed + rank)
+            a = argparse.Namespace(**vars(args))
+            a.cold_reps = 0
+            results["replicas"] = _companion_summary(single_gpu_line(a, g, args.config, K_def, F_def, world, rank,
+                                                                     device, full=False))
+            results["replicas"]["what"] = ("one independent ogbn-arxiv-size graph per rank (weak scaling, no "
+                                           "collective): the round-1 N > 1 headline")
+            del g
+        except Exception as exc:  # noqa: BLE001
+            results["replicas"] = {"error": f"{type(exc).__name__}: {exc}"}
+    for i, c in enumerate(extras):
+        # N = 1: the first extra (the Reddit-size F=41 run the N > 1 headline scales) with every exchange
+        xs = exchanges if (mode != "sharded" and i == 0) else exchanges[:1]
+        for j, x in enumerate(xs):
+            key = c if j == 0 else f"{c}_{x}"
+            try:
+                torch.cuda.empty_cache()
+                results[key] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
+                                           device, x)
+            except Exception as exc:  # noqa: BLE001
+                results[key] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
+    if mode == "sharded" and len(exchanges) > 1:
+        # the headline config with the other exchanges (same line, for the exchange comparison)
+        cfg = args.scale_config if args.mode == "auto" else args.config
+        for x in exchanges[1:]:
+            try:
+                torch.cuda.empty_cache()
+                results[f"{cfg}_{x}"] = run_sharded(cfg, args.K, args.F, args.sharded_steps, 1, args.seed, args.s,
+                                                    world, rank, device, x)
+            except Exception as exc:  # noqa: BLE001
+                results[f"{cfg}_{x}"] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
+    if watchdog is not None:
         watchdog.cancel()
     if rank == 0:
-        _attach(line, results)
+        _attach(line, results, mode)
         _emit(line, args.out)
     if world > 1:
         dist.destroy_process_group()
@@ -647,10 +748,19 @@ def _allreduce(x: float, op, device) -> float:
     return float(t.item())
 
 
-def _attach(line: dict, results: dict) -> None:
-    """First sharded run -> line["sharded"], the others -> line["sharded_<config>[_<exchange>]"]."""
-    for i, (c, r) in enumerate(results.items()):
-        line["sharded" if i == 0 else "sharded_" + c.replace("-", "")] = r
+def _attach(line: dict, results: dict, mode: str) -> None:
+    """graphs mode: the first sharded run -> line["sharded"], the others ->
+    line["sharded_<config>[_<exchange>]"]; sharded mode: every extra under
+    its own key ("replicas", "sharded_<config>[_<exchange>]")."""
+    first = mode != "sharded"
+    for c, r in results.items():
+        if c in ("replicas", "timeout"):
+            line[c] = r
+        elif first:
+            line["sharded"] = r
+            first = False
+        else:
+            line["sharded_" + c.replace("-", "")] = r
 
 
 def _emit(line: dict, out: str | None) -> None:

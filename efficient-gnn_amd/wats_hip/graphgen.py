@@ -148,6 +148,26 @@ def named_graph(name: str, seed: int = 0) -> CSRGraph:
     return rmat_graph(n, nnz, seed=seed)
 
 
+def connect_isolated(g: CSRGraph, seed: int = 0) -> CSRGraph:
+    """The same graph with every isolated node attached (both directions) to
+    one uniformly random other node: an arxiv-shaped input with no
+    closed-form rows (R-MAT at the ogbn-arxiv size leaves 44.6 % of the nodes
+    isolated; the real ogbn-arxiv has none).  Unweighted graphs only."""
+    if g.values is not None:
+        raise ValueError("connect_isolated: unweighted graphs only")
+    rng = np.random.default_rng(seed)
+    deg = np.diff(g.indptr)
+    iso = np.flatnonzero(deg == 0)
+    if iso.size == 0 or g.n < 2:
+        return g
+    other = rng.integers(0, g.n - 1, size=iso.size)
+    other = other + (other >= iso)            # never a self loop
+    rows = np.repeat(np.arange(g.n, dtype=np.int64), deg)
+    src = np.concatenate([rows, iso, other])
+    dst = np.concatenate([g.indices.astype(np.int64), other, iso])
+    return coo_to_csr(g.n, src, dst)
+
+
 def random_graph(n: int, p: float, seed: int = 0, directed: bool = True, weighted: bool = False,
                  self_loop_frac: float = 0.0, isolated_frac: float = 0.0) -> CSRGraph:
     """Small Erdos-Renyi-style graph with optional weights / self loops /
