@@ -314,6 +314,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                      "traffic": None, "kernel": kernel,
                      "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
                      "avg_exchange_us": prof["exchange_ms"] * 1e3,
+                     "exchange_overlapped": prof.get("overlapped", False),
                      "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
                      "nominal_8d_bytes": b_8d,

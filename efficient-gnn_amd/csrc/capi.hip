@@ -150,6 +150,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hub_iter")) {
     L->tune.hub_iter = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
+  } else if (!strcmp(key, "overlap")) {
+    L->tune.overlap = value ? 1 : 0;
+    return WG_OK;  // launch-time choice (a captured chain re-captures: tune_gen)
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;
   } else {

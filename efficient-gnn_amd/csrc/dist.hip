@@ -76,7 +76,10 @@ __device__ __forceinline__ void ipc_wait(const IpcPull& p, bool signal) {
     const int q = threadIdx.x;
     const int64_t target = s_target;
     bool ok = true;
-    if (q < p.world && q != p.rank) {
+    // once a wait has timed out (a lost peer) later phases do not wait again: the chain
+    // finishes in one 60 s timeout, not one per phase, and wg_dist_status reports it
+    const bool failed = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (q < p.world && q != p.rank && !failed) {
       const uint64_t t0 = wall_clock64();
       while (__hip_atomic_load(p.flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
         __builtin_amdgcn_s_sleep(2);
@@ -157,6 +160,10 @@ struct wg_dist_s {
   bool use_graph = true;
   hipStream_t cap = nullptr;  // capture / replay stream (the caller's may be the null stream)
   hipEvent_t fork = nullptr, join = nullptr;
+  // exchange overlapped with the own-column half of each step (two-phase steps, step.hip)
+  hipStream_t xs = nullptr;   // exchange stream
+  hipEvent_t xfork = nullptr, xjoin = nullptr;
+  bool overlapped = false;    // the last chain ran two-phase steps
   hipGraphExec_t exec = nullptr;
   GraphKey key{};
   int warm = 0;  // eager calls made with the current key (the first builds plans / workspace)
@@ -185,7 +192,10 @@ struct wg_dist_s {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
+    if (xfork) (void)hipEventDestroy(xfork);
+    if (xjoin) (void)hipEventDestroy(xjoin);
     if (cap) (void)hipStreamDestroy(cap);
+    if (xs) (void)hipStreamDestroy(xs);
     (void)hipFree(send_rows);
     (void)hipFree(ws);
   }
@@ -265,6 +275,35 @@ struct wg_dist_s {
     return mark(st, false);
   }
 
+  // One Chebyshev step that gathers from `cur` (own rows final, halo rows to be
+  // refreshed): without overlap, exchange then the step; with overlap, the
+  // exchange forks onto xs while phase 1 (own-column entries, into `part`) runs
+  // on st; st joins the exchange, then phase 2 (halo entries + part, epilogue).
+  // Hazards: the exchange writes only cur's halo rows and reads its own rows;
+  // phase 1 reads only own rows; it forks after every earlier kernel on st (the
+  // previous step wrote cur's own rows and last read the other buffer's halo).
+  template <typename StepFn>
+  int step_with_exchange(float* cur, float* sendbuf, int64_t Fp, hipStream_t st, int slot, const int32_t* rsplit,
+                         double* part, StepFn&& launch) {
+    if (!rsplit) {
+      if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
+      return launch(st, nullptr);
+    }
+    WG_HIP_TRY(hipEventRecord(xfork, st));
+    WG_HIP_TRY(hipStreamWaitEvent(xs, xfork, 0));
+    if (int rc = exchange(cur, sendbuf, Fp, xs, slot)) return rc;
+    WG_HIP_TRY(hipEventRecord(xjoin, xs));
+    PhaseArgs p1;
+    p1.phase = 1;
+    p1.rsplit = rsplit;
+    p1.part = part;
+    if (int rc = launch(st, &p1)) return rc;
+    WG_HIP_TRY(hipStreamWaitEvent(st, xjoin, 0));
+    PhaseArgs p2 = p1;
+    p2.phase = 2;
+    return launch(st, &p2);
+  }
+
   // the whole chain on stream st (eager, or being captured)
   int chain(const float* X0, int64_t F, int32_t K, double s, float* S, float* H, hipStream_t st) {
     Lds1Plan* lp = nullptr;
@@ -278,7 +317,14 @@ struct wg_dist_s {
     // lds: T ping-pong (own rows) + u ping-pong (padded column space); else T ping-pong over [own | halo]
     // F > 1 / weighted: heat sum by Clenshaw's recurrence (as wg_wavelet_features), X0 kept in its own buffer
     const bool clen = !lp && L->tune.clenshaw && K >= 1;
-    const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd + (clen ? own : 0);
+    // two-phase steps overlapping the exchange (gather-kernel path, rows column-sorted, peers present)
+    const int32_t* rsplit = nullptr;
+    if (!lp && L->tune.overlap && world > 1 && n_own > 0 && K >= 1)
+      if (int rc = get_row_split(L, &rsplit)) return rc;
+    overlapped = rsplit != nullptr;
+    const size_t partf = rsplit ? 2 * own : 0;  // float64 row partials (n_own x Fp doubles)
+    const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd + (clen ? own : 0) +
+                        partf;
     if (ws_floats < need) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       WG_HIP_TRY(hipStreamIsCapturing(st, &cs));
@@ -324,6 +370,7 @@ struct wg_dist_s {
     float* A[2] = {ipc ? region : take(ext), ipc ? region + slot_floats : take(ext)};
     float* sint = take(own);
     float* sendbuf = take(snd);
+    double* part = rsplit ? reinterpret_cast<double*>(take(partf)) : nullptr;  // 256-B aligned (take rounds)
     int rc = WG_OK;
     if (sig) rc = ipc_wait_only(st);
     if (!rc) rc = launch_permute_pad(L, F, Fp, X0, A[0], st);
@@ -343,22 +390,26 @@ struct wg_dist_s {
       for (int32_t j = 1; j <= K && !rc; ++j) {
         const int32_t k = K - j;  // this phase computes b_k (k = 0: the final S)
         float* cur = A[(j - 1) & 1];
-        rc = exchange(cur, sendbuf, Fp, st, (j - 1) & 1);
-        if (rc) break;
         const bool prev_stored = j >= 3;  // b_{k+2} in slot j&1 (j == 2: the implicit b_K; j == 1: zero)
         const double ck = c[k] - (j == 2 ? c[K] : 0.0);
         const double cacc = (j == 1) ? (k == 0 ? c[K] : 2.0 * c[K]) : (k == 0 ? 1.0 : 2.0);
         ClenArgs cl{x0, ck, cacc, k == 0 ? 1 : 0};
-        rc = launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr, k == 0 ? nullptr : A[j & 1],
-                         k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, st, false, nullptr, &cl);
+        rc = step_with_exchange(cur, sendbuf, Fp, st, (j - 1) & 1, rsplit, part,
+                                [&](hipStream_t s2, const PhaseArgs* ph) {
+                                  return launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr,
+                                                     k == 0 ? nullptr : A[j & 1], k == 0 ? sint : nullptr, nullptr,
+                                                     1.0, 0.0, s2, false, nullptr, &cl, ph);
+                                });
       }
     } else {
       for (int32_t k = 1; k <= K && !rc; ++k) {
         float* cur = A[(k - 1) & 1];
-        rc = exchange(cur, sendbuf, Fp, st, (k - 1) & 1);
-        if (!rc)
-          rc = launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr,
-                           1.0, std::exp(-s * (double)k), st);
+        rc = step_with_exchange(cur, sendbuf, Fp, st, (k - 1) & 1, rsplit, part,
+                                [&](hipStream_t s2, const PhaseArgs* ph) {
+                                  return launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr,
+                                                     k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
+                                                     std::exp(-s * (double)k), s2, false, nullptr, nullptr, ph);
+                                });
       }
     }
     if (!rc && sig) rc = ipc_signal(st);  // phase K
@@ -415,8 +466,11 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
       rc = fail(WG_ERR_HIP, "wg_dist_create: send_rows copy");
   }
   if (!rc && (hipStreamCreateWithFlags(&D->cap, hipStreamNonBlocking) != hipSuccess ||
+              hipStreamCreateWithFlags(&D->xs, hipStreamNonBlocking) != hipSuccess ||
               hipEventCreateWithFlags(&D->fork, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess))
+              hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess ||
+              hipEventCreateWithFlags(&D->xfork, hipEventDisableTiming) != hipSuccess ||
+              hipEventCreateWithFlags(&D->xjoin, hipEventDisableTiming) != hipSuccess))
     rc = fail(WG_ERR_HIP, "wg_dist_create: stream/event");
   if (!rc && unique_id) {  // NULL: no RCCL communicator (one-sided IPC exchange, wg_dist_ipc_*)
     ncclUniqueId id;
@@ -580,6 +634,19 @@ int wg_dist_status(wg_dist_t D, int32_t* timed_out) {
   if (!D->err) return WG_OK;
   WG_HIP_TRY(hipDeviceSynchronize());
   WG_HIP_TRY(hipMemcpy(timed_out, D->err, sizeof(int32_t), hipMemcpyDeviceToHost));
+  return WG_OK;
+}
+
+int wg_dist_info(wg_dist_t D, int64_t* out) {
+  if (!D || !out) return fail(WG_ERR_INVALID, "wg_dist_info: NULL argument");
+  out[0] = D->overlapped ? 1 : 0;
+  out[1] = D->n_own;
+  out[2] = D->n_halo;
+  out[3] = D->n_send;
+  out[4] = D->world;
+  out[5] = D->ipc ? 1 : (D->comm ? 2 : 0);
+  out[6] = D->exec ? 1 : 0;
+  out[7] = 0;
   return WG_OK;
 }
 

@@ -143,6 +143,7 @@ struct Tuning {
   int32_t hub_vidx = 0;      // hub teams: 1 = 16-B column loads, 4 consecutive entries per lane (s26, 8M R-MAT: 1725 vs 1299 us, off)
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
+  int32_t overlap = 1;       // row-sharded chain: two-phase steps overlapping the halo exchange (dist.hip)
 };
 
 }  // namespace wg
@@ -170,6 +171,7 @@ struct wg_laplacian_s {
   bool unit = false;
   bool cols_sorted = false;   // rows' entries in ascending internal column (sort_row_columns)
   double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
+  int32_t* rsplit = nullptr;  // [n_rows] first halo entry of each row (two-phase steps), lazily built
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
   bool lds1_failed[2] = {false, false};        // not applicable (too many blocks): use the gather kernel
   // workspace for wg_wavelet_features
@@ -205,9 +207,21 @@ struct ClenArgs {
   // uin: xm1 is u, uprev: xm2 is u, uout: write u (not on the final step)
   int uin = 0, uprev = 0, uout = 0;
 };
+// Two-phase step (the row-sharded chain overlaps the halo exchange with phase 1): phase 1
+// sums each row's own-column entries [row start, rsplit[row]) into part (float64, row
+// stride F, no epilogue); phase 2 sums the halo entries [rsplit[row], row end), adds part
+// and runs the step's epilogue.  phase 0 = the whole row in one launch.
+struct PhaseArgs {
+  int phase = 0;
+  const int32_t* rsplit = nullptr;  // [n_rows] first entry with column >= n_rows (rows column-sorted)
+  double* part = nullptr;           // [n_rows][F]
+};
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
-                float* S_out = nullptr, const ClenArgs* cl = nullptr);
+                float* S_out = nullptr, const ClenArgs* cl = nullptr, const PhaseArgs* ph = nullptr);
+// rsplit for two-phase steps: per internal row, the first entry whose column is a halo
+// column (>= n_rows); built once (synchronous), nullptr when rows are not column-sorted
+int get_row_split(wg_laplacian_s* L, const int32_t** out);
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef,
                     float* S, float* H, hipStream_t stream, int64_t ldi = 0);  // ldi: internal row stride (0 = F)
 // the internal signal width of an F-column chain: odd / 4-unaligned F >= 3 is

@@ -15,11 +15,21 @@
 //    row; sub-groups reduce by shuffles inside each wave, the 4 wave sums meet
 //    in LDS behind one barrier.
 //  * Split mode (hub rows longer than CH nonzeros): one workgroup per CH-nnz
-//    chunk writes a float64 partial; a small combine kernel launched right
-//    after sums each row's partials in chunk order and runs the epilogue.
-//    (An in-kernel last-arriver combine needs an agent-scope release fence
-//    per chunk -- buffer_wbl2 of the XCD L2 with the step's dirty S/T_k
-//    lines in it -- measured 1.3-2.2x slower for the whole step.)
+//    chunk writes a float64 partial.  The last chunk to arrive finishes the row
+//    in the same kernel (inkernel_combine = 1, the default): partials are sc1
+//    (write-through) stores drained by every storing wave (s_waitcnt
+//    vmcnt(0)), then one agent-scope atomic add per chunk on a monotonic
+//    per-row counter; the workgroup whose add completes the row reads every
+//    chunk's partial with sc1 loads, in chunk order, and runs the epilogue.
+//    This relies on gfx950's cache behaviour (sc1 stores write through to L2,
+//    sc1 loads bypass the L1), the hand-off of MI355X_MICROARCH.md's table
+//    row 1 -- not on HIP memory-model release/acquire ordering, which would
+//    need an agent-scope release per chunk (buffer_wbl2 of an XCD L2 full of
+//    the step's dirty lines: 1.3-2.2x slower for the whole step, DESIGN.md
+//    4.1).  inkernel_combine = 0 runs a separate combine_kernel instead.
+//  * Two-phase steps (row-sharded chain, dist.hip): phase 1 sums each row's
+//    own-column entries into a float64 row partial while the halo exchange
+//    runs; phase 2 sums the halo entries, adds the partial, runs the epilogue.
 // Row sums accumulate in float64 (products of two float32 are exact).
 #include <algorithm>
 #include <cmath>
@@ -66,7 +76,37 @@ struct StepArgs {
   // uout: xk gets u.
   const double* dinv;
   int32_t uin, uprev, uout;
+  // two-phase step (row-sharded chain, exchange overlapped): phase 1 sums each row's entries
+  // [e0, rsplit[row]) (the own columns) into part[row] (float64, row stride ld); phase 2 sums
+  // [rsplit[row], e1) (the halo columns), adds part[row] and runs the epilogue.  0 = whole row.
+  int32_t phase;
+  const int32_t* rsplit;
+  double* part;
 };
+
+// the entry range of a row (or of a split-row chunk) this launch's phase covers
+__device__ __forceinline__ void phase_range(const StepArgs& a, int64_t row, int32_t& e0, int32_t& e1) {
+  if (a.phase == 0) return;
+  const int32_t sp = a.rsplit[row];
+  if (a.phase == 1) e1 = min(e1, sp);
+  else e0 = max(e0, sp);
+  if (e1 < e0) e1 = e0;
+}
+
+// phase 1: the row's own-column sum goes to part (no epilogue); phase 2: add it before the epilogue
+template <int VEC>
+__device__ __forceinline__ void part_store(const StepArgs& a, int64_t row, int fs, const double (&acc)[VEC]) {
+  double* p = a.part + row * a.ld + (int64_t)fs * VEC;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) p[j] = acc[j];
+}
+
+template <int VEC>
+__device__ __forceinline__ void part_add(const StepArgs& a, int64_t row, int fs, double (&acc)[VEC]) {
+  const double* p = a.part + row * a.ld + (int64_t)fs * VEC;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] += p[j];
+}
 
 template <int VEC>
 __device__ __forceinline__ void load_vec(const float* p, float (&x)[VEC]) {
@@ -540,8 +580,9 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     const bool active = team < tpw && row < seg.end;
     EpiIn<VEC> in;
     if (active) {
-      if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
-      const int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
+      if (ns == 0 && a.phase != 1) epi_prefetch<VEC>(a, row, fs, in);
+      int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
+      phase_range(a, row, e0, e1);
       if constexpr (VEC == 1 && !HOT) {
         if (a.vidx && LF == 1) accumulate_vidx1(a, e0, e1, ns, LN, a.xm1, acc);
         else acc_range<VEC, BCAST, HOT, HUB>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
@@ -550,7 +591,14 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       }
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
-    if (active && ns == 0) step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
+    if (active && ns == 0) {
+      if (a.phase == 1) {
+        part_store<VEC>(a, row, fs, acc);
+      } else {
+        if (a.phase == 2) part_add<VEC>(a, row, fs, acc);
+        step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
+      }
+    }
     return;
   }
 
@@ -570,11 +618,12 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     e0 = d.e0;
     e1 = d.e1;
   }
+  phase_range(a, row, e0, e1);
   const int G = 64 / LF;
   const int sg = lane / LF;
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
-  if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
+  if (seg.mode == 1 && threadIdx.x < LF && a.phase != 1) epi_prefetch<VEC>(a, row, threadIdx.x, in);
   if constexpr (VEC == 1 && !HOT) {
     if (a.vidx && LF == 1) {
       // chunk-aligned ranges: for split chunks e0 is a multiple of CH (>= 4) from the row start, so
@@ -602,7 +651,12 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       for (int j = 0; j < VEC; ++j) acc[j] += red[(w * LF + t) * VEC + j];
     }
     if (seg.mode == 1) {
-      step_epilogue<VEC>(a, row, t, acc, in, 0);
+      if (a.phase == 1) {
+        part_store<VEC>(a, row, t, acc);
+      } else {
+        if (a.phase == 2) part_add<VEC>(a, row, t, acc);
+        step_epilogue<VEC>(a, row, t, acc, in, 0);
+      }
     } else {
       double* p = a.partial + (int64_t)cid * (LF * VEC) + t * VEC;
 #pragma unroll
@@ -629,7 +683,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     if (s_last && threadIdx.x < LF) {
       const int t = threadIdx.x;
       EpiIn<VEC> in2;
-      epi_prefetch<VEC>(a, row, t, in2);
+      if (a.phase != 1) epi_prefetch<VEC>(a, row, t, in2);
       double sum[VEC];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) sum[j] = 0.0;
@@ -638,7 +692,12 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
 #pragma unroll
         for (int j = 0; j < VEC; ++j) sum[j] += __hip_atomic_load(pp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      step_epilogue<VEC>(a, row, t, sum, in2, 0);
+      if (a.phase == 1) {
+        part_store<VEC>(a, row, t, sum);
+      } else {
+        if (a.phase == 2) part_add<VEC>(a, row, t, sum);
+        step_epilogue<VEC>(a, row, t, sum, in2, 0);
+      }
     }
   }
 }
@@ -693,7 +752,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
   const int2 rc = rowchunks[row];
   const int width = LF * VEC;
   EpiIn<VEC> in;
-  epi_prefetch<VEC>(a, row, fs, in);
+  if (a.phase != 1) epi_prefetch<VEC>(a, row, fs, in);
   double acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
@@ -702,6 +761,11 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] += p[j];
   }
+  if (a.phase == 1) {
+    part_store<VEC>(a, row, fs, acc);
+    return;
+  }
+  if (a.phase == 2) part_add<VEC>(a, row, fs, acc);
   step_epilogue<VEC>(a, row, fs, acc, in, sg * LF);
 }
 
@@ -937,12 +1001,12 @@ int launch_hub(const Plan& plan, const StepArgs& a, hipStream_t stream) {
 template <int VEC>
 int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const SegTable& tab = plan.tab;
-  if (VEC == 4 && a.hubf > 0 && a.LF > 1 && a.bcast && tab.total_blocks > 0) {
+  if (VEC == 4 && a.hubf > 0 && a.LF > 1 && a.bcast && tab.total_blocks > 0 && a.phase == 0) {
     int rc = plan.nw == 16 ? launch_hub<4, 16>(plan, a, stream)
              : plan.nw == 8 ? launch_hub<4, 8>(plan, a, stream)
                             : launch_hub<4, 4>(plan, a, stream);
     if (rc) return rc;
-  } else if (VEC == 1 && plan.hot > 0 && tab.total_blocks > 0) {
+  } else if (VEC == 1 && plan.hot > 0 && tab.total_blocks > 0 && a.phase == 0) {
     int rc = plan.nw == 16 ? launch_hot<16>(plan, a, stream) : launch_hot<4>(plan, a, stream);
     if (rc) return rc;
   } else if (tab.total_blocks > 0) {
@@ -1169,8 +1233,10 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start) {
 
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out,
-                const ClenArgs* cl) {
+                const ClenArgs* cl, const PhaseArgs* ph) {
   if (L->n_rows == 0) return WG_OK;
+  if (ph && ph->phase != 0 && (!ph->rsplit || !ph->part || S_out))
+    return fail(WG_ERR_INVALID, "launch_step: a two-phase step needs rsplit and part (and no fused finalize)");
   if (int rc = prof_mark(L, stream, true)) return rc;
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H, S_out});
   int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
@@ -1213,6 +1279,16 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       a.uout = cl->final_ ? 0 : cl->uout;
       if (a.uin) a.val = nullptr;  // unweighted: the gathered u needs no values
     }
+    if (ph && ph->phase != 0) {
+      a.phase = ph->phase;
+      a.rsplit = ph->rsplit;
+      a.part = ph->part + f0;
+      if (a.phase == 1) {  // nothing but the sums: no epilogue operands, no stores of T / S / H
+        a.xk = nullptr;
+        a.S = nullptr;
+        a.H = nullptr;
+      }
+    }
     a.chunks = plan->chunks;
     a.partial = plan->partial;
     a.rowchunks = plan->rowchunks;
@@ -1241,7 +1317,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     else rc = launch_step_vec<1>(*plan, a, stream);
     if (rc) return rc;
   }
-  if (H && !fuse_h) {
+  if (H && !fuse_h && !(ph && ph->phase == 1)) {
     hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(L->n_rows, 4)), dim3(kBlock), 0, stream, L->n_rows, F, S, H);
     WG_LAUNCH_CHECK();
   }
@@ -1332,6 +1408,43 @@ int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, flo
     hipLaunchKernelGGL(permute_in_closed_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
                        L->n_active, coef, S, H);
   WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
+namespace {
+// first entry of each row whose column is >= split (rows sorted by column)
+__global__ void row_split_kernel(int64_t n, int32_t split, const int32_t* __restrict__ rowptr,
+                                 const int32_t* __restrict__ col, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t lo = rowptr[i], hi = rowptr[i + 1];
+  while (lo < hi) {
+    const int32_t mid = lo + ((hi - lo) >> 1);
+    if (col[mid] < split) lo = mid + 1;
+    else hi = mid;
+  }
+  out[i] = lo;
+}
+}  // namespace
+
+int get_row_split(wg_laplacian_s* L, const int32_t** out) {
+  *out = nullptr;
+  if (!L->cols_sorted) return WG_OK;
+  if (!L->rsplit) {
+    int32_t* p = nullptr;
+    if (int rc = dmalloc(&p, (size_t)std::max<int64_t>(1, L->n_rows))) return rc;
+    if (L->n_rows > 0) {
+      hipLaunchKernelGGL(row_split_kernel, dim3((unsigned)ceil_div(L->n_rows, 256)), dim3(256), 0, nullptr, L->n_rows,
+                         (int32_t)L->n_rows, L->rowptr, L->col, p);
+      const hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) {
+        (void)hipFree(p);
+        return fail(WG_ERR_HIP, "row_split: %s", hipGetErrorString(e));
+      }
+    }
+    L->rsplit = p;
+  }
+  *out = L->rsplit;
   return WG_OK;
 }
 

@@ -81,6 +81,7 @@ SIGNATURES = {
     "wg_dist_destroy": (ctypes.c_int, [c_vp]),
     "wg_dist_set_graph": (ctypes.c_int, [c_vp, c_i32]),
     "wg_dist_wavelet_features": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_f64, c_vp, c_vp, c_vp]),
+    "wg_dist_info": (ctypes.c_int, [c_vp, ctypes.POINTER(c_i64)]),
     "wg_dist_profile_collect": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
     "wg_dist_ipc_local": (ctypes.c_int, [c_vp, c_i64, c_vp]),
     "wg_dist_ipc_connect": (ctypes.c_int, [c_vp, c_vp, c_vp]),

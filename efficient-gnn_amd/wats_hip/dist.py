@@ -404,9 +404,25 @@ class ShardedWavelet:
         st = self.L.profile_collect()
         self.L.profile_enable(False)
         self.profile = False
-        n = max(1, st["launches"])
+        # two-phase (overlapped) steps record two launches per Chebyshev step
+        per_step = 2 if self.info().get("overlapped") else 1
+        n = max(1, st["launches"] // per_step)
         return dict(exchange_ms=sum(ex) / max(1, len(ex)), step_ms=st["sum_ms"] / n, max_step_ms=st["max_ms"],
-                    launches=st["launches"])
+                    launches=st["launches"], overlapped=per_step == 2)
+
+    def info(self) -> dict:
+        """State of the native chain (wg_dist_info): overlapped (the last chain
+        ran two-phase steps, the exchange on its own stream), own / halo / sent
+        rows, world, exchange kind, captured graph present."""
+        if self._dist is None:
+            return {}
+        out = (ctypes.c_int64 * 8)()
+        check(_lib.load().wg_dist_info(self._dist, out), "dist_info")
+        keys = ("overlapped", "n_own", "n_halo", "n_send", "world", "exchange", "captured")
+        d = dict(zip(keys, [int(v) for v in out]))
+        d["overlapped"] = bool(d["overlapped"])
+        d["exchange"] = {1: "ipc", 2: "rccl"}.get(d["exchange"], "none")
+        return d
 
     # -------------------------------------------------------------- chain
     def u_len(self) -> int:
@@ -474,7 +490,8 @@ class ShardedWavelet:
         import math
         p = self.plan
         L = self.L
-        X = X0_local.to(self.device, torch.float32).reshape(p.n_own, -1).contiguous()
+        F_in = X0_local.shape[-1] if X0_local.dim() == 2 else 1
+        X = X0_local.to(self.device, torch.float32).reshape(p.n_own, F_in).contiguous()   # (0, F) on an empty shard
         F = X.shape[1]
         if self.exchange == "ipc" and F > self._ipc_F:
             self.close()

@@ -245,6 +245,9 @@ int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, 
  * step kernel runs.  The chain is captured into a hipGraph on its second call
  * with the same arguments and replayed from then on (wg_dist_set_graph(D, 0)
  * keeps it eager; profiling via wg_profile_enable(L) also runs eagerly).
+ * With peers and column-sorted rows (the default) each step is split in two
+ * launches: the entries of own columns run while the exchange proceeds on a
+ * second stream, the halo entries after it (tuning key "overlap" = 0: off).
  * wg_dist_unique_id fills NCCL_UNIQUE_ID_BYTES (128) bytes on one rank; every
  * rank passes the same bytes to wg_dist_create (collective: blocks until all
  * ranks joined); unique_id NULL = no RCCL communicator (IPC exchange below).  X0, S, H: own rows (n_rows, F) in the caller's order.
@@ -258,6 +261,12 @@ int wg_dist_destroy(wg_dist_t D);
 int wg_dist_set_graph(wg_dist_t D, int32_t enable);
 int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K, double s, float* S,
                              float* H, void* stream);
+/* State of the sharded chain, out8_host: [0] 1 if the last chain overlapped
+ * each step's halo exchange with the step's own-column half (two-phase
+ * steps: 2 step launches per Chebyshev step), [1] own rows, [2] halo rows,
+ * [3] rows sent, [4] world, [5] exchange (1 IPC, 2 RCCL, 0 none), [6] 1 if a
+ * captured hipGraph exists, [7] 0. */
+int wg_dist_info(wg_dist_t D, int64_t* out8_host);
 /* Total time (ms) and count of the halo exchanges (pack + RCCL, or the IPC
  * pull) recorded while profiling was enabled on the shard's handle; resets. */
 int wg_dist_profile_collect(wg_dist_t D, double* exchange_ms_host, int64_t* count_host);

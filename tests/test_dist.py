@@ -144,6 +144,9 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host"):
         H, S = outs[0]
         same = all(torch.equal(o[1], S) and torch.equal(o[0], H) for o in outs)
         if exchange == "ipc":
+            # the gather-kernel path overlaps each step's exchange with the step's own-column half
+            ov = sw.info()["overlapped"]
+            assert ov == (q_path == "t" and sw.plan.n_halo > 0), (ov, q_path, sw.plan.n_halo)
             sw.check_exchange()
             sw.close()
         q.put((rank, S.cpu().numpy(), H.cpu().numpy(), q_path, same))
@@ -400,7 +403,7 @@ def test_ipc_chain_with_an_empty_shard(F):
     procs = [ctx.Process(target=_empty_shard_worker, args=(r, 4, port, bounds, F, q)) for r in range(4)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(4)], key=lambda t: t[0])
+    res = sorted([q.get(timeout=170) for _ in range(4)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
