@@ -41,10 +41,19 @@ def _gpu():
     wats_hip._lib.load()
 
 
+def _log(msg):
+    import sys
+    import time
+    print(f"[fullsize {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _oracle(indptr, indices, X, k, cols=None):
     from oracle import wats_oracle_c as C
+    import time
     Xs = X if cols is None else np.ascontiguousarray(X[:, cols])
+    t0 = time.perf_counter()
     S, H = C.graph_wavelet_features(indptr, indices, None, Xs, k, 0.8, threads=ORACLE_THREADS)
+    _log(f"oracle: n={len(indptr) - 1} nnz={len(indices)} K={k} F={Xs.shape[1]}: {time.perf_counter() - t0:.1f} s")
     return S, H
 
 
@@ -57,6 +66,7 @@ def _graph(config, seed=0):
     key = (config, seed)
     if key not in _GRAPHS:
         n, nnz, _, _ = NAMED_CONFIGS[config]
+        _log(f"generating {config}")
         ip, ix = rmat_graph_device(n, nnz, seed=seed, device="cuda")
         _GRAPHS.clear()
         _GRAPHS[key] = (ip.cpu().numpy(), ix.cpu().numpy())
