@@ -150,6 +150,13 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hub_iter")) {
     L->tune.hub_iter = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
+  } else if (!strcmp(key, "probe")) {
+    L->tune.probe = value ? 1 : 0;
+    return WG_OK;  // launch-time, timing only
+  } else if (!strcmp(key, "fpad")) {
+    if (value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "fpad must be 4, 8 or 16");
+    L->tune.fpad = (int32_t)value;
+    return WG_OK;  // launch-time choice (workspace regrows on the next call)
   } else if (!strcmp(key, "overlap")) {
     L->tune.overlap = value ? 1 : 0;
     return WG_OK;  // launch-time choice (a captured chain re-captures: tune_gen)
@@ -254,7 +261,7 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     if (rc0) return rc0;
   }
   // internal width: F padded to a multiple of 4 (zero columns) for float4 lanes
-  const int64_t Fp = lp ? F : padded_features(F);
+  const int64_t Fp = lp ? F : padded_features(L, F);
   // workspace: T ping-pong (2) + internal S [+ u ping-pong, padded to whole column blocks], 256-B aligned
   const size_t stride = ((size_t)n * Fp + 63) / 64 * 64;
   const size_t ustride = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;

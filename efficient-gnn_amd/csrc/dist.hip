@@ -309,7 +309,7 @@ struct wg_dist_s {
     Lds1Plan* lp = nullptr;
     if (F == 1 && K >= 1)
       if (int rc = get_lds1_plan(L, /*active_only=*/false, &lp)) return rc;
-    const int64_t Fp = lp ? F : padded_features(F);  // internal width (zero pad columns, float4 lanes)
+    const int64_t Fp = lp ? F : padded_features(L, F);  // internal width (zero pad columns, float4 lanes)
     const size_t ext = ((size_t)n_cols * Fp + 63) / 64 * 64;
     const size_t own = ((size_t)n_own * Fp + 63) / 64 * 64;
     const size_t snd = ((size_t)std::max<int64_t>(n_send, 1) * Fp + 63) / 64 * 64;
@@ -507,7 +507,7 @@ int wg_dist_set_graph(wg_dist_t D, int32_t enable) {
 
 int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K, double s, float* S, float* H,
                              void* stream_) {
-  if (!D || F < 1 || K < 0 || !S || !H || (D->n_own && !X0))
+  if (!D || F < 1 || K < 0 || (D->n_own && (!X0 || !S || !H)))  // an empty shard passes no rows
     return fail(WG_ERR_INVALID, "wg_dist_wavelet_features: bad arguments (F=%lld K=%d)", (long long)F, K);
   if (!D->comm && !D->ipc && (D->n_send > 0 || D->n_halo > 0 || D->world > 1))
     return fail(WG_ERR_INVALID, "wg_dist_wavelet_features: no exchange (no RCCL id given and IPC not connected)");
@@ -564,7 +564,7 @@ int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
   if (int rc = get_lds1_plan(D->L, /*active_only=*/false, &lp)) return rc;
   if (lp) ulen = lp->u_floats();
   D->F_max = F_max;
-  D->slot_floats = (std::max<int64_t>(D->n_cols * padded_features(F_max), ulen) + 63) / 64 * 64;
+  D->slot_floats = (std::max<int64_t>(D->n_cols * padded_features(D->L, F_max), ulen) + 63) / 64 * 64;
   const size_t bytes = sizeof(float) * 2 * D->slot_floats + sizeof(int64_t) * D->world;
   if (int rc = dmalloc(reinterpret_cast<char**>(&D->region), bytes)) return rc;
   if (int rc = dmalloc(&D->count, 1)) return rc;

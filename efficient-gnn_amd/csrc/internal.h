@@ -144,6 +144,8 @@ struct Tuning {
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
   int32_t overlap = 1;       // row-sharded chain: two-phase steps overlapping the halo exchange (dist.hip)
+  int32_t probe = 0;         // timing only: gathers + one output stream, no epilogue (results wrong)
+  int32_t fpad = 4;          // internal signal width of F >= 3: a multiple of 4 (8 / 16: whole cache-line rows)
 };
 
 }  // namespace wg
@@ -227,7 +229,7 @@ int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float
 // the internal signal width of an F-column chain: odd / 4-unaligned F >= 3 is
 // padded to a multiple of 4 (zero columns), so the step kernel runs float4
 // lanes (Reddit-size F = 41: 5383 -> 1878 us per step as F = 44)
-int padded_features(int64_t F);
+int padded_features(const wg_laplacian_s* L, int64_t F);
 // launch_step would run F columns as one tile (the condition for a fused H / finalize)
 bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const void*> ptrs);
 // permute-in that also writes the closed-form rows' S and H in the caller's order

@@ -82,6 +82,7 @@ struct StepArgs {
   int32_t phase;
   const int32_t* rsplit;
   double* part;
+  int32_t probe;  // timing probe (knob "probe"): gathers only -- no epilogue operands, acc stored to xk
 };
 
 // the entry range of a row (or of a split-row chunk) this launch's phase covers
@@ -161,6 +162,7 @@ struct EpiIn {
 
 template <int VEC>
 __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int fs, EpiIn<VEC>& in) {
+  if (a.probe) return;
   const int64_t off = row * a.ld + (int64_t)fs * VEC;
   in.iso = a.iso[row];
   in.orow = a.out_perm ? a.out_perm[row] : (int32_t)row;
@@ -187,6 +189,10 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
                                               const EpiIn<VEC>& in, int lane0) {
   const int64_t off = row * a.ld + (int64_t)fs * VEC;
   const bool nt_st = (a.nt & 4) != 0;
+  if (a.probe) {  // timing probe: the row sums only (results are not the chain's)
+    if (a.xk) store_vec<VEC>(a.xk + off, acc);
+    return;
+  }
   if (a.clen && a.uin) {  // sum of u_j over the row: L_hat b = -dinv_i * sum (off-diagonal part)
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] *= -in.dinv;
@@ -1289,6 +1295,8 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.H = nullptr;
       }
     }
+    a.probe = L->tune.probe;
+    if (a.probe && !a.xk) a.xk = S ? S + f0 : nullptr;  // the final step of a chain stores into S
     a.chunks = plan->chunks;
     a.partial = plan->partial;
     a.rowchunks = plan->rowchunks;
@@ -1448,7 +1456,13 @@ int get_row_split(wg_laplacian_s* L, const int32_t** out) {
   return WG_OK;
 }
 
-int padded_features(int64_t F) { return (int)((F >= 3 && F % 4) ? (F + 3) / 4 * 4 : F); }
+int padded_features(const wg_laplacian_s* L, int64_t F) {
+  if (F < 3) return (int)F;
+  // knob fpad: round the width up to a multiple of 4 (default: float4 lanes) or of 8 / 16
+  // (F = 44 -> 48: a 192-B row at 64-B alignment spans 2 cache lines, a 176-B row 2.25 on average)
+  const int64_t m = (L && (L->tune.fpad == 8 || L->tune.fpad == 16)) ? L->tune.fpad : 4;
+  return (int)((F + m - 1) / m * m);
+}
 
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream) {
   hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(n, 4)), dim3(kBlock), 0, stream, n, F, S, H);

@@ -153,9 +153,13 @@ def _free_port():
 
 
 def _shard_worker(rank, world, port, config, F, K, seed_x, q):
+    import faulthandler
     import sys
+    faulthandler.dump_traceback_later(120, exit=False)   # where a stuck rank is, before the parent gives up
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["WATS_DIST_LOG"] = "1"
+    os.environ["RANK"] = str(rank)
     sys.path.insert(0, os.path.join(REPO, "efficient-gnn_amd"))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -173,7 +177,11 @@ def _shard_worker(rank, world, port, config, F, K, seed_x, q):
         sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n, bounds, exchange="ipc", device="cuda:0",
                             max_features=F)
         X = np.random.default_rng(seed_x).standard_normal((n, F)).astype(np.float32)[r0:r1]
-        outs = [sw.wavelet_features(torch.from_numpy(X), k=K, s=0.8) for _ in range(3)]  # eager, captured, replayed
+        outs = []
+        for i in range(3):   # eager, captured, replayed
+            outs.append(sw.wavelet_features(torch.from_numpy(X), k=K, s=0.8))
+            torch.cuda.synchronize()
+            _log(f"rank {rank}: chain {i} done")
         H, S = outs[0]
         same = all(torch.equal(o[1], S) for o in outs)
         path = "u" if (F == 1 and sw.u_len() > 0) else "t"
@@ -191,13 +199,19 @@ def _run_sharded(world, config, F, K, seed_x):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, config, F, K, seed_x, q)) for r in range(world)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, config, F, K, seed_x, q), daemon=True)
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    try:
+        res = sorted([q.get(timeout=170) for _ in range(world)], key=lambda t: t[0])
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
     return res
 
 

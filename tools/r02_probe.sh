@@ -29,6 +29,37 @@ for part in $PARTS; do
         timeout -k 10 1000 bash tools/pmc_deep.sh > "$OUT/pmc_rmat8m.log" 2>&1
       fatal pmc_rmat8m $?
       ;;
+    sweeps)
+      # gather-only probe (knob probe) and cache-line row padding (knob fpad) on the two wide workloads
+      timeout -k 10 300 python3 tools/sweep.py --config ogbn-arxiv --grid "probe=0,1,0,1" --K 16 --reps 20 \
+        > "$OUT/sweep_arxiv_probe.log" 2>&1
+      fatal sweep_arxiv_probe $?
+      timeout -k 10 400 python3 tools/sweep.py --config reddit-f41 --grid "fpad=4,8,4,8;probe=0,1" --K 16 --reps 5 \
+        > "$OUT/sweep_reddit_fpad_probe.log" 2>&1
+      fatal sweep_reddit $?
+      ;;
+    pmcprobe)
+      # PMC of the arxiv gather-only probe: requests, latency, L2 hits (compare profiles/r01/s38_pmc_deep.json)
+      SESSION=${SESSION:-r02}/pmc_arxiv_probe CONFIG=ogbn-arxiv GRID="probe=1" KERNEL="cheb_step_kernel<4" PMC_K=16 \
+        timeout -k 10 900 bash tools/pmc_deep.sh > "$OUT/pmc_arxiv_probe.log" 2>&1
+      fatal pmc_arxiv_probe $?
+      ;;
+    bench)
+      timeout -k 10 500 python3 bench.py --out "$OUT/bench.json" > "$OUT/bench.log" 2>&1
+      fatal bench $?
+      ;;
+    benchprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o run -- \
+        python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --sharded-extra none --cold-reps 0 \
+        --connected-companion 0 > "$OUT/prof.log" 2>&1
+      fatal benchprof $?
+      ;;
+    rehearse2)
+      WATS_BENCH_PG=gloo WATS_BENCH_DEVICE=0 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node=2 --master-addr=127.0.0.1 --master-port=29611 bench.py --gpus 2 --exchange ipc \
+        --sharded-extra reddit,rmat-8m --out "$OUT/rehearse2.json" > "$OUT/rehearse2.log" 2>&1
+      fatal rehearse2 $?
+      ;;
     *)
       if [ -n "${EXTRA:-}" ]; then timeout -k 10 900 bash -c "$EXTRA" > "$OUT/extra.log" 2>&1; fatal extra $?; fi
       ;;
