@@ -152,7 +152,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _shard_worker(rank, world, port, config, F, K, seed_x, q):
+def _shard_worker(rank, world, port, config, F, K, seed_x, q, graph_dir):
     import faulthandler
     import sys
     faulthandler.dump_traceback_later(120, exit=False)   # where a stuck rank is, before the parent gives up
@@ -166,14 +166,15 @@ def _shard_worker(rank, world, port, config, F, K, seed_x, q):
     try:
         from wats_hip.dist import ShardedWavelet, partition_rows
         n, nnz, _, _ = NAMED_CONFIGS[config]
-        ip, ix = rmat_graph_device(n, nnz, seed=0, device="cuda:0")
-        indptr = ip.cpu().numpy()
+        # the graph the parent generated (ranks generating it concurrently on the one shared GPU
+        # stalled for minutes inside torch.unique's radix sort), memory-mapped
+        indptr = np.load(os.path.join(graph_dir, "indptr.npy"))
+        ix = np.load(os.path.join(graph_dir, "indices.npy"), mmap_mode="r")
         bounds = partition_rows(indptr, world)
         r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
         lo, hi = int(indptr[r0]), int(indptr[r1])
-        cols = ix[lo:hi].cpu().numpy()
-        del ip, ix
-        torch.cuda.empty_cache()
+        cols = np.ascontiguousarray(ix[lo:hi])
+        del ix
         sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n, bounds, exchange="ipc", device="cuda:0",
                             max_features=F)
         X = np.random.default_rng(seed_x).standard_normal((n, F)).astype(np.float32)[r0:r1]
@@ -195,12 +196,15 @@ def _shard_worker(rank, world, port, config, F, K, seed_x, q):
         dist.destroy_process_group()
 
 
-def _run_sharded(world, config, F, K, seed_x):
+def _run_sharded(world, config, F, K, seed_x, graph_dir):
+    indptr, indices = _graph(config)
+    np.save(os.path.join(graph_dir, "indptr.npy"), indptr)
+    np.save(os.path.join(graph_dir, "indices.npy"), indices)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, config, F, K, seed_x, q), daemon=True)
-             for r in range(world)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, config, F, K, seed_x, q, graph_dir),
+                         daemon=True) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -217,13 +221,13 @@ def _run_sharded(world, config, F, K, seed_x):
 
 @pytest.mark.parametrize("world,config,F,cols", [(2, "reddit", 1, None), (4, "reddit", 1, None),
                                                  (4, "reddit", 41, [0, 21, 40]), (2, "rmat-8m", 1, None)])
-def test_sharded_full_size_vs_oracle(world, config, F, cols):
+def test_sharded_full_size_vs_oracle(world, config, F, cols, tmp_path):
     """The row-sharded chain (nnz-balanced shards, [own | halo] columns, the
     one-sided IPC exchange, the chain captured and replayed as a hipGraph) on
     the full-size graph with a random signal: every rank's rows against the
     oracle, eager == captured == replayed bit for bit."""
     K = NAMED_CONFIGS[config][2]
-    res = _run_sharded(world, config, F, K, seed_x=100 + F)
+    res = _run_sharded(world, config, F, K, 100 + F, str(tmp_path))
     for r in res:
         assert r[1] is not None, f"rank {r[0]} failed: {r[6]}"
         assert r[5], f"rank {r[0]}: eager / captured / replayed chains differ"
