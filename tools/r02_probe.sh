@@ -44,6 +44,10 @@ for part in $PARTS; do
         timeout -k 10 900 bash tools/pmc_deep.sh > "$OUT/pmc_arxiv_probe.log" 2>&1
       fatal pmc_arxiv_probe $?
       ;;
+    parity)
+      timeout -k 10 400 python3 tools/parity_distribution.py --out "$OUT/parity_distribution.json" > "$OUT/parity.log" 2>&1
+      fatal parity $?
+      ;;
     bench)
       timeout -k 10 500 python3 bench.py --out "$OUT/bench.json" > "$OUT/bench.log" 2>&1
       fatal bench $?
