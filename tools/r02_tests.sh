@@ -13,7 +13,7 @@ run() {  # $1 = tag, $2 = seconds, rest = pytest args
   echo "[$tag] rc=$rc" | tee -a "$OUT/steps.log"
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "fatal rc in $tag, stopping"; exit "$rc"; fi
 }
-for grp in ${GROUPS:-main fullsize}; do
+for grp in ${TEST_GROUPS:-main fullsize}; do
   case $grp in
     main) run main 700 tests -m gpu --ignore=tests/test_fullsize.py ;;
     fullsize) run fullsize 700 tests/test_fullsize.py -m gpu ;;
