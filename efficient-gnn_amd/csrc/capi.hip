@@ -154,7 +154,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.probe = value ? 1 : 0;
     return WG_OK;  // launch-time, timing only
   } else if (!strcmp(key, "fpad")) {
-    if (value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "fpad must be 4, 8 or 16");
+    if (value != 0 && value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "fpad must be 0, 4, 8 or 16");
     L->tune.fpad = (int32_t)value;
     return WG_OK;  // launch-time choice (workspace regrows on the next call)
   } else if (!strcmp(key, "overlap")) {

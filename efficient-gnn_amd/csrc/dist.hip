@@ -416,6 +416,11 @@ struct wg_dist_s {
         rc = fail(WG_ERR_HIP, "wg_dist: copy X0");
       std::vector<double> c(K + 1);
       for (int32_t k = 0; k <= K; ++k) c[k] = std::exp(-s * (double)k);
+      // unweighted graph (every rank created its shard with values == NULL): the stored b_k
+      // are u_k = b_k * dinv, so the gathers read no CSR values (as wg_wavelet_features,
+      // DESIGN.md 4.1) and the halo rows exchanged are u rows; X0 (phase 1) stays unscaled
+      const int useu = (L->unit && L->values_null && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 &&
+                        L->tune.hot == 0) ? 1 : 0;
       for (int32_t j = 1; j <= K && !rc; ++j) {
         const int32_t k = K - j;  // this phase computes b_k (k = 0: the final S)
         float* cur = A[(j - 1) & 1];
@@ -423,6 +428,9 @@ struct wg_dist_s {
         const double ck = c[k] - (j == 2 ? c[K] : 0.0);
         const double cacc = (j == 1) ? (k == 0 ? c[K] : 2.0 * c[K]) : (k == 0 ? 1.0 : 2.0);
         ClenArgs cl{x0, ck, cacc, k == 0 ? 1 : 0};
+        cl.uin = useu && j >= 2;          // j == 1 gathers X0 itself
+        cl.uprev = useu && prev_stored;
+        cl.uout = useu;                   // ignored on the final step (k == 0 writes S)
         rc = step_with_exchange(cur, sendbuf, Fp, st, (j - 1) & 1, rsplit, part,
                                 [&](hipStream_t s2, const PhaseArgs* ph) {
                                   return launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr,

@@ -145,7 +145,7 @@ struct Tuning {
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
   int32_t overlap = 1;       // row-sharded chain: two-phase steps overlapping the halo exchange (dist.hip)
   int32_t probe = 0;         // timing only: gathers + one output stream, no epilogue (results wrong)
-  int32_t fpad = 4;          // internal signal width of F >= 3: a multiple of 4 (8 / 16: whole cache-line rows)
+  int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple
 };
 
 }  // namespace wg
@@ -172,6 +172,8 @@ struct wg_laplacian_s {
   // up to scipy's float32 rounding, so the F == 1 LDS kernel reads no values
   bool unit = false;
   bool cols_sorted = false;   // rows' entries in ascending internal column (sort_row_columns)
+  bool values_null = false;   // created with values == NULL (unweighted by construction: every shard of the
+                              // graph agrees, so a row-sharded chain may exchange u = b * dinv)
   double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
   int32_t* rsplit = nullptr;  // [n_rows] first halo entry of each row (two-phase steps), lazily built
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]

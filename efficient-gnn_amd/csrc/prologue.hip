@@ -585,6 +585,7 @@ int wg_laplacian_create(int64_t n_rows, int64_t n_cols, int64_t nnz, const int64
   L->n_cols = n_cols;
   L->nnz_input = nnz;
   L->reordered = !(flags & WG_FLAG_NO_REORDER);
+  L->values_null = (values == nullptr);
   int rc = build_operator(L, indptr, indices, values, w_cols, /*raw=*/false, as_stream(stream_));
   if (rc == WG_OK && !(flags & WG_FLAG_KEEP_COLUMN_ORDER)) rc = sort_row_columns(L, as_stream(stream_));
   if (rc != WG_OK) {

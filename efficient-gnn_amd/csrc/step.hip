@@ -1456,12 +1456,29 @@ int get_row_split(wg_laplacian_s* L, const int32_t** out) {
   return WG_OK;
 }
 
+namespace {
+// mean 128-B cache lines one gathered row of W floats spans (rows back to back from a
+// 256-B aligned base; the offsets mod 128 repeat with period <= 32 rows)
+double lines_per_row(int64_t W) {
+  int64_t tot = 0;
+  for (int64_t i = 0; i < 32; ++i) {
+    const int64_t o = (4 * W * i) % 128;
+    tot += (o + 4 * W + 127) / 128;
+  }
+  return tot / 32.0;
+}
+}  // namespace
+
 int padded_features(const wg_laplacian_s* L, int64_t F) {
   if (F < 3) return (int)F;
-  // knob fpad: round the width up to a multiple of 4 (default: float4 lanes) or of 8 / 16
-  // (F = 44 -> 48: a 192-B row at 64-B alignment spans 2 cache lines, a 176-B row 2.25 on average)
-  const int64_t m = (L && (L->tune.fpad == 8 || L->tune.fpad == 16)) ? L->tune.fpad : 4;
-  return (int)((F + m - 1) / m * m);
+  const int64_t f4 = (F + 3) / 4 * 4;
+  const int knob = L ? L->tune.fpad : 0;
+  if (knob == 4 || knob == 8 || knob == 16) return (int)((F + knob - 1) / knob * knob);
+  // auto: the width (a multiple of 4, or of 8) whose rows span the fewest cache lines -- the
+  // step kernel is bound by gathered-line requests: F = 44 -> 48 (2.25 -> 2
+  // lines per row; Reddit-size F=41 1504 -> 1422 us per step, profiles/r02/s6), F = 40 stays 40
+  const int64_t f8 = (F + 7) / 8 * 8;
+  return (int)(lines_per_row(f8) < lines_per_row(f4) - 1e-9 ? f8 : f4);
 }
 
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream) {
