@@ -82,6 +82,8 @@ def parse():
                          "as 'sharded' (first) and 'sharded_<config>' objects of the line; 'none' to skip.  At N > 1 "
                          "the --scale-config run is the headline and is not repeated here")
     ap.add_argument("--sharded-steps", type=int, default=5)
+    ap.add_argument("--headline-timeout", type=float, default=900.0,
+                    help="N > 1: seconds the row-sharded headline may take before an error line is printed")
     ap.add_argument("--sharded-timeout", type=float, default=420.0,
                     help="seconds the extras may take before the line is printed without the unfinished ones")
     ap.add_argument("--exchange", default="rccl,ipc",
@@ -629,10 +631,26 @@ def main():
 
     line = None
     if mode == "sharded":
-        # the N > 1 headline: one graph row-sharded over every rank (strong scaling)
+        # the N > 1 headline: one graph row-sharded over every rank (strong scaling).  A
+        # collective that never completes must not cost the whole line: a watchdog prints
+        # an error line and ends the process after --headline-timeout seconds.
+        import threading
         cfg = args.scale_config if args.mode == "auto" else args.config
+
+        def _expire_headline():
+            if rank == 0:
+                _emit({"metric": f"Chebyshev SpMM-chain edges*K/s ({cfg}-size, row-sharded over {world} GPUs)",
+                       "value": None, "unit": "edges*K/s", "n_gpus": world, "steps": args.steps,
+                       "warmup": args.warmup, "higher_is_better": True, "scaling": "strong",
+                       "error": f"the row-sharded headline did not finish within {args.headline_timeout:.0f} s"},
+                      args.out)
+            os._exit(3)
+        hw = threading.Timer(args.headline_timeout, _expire_headline)
+        hw.daemon = True
+        hw.start()
         line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
                            exchanges[0], median_reps=max(20, args.steps))
+        hw.cancel()
         line["metric"] = (f"Chebyshev SpMM-chain edges*K/s ({cfg}-size, K={line['config']['K']}, F="
                           f"{line['config']['F']}, row-sharded over {world} GPUs)")
         line["headline_note"] = ("N > 1 headline: BASELINE.json configs[3] (Reddit-size, 1-D row-sharded, RCCL "

@@ -348,7 +348,8 @@ struct wg_dist_s {
     const bool clen = !lp && L->tune.clenshaw && K >= 1;
     // two-phase steps overlapping the exchange (gather-kernel path, rows column-sorted, peers present)
     const int32_t* rsplit = nullptr;
-    if (!lp && L->tune.overlap && world > 1 && n_own > 0 && K >= 1)
+    // (any halo: at world 1 too -- the one-GPU loopback test exercises the overlapped RCCL path)
+    if (!lp && L->tune.overlap && n_halo > 0 && (comm || ipc) && n_own > 0 && K >= 1)
       if (int rc = get_row_split(L, &rsplit)) return rc;
     overlapped = rsplit != nullptr;
     const size_t partf = rsplit ? 2 * own : 0;  // float64 row partials (n_own x Fp doubles)

@@ -301,6 +301,10 @@ def test_native_chain_loopback_exchange(F, lds, graph):
         for r in res:
             assert np.array_equal(r, res[0])
         assert_parity(res[0], ref["S"], what=f"loopback F={F} lds={lds} graph={graph}")
+        info = (ctypes.c_int64 * 8)()
+        check(lib.wg_dist_info(h, info), "dist_info")
+        # the gather-kernel path overlaps the RCCL exchange with the own-column half of each step
+        assert info[0] == (1 if (F > 1 or lds == 0) else 0), list(info)
         L.profile_enable(True)
         check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")
         tot, cnt = ctypes.c_double(0), ctypes.c_int64(0)
