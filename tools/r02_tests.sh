@@ -17,7 +17,7 @@ for grp in ${TEST_GROUPS:-main fullsize}; do
   case $grp in
     main) run main 700 tests -m gpu --ignore=tests/test_fullsize.py ;;
     fullsize) run fullsize 700 tests/test_fullsize.py -m gpu ;;
-    *) run "$grp" 600 $grp -m gpu ;;
+    *) run "$(echo "$grp" | tr '/.:' '___')" 600 $grp -m gpu ;;
   esac
 done
 echo done
