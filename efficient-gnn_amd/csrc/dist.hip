@@ -305,9 +305,11 @@ struct wg_dist_s {
   }
 
   // One Chebyshev step that gathers from `cur` (own rows final, halo rows to be
-  // refreshed): without overlap, exchange then the step; with overlap, the
-  // exchange forks onto xs while phase 1 (own-column entries, into `part`) runs
-  // on st; st joins the exchange, then phase 2 (halo entries + part, epilogue).
+  // refreshed): without overlap, exchange then the step; with overlap, phase 1
+  // (own-column entries, into `part`) forks onto xs while the exchange runs on
+  // st; st joins phase 1, then phase 2 (halo entries + part, epilogue).  The
+  // exchange stays on st, the stream a captured chain is recorded on (RCCL
+  // under a capture joined by a side stream crashed in the one-GPU loopback).
   // Hazards: the exchange writes only cur's halo rows and reads its own rows;
   // phase 1 reads only own rows; it forks after every earlier kernel on st (the
   // previous step wrote cur's own rows and last read the other buffer's halo).
@@ -318,15 +320,15 @@ struct wg_dist_s {
       if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
       return launch(st, nullptr);
     }
-    WG_HIP_TRY(hipEventRecord(xfork, st));
-    WG_HIP_TRY(hipStreamWaitEvent(xs, xfork, 0));
-    if (int rc = exchange(cur, sendbuf, Fp, xs, slot)) return rc;
-    WG_HIP_TRY(hipEventRecord(xjoin, xs));
     PhaseArgs p1;
     p1.phase = 1;
     p1.rsplit = rsplit;
     p1.part = part;
-    if (int rc = launch(st, &p1)) return rc;
+    WG_HIP_TRY(hipEventRecord(xfork, st));
+    WG_HIP_TRY(hipStreamWaitEvent(xs, xfork, 0));
+    if (int rc = launch(xs, &p1)) return rc;
+    WG_HIP_TRY(hipEventRecord(xjoin, xs));
+    if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
     WG_HIP_TRY(hipStreamWaitEvent(st, xjoin, 0));
     PhaseArgs p2 = p1;
     p2.phase = 2;
