@@ -648,8 +648,18 @@ def main():
         hw = threading.Timer(args.headline_timeout, _expire_headline)
         hw.daemon = True
         hw.start()
-        line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
-                           exchanges[0], median_reps=max(20, args.steps))
+        try:
+            line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
+                               exchanges[0], median_reps=max(20, args.steps))
+        except Exception as exc:  # noqa: BLE001 -- keep a headline: the next exchange, noted in the line
+            if len(exchanges) < 2:
+                raise
+            _log(f"headline with exchange {exchanges[0]} failed ({type(exc).__name__}: {exc}); using {exchanges[1]}")
+            torch.cuda.empty_cache()
+            line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
+                               exchanges[1], median_reps=max(20, args.steps))
+            line["headline_fallback"] = f"exchange {exchanges[0]} failed: {type(exc).__name__}: {exc}"
+            exchanges = exchanges[1:] + exchanges[:1]
         hw.cancel()
         line["metric"] = (f"Chebyshev SpMM-chain edges*K/s ({cfg}-size, K={line['config']['K']}, F="
                           f"{line['config']['F']}, row-sharded over {world} GPUs)")
