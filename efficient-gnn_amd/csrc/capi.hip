@@ -172,6 +172,21 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   return WG_OK;
 }
 
+int wg_laplacian_set_halo_groups(wg_laplacian_t L, int32_t n_groups, const int64_t* offsets) {
+  if (!L || n_groups < 0 || (n_groups > 0 && !offsets))
+    return fail(WG_ERR_INVALID, "wg_laplacian_set_halo_groups: bad arguments");
+  if (n_groups > 0 && (offsets[0] != 0 || offsets[n_groups] != L->n_cols - L->n_rows))
+    return fail(WG_ERR_INVALID, "wg_laplacian_set_halo_groups: offsets must run from 0 to the halo size %lld",
+                (long long)(L->n_cols - L->n_rows));
+  for (int32_t q = 0; q < n_groups; ++q)
+    if (offsets[q + 1] < offsets[q]) return fail(WG_ERR_INVALID, "wg_laplacian_set_halo_groups: offsets decrease");
+  WG_HIP_TRY(hipDeviceSynchronize());
+  if (n_groups > 0) L->halo_off.assign(offsets, offsets + n_groups + 1);
+  else L->halo_off.clear();
+  release_lds1(L);
+  return WG_OK;
+}
+
 const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
   g_text.clear();
   if (!L || F < 1) return "";

@@ -494,6 +494,12 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
   }
   D->n_send = D->send_off[world];
   D->n_halo = D->recv_off[world];
+  if (D->n_halo > 0 && D->n_own + D->n_halo == L->n_cols) {
+    // the halo groups (one per peer, each in descending degree: wats_hip/dist.py) for the F = 1
+    // hub plan of a shard; plans built before this point are dropped
+    L->halo_off.assign(D->recv_off.begin(), D->recv_off.end());
+    release_lds1(L);
+  }
   if (D->n_own + D->n_halo != D->n_cols || (D->n_send > 0 && !send_rows)) {
     const long long nh = (long long)D->n_halo, nc = (long long)D->n_cols, no = (long long)D->n_own;
     delete D;

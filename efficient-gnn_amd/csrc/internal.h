@@ -108,6 +108,13 @@ struct Lds1Plan {
   int32_t* pos = nullptr;     // device [nb * n]: segment id of (block, row), -1 if empty
   int4* wdesc = nullptr;      // device [n_wg * 16]: {first chunk, end chunk, first segment, 0}
   int32_t* wblock = nullptr;  // device [n_wg]: column block of each workgroup
+  // mode 4 on a row shard: the hub is the highest-degree columns of the own range and of
+  // each peer's halo group (prefixes: each is degree-ordered), staged from n_hranges
+  // ranges; the kernel reads remapped columns hcol (hub column -> its LDS slot, any
+  // other column c -> c + hub, gathered from u[c])
+  int32_t* hcol = nullptr;    // device [nnz + 4]
+  int4* hranges = nullptr;    // device [n_hranges]: {u begin, LDS slot begin, length, 0}
+  int32_t n_hranges = 0;
   std::string text;
   void release();
   // floats of the gather vector u the kernel reads (padded column space)
@@ -176,6 +183,8 @@ struct wg_laplacian_s {
                               // graph agrees, so a row-sharded chain may exchange u = b * dinv)
   double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
   int32_t* rsplit = nullptr;  // [n_rows] first halo entry of each row (two-phase steps), lazily built
+  std::vector<int64_t> halo_off;  // row shard: halo columns [n_rows + halo_off[q], n_rows + halo_off[q+1])
+                                  // come from peer q, each group in descending degree (wg_dist_create)
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
   bool lds1_failed[2] = {false, false};        // not applicable (too many blocks): use the gather kernel
   // workspace for wg_wavelet_features

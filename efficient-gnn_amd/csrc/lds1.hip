@@ -47,9 +47,12 @@ constexpr int kLdsThreads = 1024;
 struct Lds1Args {
   const int32_t* brp;
   const uint16_t* bcol;
-  const int32_t* gcol;  // mode 4: the operator's int32 columns (internal, sorted per row)
+  const int32_t* gcol;  // mode 4: the operator's int32 columns (internal, sorted per row), or a shard's remapped ones
   int32_t hub;          // mode 4: columns [0, hub) staged in LDS, LDS slot hub = 0
   int32_t u_bytes;      // mode 4: extent of u_in (raw-buffer gathers of the tail columns)
+  int32_t gshift;       // mode 4: a tail column c (>= hub) is gathered from u[c - gshift] (0, or hub on a shard)
+  int32_t n_hranges;    // mode 4 on a shard: LDS slots filled from these ranges of u (0: slots = u[0, hub))
+  const int4* hranges;
   const int2* groups;
   const int4* wgs;
   const float* u_in;   // u_{k-1}, n_cols (padded to a multiple of 32)
@@ -165,10 +168,16 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   constexpr uint32_t kDrop = 0x80000000u;
   const int4 d = a.wgs[blockIdx.x];
   const int H = a.hub;
-  {
+  if (a.n_hranges == 0) {
     const float4* src = reinterpret_cast<const float4*>(a.u_in);
     float4* dst = reinterpret_cast<float4*>(g_u_lds);
     for (int i = threadIdx.x; i < H / 4; i += kLdsThreads) dst[i] = src[i];
+    if (threadIdx.x < 32) g_u_lds[H + threadIdx.x] = 0.0f;
+  } else {  // a shard's hub: its own top columns and each peer group's top columns
+    for (int r = 0; r < a.n_hranges; ++r) {
+      const int4 hr = a.hranges[r];
+      for (int i = threadIdx.x; i < hr.z; i += kLdsThreads) g_u_lds[hr.y + i] = a.u_in[(int64_t)hr.x + i];
+    }
     if (threadIdx.x < 32) g_u_lds[H + threadIdx.x] = 0.0f;
   }
   if (threadIdx.x == 0) s_next = d.y;
@@ -179,9 +188,10 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   const float* __restrict__ u = g_u_lds;
   const int32_t* __restrict__ col = a.gcol;
   const int32_t* __restrict__ rp = a.brp;
+  const int32_t gs = a.gshift;
   auto x_of = [&](int32_t c) {
     const float xl = u[min(c, H)];
-    const uint32_t off = c >= H ? (uint32_t)c * 4u : kDrop;
+    const uint32_t off = c >= H ? (uint32_t)(c - gs) * 4u : kDrop;
     const float xg = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
     return xl + xg;
   };
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
         for (int j = 0; j < 4; ++j) {
           const bool ok = qq + j >= e0 && qq + j < e1;
           const float xl = u[ok ? min(cc[j], H) : H];
-          const uint32_t off = (ok && cc[j] >= H) ? (uint32_t)cc[j] * 4u : kDrop;
+          const uint32_t off = (ok && cc[j] >= H) ? (uint32_t)(cc[j] - gs) * 4u : kDrop;
           x[j] = xl + __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
         }
 #pragma unroll
@@ -233,6 +243,32 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   }
 }
 
+
+// a row shard's hub plan: column c -> its LDS slot when it is a hub column, else c + hub.
+// g (device, 3 * ng + 1 ints): [0, ng] halo group offsets, [ng + 1, 2 ng] hub length per
+// group, [2 ng + 1, 3 ng] first slot per group.
+__global__ void hub_remap_kernel(int64_t nnz, int32_t n_own, int32_t h1, int32_t hub, int32_t ng,
+                                 const int32_t* __restrict__ g, const int32_t* __restrict__ col,
+                                 int32_t* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  const int32_t c = col[e];
+  int32_t slot = -1;
+  if (c < n_own) {
+    slot = c < h1 ? c : -1;
+  } else {
+    const int32_t h = c - n_own;
+    int lo = 0, hi = ng;  // group q with g[q] <= h < g[q + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (g[mid] <= h) lo = mid;
+      else hi = mid;
+    }
+    const int32_t idx = h - g[lo];
+    slot = idx < g[ng + 1 + lo] ? g[2 * ng + 1 + lo] + idx : -1;
+  }
+  out[e] = slot >= 0 ? slot : c + hub;
+}
 
 __global__ __launch_bounds__(256) void combine_lds1_kernel(Lds1Args a) {
   const int32_t row = blockIdx.x * 256 + threadIdx.x;
@@ -857,8 +893,11 @@ int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cn
 
 void Lds1Plan::release() {
   for (void* p : {(void*)brp, (void*)bcol, (void*)groups, (void*)wgs, (void*)part, (void*)chunk, (void*)pos,
-                  (void*)wdesc, (void*)wblock})
+                  (void*)wdesc, (void*)wblock, (void*)hcol, (void*)hranges})
     (void)hipFree(p);
+  hcol = nullptr;
+  hranges = nullptr;
+  n_hranges = 0;
   chunk = nullptr;
   pos = nullptr;
   wdesc = nullptr;
@@ -879,6 +918,66 @@ void release_lds1(wg_laplacian_s* L) {
     }
     L->lds1_failed[i] = false;
   }
+}
+
+// A row shard's hub: the p->hub highest-degree columns among the own columns
+// [0, n_rows) and each peer's halo group, each of which is a descending-degree
+// list, so the choice is a prefix of each; LDS slots own prefix first, then the
+// groups in peer order.  Builds the remapped column array the kernel reads.
+static int build_shard_hub(wg_laplacian_s* L, Lds1Plan* p, int32_t nnz) {
+  const int64_t n_own = L->n_rows, n_cols = L->n_cols;
+  const int ng = (int)L->halo_off.size() - 1;
+  const int64_t hmax = p->hub;
+  std::vector<double> dinv(n_cols);
+  WG_HIP_TRY(hipMemcpy(dinv.data(), L->dinv, sizeof(double) * n_cols, hipMemcpyDeviceToHost));
+  // candidates: the first hmax of each list, by degree w = 1 / dinv^2 (largest first)
+  std::vector<std::pair<double, int>> cand;  // (dinv: smaller = higher degree, list)
+  auto add_list = [&](int64_t b, int64_t e, int id) {
+    for (int64_t i = b; i < std::min(e, b + hmax); ++i) cand.push_back({dinv[i], id});
+  };
+  add_list(0, n_own, 0);
+  for (int q = 0; q < ng; ++q) add_list(n_own + L->halo_off[q], n_own + L->halo_off[q + 1], q + 1);
+  const int64_t take = std::min<int64_t>(hmax, (int64_t)cand.size());
+  std::nth_element(cand.begin(), cand.begin() + std::max<int64_t>(take - 1, 0), cand.end(),
+                   [](const std::pair<double, int>& x, const std::pair<double, int>& y) { return x.first < y.first; });
+  std::vector<int32_t> cnt(ng + 1, 0);
+  for (int64_t i = 0; i < take; ++i) ++cnt[cand[i].second];
+  // slots: own prefix, then each group's prefix
+  std::vector<int4> ranges;
+  std::vector<int32_t> g(3 * ng + 1, 0);
+  int32_t slot = 0;
+  if (cnt[0] > 0) ranges.push_back(make_int4(0, 0, cnt[0], 0));
+  slot = cnt[0];
+  for (int q = 0; q < ng; ++q) {
+    g[q] = (int32_t)L->halo_off[q];
+    g[ng + 1 + q] = cnt[q + 1];
+    g[2 * ng + 1 + q] = slot;
+    if (cnt[q + 1] > 0) ranges.push_back(make_int4((int)(n_own + L->halo_off[q]), slot, cnt[q + 1], 0));
+    slot += cnt[q + 1];
+  }
+  g[ng] = (int32_t)L->halo_off[ng];
+  p->hub = slot;
+  p->lchunks = slot / 32 + 2;  // + the zero slots (32 at slot `hub`)
+  p->n_hranges = (int32_t)ranges.size();
+  if (int rc = dmalloc(&p->hranges, std::max<size_t>(1, ranges.size()))) return rc;
+  if (!ranges.empty())
+    WG_HIP_TRY(hipMemcpy(p->hranges, ranges.data(), sizeof(int4) * ranges.size(), hipMemcpyHostToDevice));
+  int32_t* gd = nullptr;
+  if (int rc = dmalloc(&gd, g.size())) return rc;
+  WG_HIP_TRY(hipMemcpy(gd, g.data(), sizeof(int32_t) * g.size(), hipMemcpyHostToDevice));
+  if (int rc = dmalloc(&p->hcol, (size_t)nnz + 4)) {
+    (void)hipFree(gd);
+    return rc;
+  }
+  WG_HIP_TRY(hipMemset(p->hcol + nnz, 0, 4 * sizeof(int32_t)));
+  if (nnz > 0)
+    hipLaunchKernelGGL(hub_remap_kernel, dim3((unsigned)ceil_div(nnz, 256)), dim3(256), 0, 0, (int64_t)nnz,
+                       (int32_t)n_own, cnt[0], p->hub, ng, gd, L->col, p->hcol);
+  const hipError_t e1 = hipGetLastError();
+  const hipError_t e2 = hipDeviceSynchronize();
+  (void)hipFree(gd);
+  if (e1 != hipSuccess || e2 != hipSuccess) return fail(WG_ERR_HIP, "hub_remap: %s", hipGetErrorString(e1 ? e1 : e2));
+  return WG_OK;
 }
 
 int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
@@ -909,9 +1008,9 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
       mode = 1;
     } else if (n > 0 && nnz_rows / n >= 64) {
       mode = 2;
-    } else if (hub_auto >= 16384 && L->n_cols == L->n_rows) {
-      // (row shards: the hub would be the shard's own highest-degree columns, but most
-      // gathers go to halo columns, which are not degree-ordered -> gather kernel)
+    } else if (hub_auto >= 16384 && (L->n_cols == L->n_rows || !L->halo_off.empty())) {
+      // (a row shard's hub mixes its own top columns with each peer's: the halo groups are
+      // degree-ordered by the plan, wg_dist_create hands over their offsets)
       mode = 4;
       hub = (int32_t)hub_auto;
     } else {
@@ -936,15 +1035,16 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
     p->ulen = cols32;
     std::vector<int32_t> h(n + 1);
     WG_HIP_TRY(hipMemcpy(h.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
-    const int rc = build_groups(L, p, h, 1, L->tune.hub_iter);
+    int rc = build_groups(L, p, h, 1, L->tune.hub_iter);
+    if (!rc && L->n_cols > L->n_rows && !L->halo_off.empty() && !active_only) rc = build_shard_hub(L, p, nnz_rows);
     if (rc) {
       p->release();
       delete p;
       return rc;
     }
     char buf[256];
-    snprintf(buf, sizeof(buf), "lds1: hub teams rows=%lld cols=%lld nnz=%d hub=%d groups=%d workgroups=%d\n",
-             (long long)n, (long long)n_cols, nnz_rows, p->hub, p->n_groups, p->n_wg);
+    snprintf(buf, sizeof(buf), "lds1: hub teams rows=%lld cols=%lld nnz=%d hub=%d groups=%d workgroups=%d ranges=%d\n",
+             (long long)n, (long long)n_cols, nnz_rows, p->hub, p->n_groups, p->n_wg, p->n_hranges);
     p->text = buf;
     L->lds1[slot] = p;
     *out = p;
@@ -1059,9 +1159,12 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
       attr4[vx] = true;
     }
     a.brp = L->rowptr;
-    a.gcol = L->col;
+    a.gcol = p->hcol ? p->hcol : L->col;
     a.hub = p->hub;
     a.u_bytes = (int32_t)(p->ulen * 4);
+    a.gshift = p->hcol ? p->hub : 0;
+    a.n_hranges = p->n_hranges;
+    a.hranges = p->hranges;
     if (vx) hipLaunchKernelGGL(cheb_hub1_kernel<true>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
     else hipLaunchKernelGGL(cheb_hub1_kernel<false>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
     WG_LAUNCH_CHECK();

@@ -121,11 +121,15 @@ def exchange_int_lists(lists: list, group=None) -> list:
 
 
 def build_halo_plan(indptr_local: np.ndarray, indices_global, bounds: np.ndarray, group=None,
-                    compute_device=None) -> HaloPlan:
+                    compute_device=None, col_degree=None) -> HaloPlan:
     """Renumber this rank's CSR columns to [own | halo] and agree with every
-    peer on who sends which rows (collective).  The column work (unique,
-    searchsorted over nnz entries) runs with torch on ``compute_device`` (the
-    GPU for large shards; default CPU)."""
+    peer on who sends which rows (collective).  The halo is grouped by owner
+    rank; with ``col_degree`` (the global column degree, indexed by global
+    id) each group is in descending degree (ties by id), so the highest-degree
+    halo columns of every peer are a prefix of its group -- the F = 1 hub
+    kernel stages those prefixes in LDS (csrc/lds1.hip, build_shard_hub).
+    The column work (unique, searchsorted over nnz entries) runs with torch on
+    ``compute_device`` (the GPU for large shards; default CPU)."""
     rank, world = _rank_world(group)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
     dev = torch.device(compute_device) if compute_device is not None else torch.device("cpu")
@@ -136,9 +140,18 @@ def build_halo_plan(indptr_local: np.ndarray, indices_global, bounds: np.ndarray
     halo_t = torch.unique(remote, sorted=True)
     n_own = r1 - r0
     local = cols - r0
-    local[~own] = n_own + torch.searchsorted(halo_t, remote)
-    halo_global = halo_t.cpu().numpy()
-    owner = np.searchsorted(bounds, halo_global, side="right") - 1
+    halo_sorted = halo_t.cpu().numpy()
+    owner_sorted = np.searchsorted(bounds, halo_sorted, side="right") - 1
+    if col_degree is not None and halo_sorted.size:
+        deg = np.asarray(col_degree.cpu().numpy() if isinstance(col_degree, torch.Tensor) else col_degree)
+        order = np.lexsort((halo_sorted, -deg[halo_sorted].astype(np.float64), owner_sorted))
+    else:
+        order = np.arange(halo_sorted.size)
+    rank_of = np.empty(halo_sorted.size, np.int64)   # position in the halo of the id at sorted position i
+    rank_of[order] = np.arange(halo_sorted.size)
+    local[~own] = n_own + torch.from_numpy(rank_of).to(dev)[torch.searchsorted(halo_t, remote)]
+    halo_global = halo_sorted[order]
+    owner = owner_sorted[order]
     recv_lists = [halo_global[owner == q] for q in range(world)]
     requested = exchange_int_lists(recv_lists, group) if world > 1 else recv_lists  # what each peer needs from us
     send_rows = np.concatenate(requested).astype(np.int64) - r0 if world else np.zeros(0, np.int64)
@@ -173,10 +186,10 @@ def gather_rows(X_local: torch.Tensor, bounds: np.ndarray, group=None) -> torch.
     return out.to(X_local.device)
 
 
-def global_column_degree(partial_colsum: torch.Tensor, partial_diag: torch.Tensor, plan: HaloPlan,
-                         group=None) -> torch.Tensor:
-    """``w = colsum(A) - diag(A)`` for the columns [own | halo] of this rank:
-    all-reduce the float64 partial sums, then scipy's float32 subtraction."""
+def allreduce_column_degree(partial_colsum: torch.Tensor, partial_diag: torch.Tensor, group=None) -> torch.Tensor:
+    """``w = colsum(A) - diag(A)`` for every global column: all-reduce the
+    float64 partial sums of the shards, then scipy's float32 subtraction
+    (``_laplacian.py:467``)."""
     world = _rank_world(group)[1]
     dev = _device_for(group) if world > 1 else partial_colsum.device
     cs = partial_colsum.to(dev, torch.float64)
@@ -184,8 +197,20 @@ def global_column_degree(partial_colsum: torch.Tensor, partial_diag: torch.Tenso
     if world > 1:
         dist.all_reduce(cs, group=group)
         dist.all_reduce(dg, group=group)
-    ids = torch.from_numpy(np.concatenate([np.arange(plan.r0, plan.r1), plan.halo_global]).astype(np.int64)).to(dev)
-    return cs[ids].to(torch.float32) - dg[ids].to(torch.float32)
+    return cs.to(torch.float32) - dg.to(torch.float32)
+
+
+def plan_column_degree(w_global: torch.Tensor, plan: HaloPlan) -> torch.Tensor:
+    """The global column degree at this rank's columns [own | halo]."""
+    ids = torch.from_numpy(np.concatenate([np.arange(plan.r0, plan.r1), plan.halo_global]).astype(np.int64))
+    return w_global[ids.to(w_global.device)]
+
+
+def global_column_degree(partial_colsum: torch.Tensor, partial_diag: torch.Tensor, plan: HaloPlan,
+                         group=None) -> torch.Tensor:
+    """``w = colsum(A) - diag(A)`` for the columns [own | halo] of this rank:
+    all-reduce the float64 partial sums, then scipy's float32 subtraction."""
+    return plan_column_degree(allreduce_column_degree(partial_colsum, partial_diag, group), plan)
 
 
 def halo_exchange(ext: torch.Tensor, plan: HaloPlan, pack, sendbuf: torch.Tensor, group=None,
@@ -230,11 +255,11 @@ class ShardedWavelet:
         self.group = group
         self.exchange = exchange
         indptr_local = np.asarray(indptr_local, np.int64)
-        _trace("halo plan")
-        self.plan = build_halo_plan(indptr_local, indices_global, bounds, group, compute_device=self.device)
-        p = self.plan
-        _trace(f"halo plan done ({p.n_halo} halo rows); column degrees")
-        # partial column degrees of this shard, on the GPU (float64 atomics)
+        rank, world = _rank_world(group)
+        r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+        _trace("column degrees")
+        # partial column degrees of this shard, on the GPU (float64 atomics), all-reduced:
+        # the halo plan orders each peer's group by this degree (the F = 1 hub kernel)
         lib = _lib.load()
         ip = torch.from_numpy(indptr_local).to(self.device)
         ix = torch.from_numpy(np.asarray(indices_global, np.int32)).to(self.device)
@@ -243,11 +268,17 @@ class ShardedWavelet:
         diag = torch.zeros(n_global, dtype=torch.float64, device=self.device)
         with torch.cuda.device(self.device):
             st = torch.cuda.current_stream(self.device).cuda_stream
-            check(lib.wg_column_degree(p.n_own, p.r0, ptr(ip), ptr(ix) if ix.numel() else None, ptr(vals),
+            check(lib.wg_column_degree(r1 - r0, r0, ptr(ip), ptr(ix) if ix.numel() else None, ptr(vals),
                                        ptr(colsum), ptr(diag), st), "column_degree")
-        w_cols = global_column_degree(colsum, diag, p, group).to(self.device)
+        w_global = allreduce_column_degree(colsum, diag, group)
         del colsum, diag
-        _trace("column degrees done; operator")
+        _trace("column degrees done; halo plan")
+        self.plan = build_halo_plan(indptr_local, indices_global, bounds, group, compute_device=self.device,
+                                    col_degree=w_global)
+        p = self.plan
+        w_cols = plan_column_degree(w_global, p).to(self.device)
+        del w_global
+        _trace(f"halo plan done ({p.n_halo} halo rows); operator")
         self.L = NormalizedLaplacian(p.n_own, ip, torch.from_numpy(p.local_indices), vals, n_cols=p.n_cols,
                                      w_cols=w_cols, device=self.device)
         _trace("operator done")

@@ -209,6 +209,13 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
  * efficient-gnn_amd/csrc/internal.h (struct Tuning).  Plan-shaping keys are
  * synchronous (they drop cached plans); launch-time keys are not. */
 int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value);
+/* Row shards: the halo columns [n_rows + offsets[q], n_rows + offsets[q+1])
+ * come from peer q (q < n_groups; offsets[0] = 0, offsets[n_groups] = halo
+ * size), each group in descending degree.  Lets the F = 1 hub kernel stage
+ * the top columns of the own range and of every group in LDS.
+ * wg_dist_create sets it from the receive counts; synchronous; drops the F = 1
+ * plans built so far.  n_groups = 0 clears it. */
+int wg_laplacian_set_halo_groups(wg_laplacian_t L, int32_t n_groups, const int64_t* offsets_host);
 /* Human-readable launch plan of the step kernel for an F-column signal
  * (thread-local string, valid until the next call on this thread). */
 const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F);

@@ -55,7 +55,15 @@ def _cpu_worker(rank, world, port, kind, K, F, q):
         indptr_l = g.indptr[r0:r1 + 1] - lo
         cols_g = g.indices[lo:hi]
         vals_l = None if g.values is None else g.values[lo:hi]
-        plan = build_halo_plan(indptr_l, cols_g, bounds, None)
+        # rmat: the halo groups in descending global degree (what ShardedWavelet passes)
+        col_degree = np.bincount(g.indices, minlength=g.n) if kind == "rmat" else None
+        plan = build_halo_plan(indptr_l, cols_g, bounds, None, col_degree=col_degree)
+        if col_degree is not None:
+            owner = np.searchsorted(bounds, plan.halo_global, side="right") - 1
+            assert np.all(np.diff(owner) >= 0), "halo not grouped by owner"
+            for peer in range(world):
+                dq = col_degree[plan.halo_global[owner == peer]]
+                assert np.all(np.diff(dq) <= 0), "halo group not in descending degree"
         # partial column degrees of this shard (the GPU path does this with wg_column_degree)
         cs = np.zeros(g.n)
         dg = np.zeros(g.n)
@@ -135,7 +143,9 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host"):
         sw = ShardedWavelet(g.indptr[r0:r1 + 1] - lo, g.indices[lo:hi],
                             None if g.values is None else g.values[lo:hi], g.n, bounds, exchange=exchange,
                             device="cuda:0")
-        sw.L.tune(lds=lds)
+        # lds 4 (hub teams) with a 256-column hub: the shard's hub mixes its own top columns
+        # with every peer group's (halo groups in descending degree), the rest is gathered
+        sw.L.tune(lds=lds, **({"lds_cb": 256} if lds == 4 else {}))
         q_path = "u" if (F == 1 and sw.u_len() > 0) else "t"
         rng = np.random.default_rng(0)
         X = rng.standard_normal((g.n, F)).astype(np.float32)

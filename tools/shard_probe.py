@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--lds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--groups", type=int, default=1, help="hand the degree-ordered halo groups to the handle "
+                                                          "(the F = 1 hub kernel applies to the shard)")
     ap.add_argument("--grid", default="", help="';'-separated knob sets to time, e.g. 'lds_wg=64;lds_wg=128,lds_k=2'")
     a = ap.parse_args()
     n, nnz_t, K, _ = NAMED_CONFIGS[a.config]
@@ -38,14 +40,27 @@ def main():
     b = partition_rows(indptr, a.world)
     r0, r1 = int(b[a.rank]), int(b[a.rank + 1])
     cols = ix[int(indptr[r0]):int(indptr[r1])].to(torch.int64)
+    # the shard as wats_hip.dist builds it: [own | halo], halo grouped by owner, each group in
+    # descending degree (build_halo_plan with col_degree), group offsets handed to the handle
+    plan_bounds = np.asarray(b)
     own = (cols >= r0) & (cols < r1)
-    halo = torch.unique(cols[~own], sorted=True)
+    halo_sorted = torch.unique(cols[~own], sorted=True).cpu().numpy()
+    owner_sorted = np.searchsorted(plan_bounds, halo_sorted, side="right") - 1
+    order = np.lexsort((halo_sorted, -deg[halo_sorted].astype(np.float64), owner_sorted))
+    rank_of = np.empty(halo_sorted.size, np.int64)
+    rank_of[order] = np.arange(halo_sorted.size)
     local = cols - r0
-    local[~own] = (r1 - r0) + torch.searchsorted(halo, cols[~own])
-    n_own, n_cols = r1 - r0, (r1 - r0) + int(halo.numel())
-    w = torch.from_numpy(np.concatenate([deg[r0:r1], deg[halo.cpu().numpy()]]))
+    local[~own] = (r1 - r0) + torch.from_numpy(rank_of).to(dev)[
+        torch.searchsorted(torch.from_numpy(halo_sorted).to(dev), cols[~own])]
+    halo = halo_sorted[order]
+    counts = np.bincount(owner_sorted[order], minlength=a.world)
+    n_own, n_cols = r1 - r0, (r1 - r0) + int(halo.size)
+    w = torch.from_numpy(np.concatenate([deg[r0:r1], deg[halo]]))
     L = wats_hip.NormalizedLaplacian(n_own, torch.from_numpy(indptr[r0:r1 + 1] - indptr[r0]),
                                      local.to(torch.int32), None, n_cols=n_cols, w_cols=w, device=dev)
+    if a.groups and a.world > 1:
+        offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        check(_lib.load().wg_laplacian_set_halo_groups(L.handle, a.world, offs.ctypes.data), "set_halo_groups")
     del ip, ix, cols, local
     lib = _lib.load()
     for knobs in (a.grid.split(";") if a.grid else [""]):
