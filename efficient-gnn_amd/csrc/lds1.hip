@@ -1008,9 +1008,12 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
       mode = 1;
     } else if (n > 0 && nnz_rows / n >= 64) {
       mode = 2;
-    } else if (hub_auto >= 16384 && (L->n_cols == L->n_rows || !L->halo_off.empty())) {
-      // (a row shard's hub mixes its own top columns with each peer's: the halo groups are
-      // degree-ordered by the plan, wg_dist_create hands over their offsets)
+    } else if (hub_auto >= 16384 && L->n_cols == L->n_rows) {
+      // Row shards take the gather kernel.  Their halo groups are in descending degree
+      // (wats_hip/dist.py), so the hot columns sit in few cache lines and the gather kernel
+      // reads them from L2: 8M R-MAT 8-way shard 211 us per step vs 282 us with the hub
+      // kernel staging the shard's own + every group's top columns (lds = 4, ranged hub);
+      // 4-way 425 vs 767, 2-way 822 vs 837 (profiles/r02/s10_shard_probe_8m.log)
       mode = 4;
       hub = (int32_t)hub_auto;
     } else {
