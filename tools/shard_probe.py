@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--lds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--F", type=int, default=1, help="signal width (F > 1: the gather kernel at this width)")
     ap.add_argument("--groups", type=int, default=1, help="hand the degree-ordered halo groups to the handle "
                                                           "(the F = 1 hub kernel applies to the shard)")
     ap.add_argument("--grid", default="", help="';'-separated knob sets to time, e.g. 'lds_wg=64;lds_wg=128,lds_k=2'")
@@ -77,7 +78,13 @@ def probe(L, lib, n_own, n_cols, K, a, dev, kv):
     print(f"shard {a.rank}/{a.world}: rows {n_own}, cols {n_cols}, nnz {L.nnz}, u_len {ulen.value}", flush=True)
     T = [torch.rand(n_own, device=dev) for _ in range(3)]
     S = torch.zeros(n_own, device=dev)
-    if ulen.value:
+    if a.F > 1:
+        F = a.F
+        X = [torch.rand(n_cols, F, device=dev), torch.rand(n_own, F, device=dev), torch.rand(n_own, F, device=dev)]
+        SF = torch.zeros(n_own, F, device=dev)
+        run = lambda k: L.step(k, X[0], X[1], X[2], S=SF, alpha0=1.0, alpha_k=math.exp(-0.8 * k))
+        info = f"gather kernel F={F}"
+    elif ulen.value:
         U = [torch.rand(ulen.value, device=dev) for _ in range(2)]
         run = lambda k: check(lib.wg_cheb_step_u(L.handle, k, ptr(U[0]), ptr(T[0]), ptr(T[1]), ptr(T[2]), ptr(U[1]),
                                                  ptr(S), 1.0, math.exp(-0.8 * k), st), "step_u")
