@@ -74,8 +74,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--traffic-json", default="auto",
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py); "
-                         "'auto': the committed PMC summary of the default workload (profiles/r01/s56_traffic.json, "
-                         "tools/gpu_session.sh RUN_PMC=1) when the workload is the default one; 'none' to omit")
+                         "'auto': the committed PMC summary of the default workload (profiles/r02/s12_traffic.json, "
+                         "tools/r02_traffic.sh) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--sharded-extra", default="reddit-f41,reddit,rmat-8m",
                     help="comma-separated configs also measured row-sharded over all ranks (halo exchange), attached "
