@@ -91,6 +91,9 @@ def parse():
                          "(rccl) or the one-sided IPC pull (ipc), or torch all_to_all_single per step (nccl); the "
                          "first is the headline's (N > 1) and the extras'; the others are timed for the first "
                          "sharded config only, as 'sharded_<config>_<exchange>'")
+    ap.add_argument("--halo-tiers", type=int, default=None,
+                    help="sharded runs: halo tiers (1, or 2: the hot halo rows exchanged first and their entries "
+                         "summed while the rest is in flight); default: 2 at N > 1, 1 at N = 1")
     ap.add_argument("--cold-reps", type=int, default=5,
                     help="chains timed after writing a 512 MiB scratch buffer (cold Infinity Cache / L2); 0 = skip")
     ap.add_argument("--f1-companion", type=int, default=1,
@@ -199,7 +202,7 @@ def _rel_err(got, ref) -> float:
 
 # ----------------------------------------------------------------------------- row-sharded runs
 def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl",
-                median_reps: int = 0, check: bool = True):
+                median_reps: int = 0, check: bool = True, halo_tiers=None):
     """One graph (generated identically on every rank, on the GPU) split into
     nnz-balanced row blocks; per Chebyshev step one halo exchange (`exchange`:
     RCCL send/recv or IPC pull in the native chain, or torch
@@ -226,7 +229,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     torch.cuda.empty_cache()
     with _stdout_to_stderr():   # RCCL prints its version banner at communicator init: keep stdout one JSON line
         sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device,
-                            max_features=F)
+                            max_features=F, halo_tiers=halo_tiers)
     if F == 1:
         X = sw.L.log1p_degree()
     else:
@@ -309,7 +312,8 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                                   "nccl": "(torch all_to_all_single, RCCL)"}[exchange] + f"; K={K} F={F}",
                    "exchange": exchange,
                    "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
-                   "rank0_rows": p.n_own, "rank0_halo_rows": p.n_halo, "parallelism": f"rows x{world}"},
+                   "rank0_rows": p.n_own, "rank0_halo_rows": p.n_halo, "halo_tiers": p.tiers,
+                   "rank0_hot_halo_rows": p.n_hot, "parallelism": f"rows x{world}"},
         "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None,
@@ -650,14 +654,14 @@ def main():
         hw.start()
         try:
             line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
-                               exchanges[0], median_reps=max(20, args.steps))
+                               exchanges[0], median_reps=max(20, args.steps), halo_tiers=args.halo_tiers)
         except Exception as exc:  # noqa: BLE001 -- keep a headline: the next exchange, noted in the line
             if len(exchanges) < 2:
                 raise
             _log(f"headline with exchange {exchanges[0]} failed ({type(exc).__name__}: {exc}); using {exchanges[1]}")
             torch.cuda.empty_cache()
             line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
-                               exchanges[1], median_reps=max(20, args.steps))
+                               exchanges[1], median_reps=max(20, args.steps), halo_tiers=args.halo_tiers)
             line["headline_fallback"] = f"exchange {exchanges[0]} failed: {type(exc).__name__}: {exc}"
             exchanges = exchanges[1:] + exchanges[:1]
         hw.cancel()
@@ -724,7 +728,7 @@ def main():
             try:
                 torch.cuda.empty_cache()
                 results[key] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
-                                           device, x)
+                                           device, x, halo_tiers=args.halo_tiers)
             except Exception as exc:  # noqa: BLE001
                 results[key] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
     if mode == "sharded" and len(exchanges) > 1:
@@ -734,9 +738,20 @@ def main():
             try:
                 torch.cuda.empty_cache()
                 results[f"{cfg}_{x}"] = run_sharded(cfg, args.K, args.F, args.sharded_steps, 1, args.seed, args.s,
-                                                    world, rank, device, x)
+                                                    world, rank, device, x, halo_tiers=args.halo_tiers)
             except Exception as exc:  # noqa: BLE001
                 results[f"{cfg}_{x}"] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
+    if mode == "sharded" and world > 1 and args.halo_tiers is None:
+        # the headline's exchange with the halo in one tier: what the two-tier exchange buys
+        cfg = args.scale_config if args.mode == "auto" else args.config
+        try:
+            torch.cuda.empty_cache()
+            results[f"{cfg}_{exchanges[0]}_tiers1"] = run_sharded(cfg, args.K, args.F, args.sharded_steps, 1,
+                                                                  args.seed, args.s, world, rank, device,
+                                                                  exchanges[0], check=False, halo_tiers=1)
+        except Exception as exc:  # noqa: BLE001
+            results[f"{cfg}_{exchanges[0]}_tiers1"] = {"error": f"{type(exc).__name__}: {exc}",
+                                                      "exchange": exchanges[0]}
     if watchdog is not None:
         watchdog.cancel()
     if rank == 0:

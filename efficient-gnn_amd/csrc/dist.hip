@@ -99,12 +99,12 @@ __device__ __forceinline__ void ipc_wait(const IpcPull& p, bool signal) {
 // ext[n_own + h].  Launched after ipc_wait_kernel on the same stream, so it
 // needs no wait of its own and can use a full grid (one remote load per lane:
 // the pull is latency-bound, 0.8 MB per Reddit-size step over 7 links).
-__global__ __launch_bounds__(256) void ipc_pull_kernel(IpcPull p, int slot, int64_t n_own, int64_t n_halo, int64_t F,
-                                                       const int32_t* __restrict__ owner,
+__global__ __launch_bounds__(256) void ipc_pull_kernel(IpcPull p, int slot, int64_t n_own, int64_t h0, int64_t n_halo,
+                                                       int64_t F, const int32_t* __restrict__ owner,
                                                        const int32_t* __restrict__ src, float* __restrict__ ext) {
   const int64_t total = n_halo * F;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t idx = h0 * F + i;  // halo rows [h0, h0 + n_halo)
     const int64_t h = idx / F;
     const int q = owner[h];
     const float* from = p.slot_base[q] + slot * p.slot_floats[q] + (int64_t)src[h] * F + (idx - h * F);
@@ -115,14 +115,14 @@ __global__ __launch_bounds__(256) void ipc_pull_kernel(IpcPull p, int slot, int6
 // The same pull with 16-B loads (F % 4 == 0: every row and slot is 16-B aligned): one
 // system-scope (sc0 sc1: no stale cached copy of the owner's slot) dwordx4 buffer load
 // per lane, 4x fewer remote transactions than ipc_pull_kernel for the F = 44 rows.
-__global__ __launch_bounds__(256) void ipc_pull4_kernel(IpcPull p, int slot, int64_t n_own, int64_t n_halo, int64_t F,
-                                                        const int32_t* __restrict__ owner,
+__global__ __launch_bounds__(256) void ipc_pull4_kernel(IpcPull p, int slot, int64_t n_own, int64_t h0, int64_t n_halo,
+                                                        int64_t F, const int32_t* __restrict__ owner,
                                                         const int32_t* __restrict__ src, float* __restrict__ ext) {
   constexpr int kSysCoherent = 1 | 16;  // cache policy sc0 | sc1 (gfx940+ CPol bits)
   const int64_t F4 = F >> 2;
   const int64_t total = n_halo * F4;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t idx = h0 * F4 + i;  // halo rows [h0, h0 + n_halo)
     const int64_t h = idx / F4;
     const int64_t c4 = idx - h * F4;
     const int q = owner[h];
@@ -177,7 +177,11 @@ struct wg_dist_s {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   int64_t n_own = 0, n_cols = 0, n_send = 0, n_halo = 0;
-  int32_t* send_rows = nullptr;  // internal ids of own rows, grouped by peer
+  // tiers (1 or 2): the halo is [tier 0 | tier 1], each grouped by owner; tier 0 holds every
+  // peer's highest-degree rows (most of the gathers), exchanged first so the step's hot-halo
+  // entries run while tier 1 is in flight.  Counts and offsets are tier-major: [t * world + q].
+  int tiers = 1;
+  int32_t* send_rows = nullptr;  // internal ids of own rows, grouped by (tier, peer)
   std::vector<int64_t> send_cnt, recv_cnt, send_off, recv_off;
   float* ws = nullptr;
   size_t ws_floats = 0;
@@ -186,7 +190,7 @@ struct wg_dist_s {
   hipEvent_t fork = nullptr, join = nullptr;
   // exchange overlapped with the own-column half of each step (two-phase steps, step.hip)
   hipStream_t xs = nullptr;   // exchange stream
-  hipEvent_t xfork = nullptr, xjoin = nullptr;
+  hipEvent_t xfork = nullptr, xjoin = nullptr, xtier = nullptr;
   bool overlapped = false;    // the last chain ran two-phase steps
   hipGraphExec_t exec = nullptr;
   GraphKey key{};
@@ -218,6 +222,7 @@ struct wg_dist_s {
     if (join) (void)hipEventDestroy(join);
     if (xfork) (void)hipEventDestroy(xfork);
     if (xjoin) (void)hipEventDestroy(xjoin);
+    if (xtier) (void)hipEventDestroy(xtier);
     if (cap) (void)hipStreamDestroy(cap);
     if (xs) (void)hipStreamDestroy(xs);
     (void)hipFree(send_rows);
@@ -252,62 +257,78 @@ struct wg_dist_s {
     return WG_OK;
   }
 
-  // refresh the halo rows ext[n_own ...] (F floats per row) from their owners.
-  // ipc: `slot` is the region slot ext lives in (the owners' rows are read from
-  // the same slot of their regions); the previous phase's completion is
-  // signalled by the same one-workgroup kernel that then waits for the peers
-  int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot = 0) {
+  // refresh halo tier `tier` (-1: every tier) of ext[n_own ...] (F floats per row) from the
+  // owners.  ipc: `slot` is the region slot ext lives in (the owners' rows are read from the
+  // same slot of their regions); the previous phase's completion is signalled by the same
+  // one-workgroup kernel that then waits for the peers -- once per phase, with the first tier.
+  // rccl: every send row is packed with the first tier; one grouped send/receive per call.
+  // The profiling events span the first tier's start to the last tier's end.
+  int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot = 0, int tier = -1) {
+    const int t0 = tier < 0 ? 0 : tier, t1 = tier < 0 ? tiers - 1 : tier;
+    const bool first = t0 == 0, last = t1 == tiers - 1;
     if (ipc && world == 1) return WG_OK;  // no peers: nothing to wait for or pull
     if (ipc) {
-      if (int rc = mark(st, true)) return rc;
-      // one spinning workgroup signals and waits (ranks sharing a GPU in tests must not
-      // starve each other's kernels), then a full grid pulls the halo rows
-      if (int rc = ipc_wait_only(st, /*signal_first=*/true)) return rc;
-      const int64_t total = n_halo * F;
+      if (first) {
+        if (int rc = mark(st, true)) return rc;
+        // one spinning workgroup signals and waits (ranks sharing a GPU in tests must not
+        // starve each other's kernels), then full grids pull the halo rows
+        if (int rc = ipc_wait_only(st, /*signal_first=*/true)) return rc;
+      }
+      const int64_t h0 = recv_off[(size_t)t0 * world], h1 = recv_off[(size_t)(t1 + 1) * world];
+      const int64_t total = (h1 - h0) * F;
       const bool v4 = (F % 4 == 0) && slot_floats * 4 < ((int64_t)1 << 31);
       if (total > 0) {
         const int blocks = (int)std::min<int64_t>(65535, ceil_div(v4 ? total / 4 : total, 256));
         if (v4)
-          hipLaunchKernelGGL(ipc_pull4_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, n_halo, F,
+          hipLaunchKernelGGL(ipc_pull4_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, h0, h1 - h0, F,
                              halo_owner, halo_src, ext);
         else
-          hipLaunchKernelGGL(ipc_pull_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, n_halo, F,
+          hipLaunchKernelGGL(ipc_pull_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, h0, h1 - h0, F,
                              halo_owner, halo_src, ext);
         WG_LAUNCH_CHECK();
       }
-      return mark(st, false);
+      return last ? mark(st, false) : WG_OK;
     }
     if (world == 1 && n_send == 0) return WG_OK;
-    if (int rc = mark(st, true)) return rc;
-    if (n_send > 0) {
-      hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)ceil_div(n_send * F, 256)), dim3(256), 0, st, n_send, F,
-                         send_rows, ext, sendbuf);
-      WG_LAUNCH_CHECK();
+    if (first) {
+      if (int rc = mark(st, true)) return rc;
+      if (n_send > 0) {
+        hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)ceil_div(n_send * F, 256)), dim3(256), 0, st, n_send, F,
+                           send_rows, ext, sendbuf);
+        WG_LAUNCH_CHECK();
+      }
     }
+    // one grouped send / receive for the tiers asked for (all of them: one group)
     if (int rc = nccl_try(ncclGroupStart(), "ncclGroupStart")) return rc;
-    for (int q = 0; q < world; ++q) {
-      if (send_cnt[q] > 0)
-        if (int rc = nccl_try(ncclSend(sendbuf + send_off[q] * F, (size_t)(send_cnt[q] * F), ncclFloat32, q, comm, st),
-                              "ncclSend")) {
-          (void)ncclGroupEnd();
-          return rc;
-        }
-      if (recv_cnt[q] > 0)
-        if (int rc = nccl_try(ncclRecv(ext + (n_own + recv_off[q]) * F, (size_t)(recv_cnt[q] * F), ncclFloat32, q,
-                                       comm, st),
-                              "ncclRecv")) {
-          (void)ncclGroupEnd();
-          return rc;
-        }
+    for (int t = t0; t <= t1; ++t) {
+      for (int q = 0; q < world; ++q) {
+        const size_t i = (size_t)t * world + q;
+        if (send_cnt[i] > 0)
+          if (int rc = nccl_try(ncclSend(sendbuf + send_off[i] * F, (size_t)(send_cnt[i] * F), ncclFloat32, q, comm, st),
+                                "ncclSend")) {
+            (void)ncclGroupEnd();
+            return rc;
+          }
+        if (recv_cnt[i] > 0)
+          if (int rc = nccl_try(ncclRecv(ext + (n_own + recv_off[i]) * F, (size_t)(recv_cnt[i] * F), ncclFloat32, q,
+                                         comm, st),
+                                "ncclRecv")) {
+            (void)ncclGroupEnd();
+            return rc;
+          }
+      }
     }
     if (int rc = nccl_try(ncclGroupEnd(), "ncclGroupEnd")) return rc;
-    return mark(st, false);
+    return last ? mark(st, false) : WG_OK;
   }
 
   // One Chebyshev step that gathers from `cur` (own rows final, halo rows to be
   // refreshed): without overlap, exchange then the step; with overlap, phase 1
   // (own-column entries, into `part`) forks onto xs while the exchange runs on
-  // st; st joins phase 1, then phase 2 (halo entries + part, epilogue).  The
+  // st; st joins phase 1, then phase 2 (halo entries + part, epilogue).  With
+  // two halo tiers, phase 3 (tier-0 halo entries, added into part) runs on xs
+  // between the tier-0 and the tier-1 exchange, and phase 2 takes the tier-1
+  // entries only.  The
   // exchange stays on st, the stream a captured chain is recorded on (RCCL
   // under a capture joined by a side stream crashed in the one-GPU loopback).
   // Hazards: the exchange writes only cur's halo rows and reads its own rows;
@@ -315,7 +336,7 @@ struct wg_dist_s {
   // previous step wrote cur's own rows and last read the other buffer's halo).
   template <typename StepFn>
   int step_with_exchange(float* cur, float* sendbuf, int64_t Fp, hipStream_t st, int slot, const int32_t* rsplit,
-                         double* part, StepFn&& launch) {
+                         const int32_t* rsplit2, double* part, StepFn&& launch) {
     if (!rsplit) {
       if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
       return launch(st, nullptr);
@@ -327,11 +348,26 @@ struct wg_dist_s {
     WG_HIP_TRY(hipEventRecord(xfork, st));
     WG_HIP_TRY(hipStreamWaitEvent(xs, xfork, 0));
     if (int rc = launch(xs, &p1)) return rc;
-    WG_HIP_TRY(hipEventRecord(xjoin, xs));
-    if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
-    WG_HIP_TRY(hipStreamWaitEvent(st, xjoin, 0));
     PhaseArgs p2 = p1;
     p2.phase = 2;
+    if (rsplit2) {
+      // tier 0 (every peer's hottest rows) first; its entries (phase 3, added into part) run
+      // on xs after phase 1 while tier 1 is exchanged on st
+      if (int rc = exchange(cur, sendbuf, Fp, st, slot, 0)) return rc;
+      WG_HIP_TRY(hipEventRecord(xtier, st));
+      WG_HIP_TRY(hipStreamWaitEvent(xs, xtier, 0));
+      PhaseArgs p3 = p1;
+      p3.phase = 3;
+      p3.rsplit2 = rsplit2;
+      if (int rc = launch(xs, &p3)) return rc;
+      WG_HIP_TRY(hipEventRecord(xjoin, xs));
+      if (int rc = exchange(cur, sendbuf, Fp, st, slot, 1)) return rc;
+      p2.rsplit2 = rsplit2;
+    } else {
+      WG_HIP_TRY(hipEventRecord(xjoin, xs));
+      if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
+    }
+    WG_HIP_TRY(hipStreamWaitEvent(st, xjoin, 0));
     return launch(st, &p2);
   }
 
@@ -350,9 +386,14 @@ struct wg_dist_s {
     const bool clen = !lp && L->tune.clenshaw && K >= 1;
     // two-phase steps overlapping the exchange (gather-kernel path, rows column-sorted, peers present)
     const int32_t* rsplit = nullptr;
+    const int32_t* rsplit2 = nullptr;  // first tier-1 halo entry of each row (two tiers)
     // (any halo: at world 1 too -- the one-GPU loopback test exercises the overlapped RCCL path)
-    if (!lp && L->tune.overlap && n_halo > 0 && (comm || ipc) && n_own > 0 && K >= 1)
-      if (int rc = get_row_split(L, &rsplit)) return rc;
+    if (!lp && L->tune.overlap && n_halo > 0 && (comm || ipc) && n_own > 0 && K >= 1) {
+      if (int rc = get_row_split(L, n_own, &rsplit)) return rc;
+      const int64_t n_hot = recv_off[world];
+      if (rsplit && tiers == 2 && n_hot > 0 && n_hot < n_halo)
+        if (int rc = get_row_split(L, n_own + n_hot, &rsplit2)) return rc;
+    }
     overlapped = rsplit != nullptr;
     const size_t partf = rsplit ? 2 * own : 0;  // float64 row partials (n_own x Fp doubles)
     const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd + (clen ? own : 0) +
@@ -434,7 +475,7 @@ struct wg_dist_s {
         cl.uin = useu && j >= 2;          // j == 1 gathers X0 itself
         cl.uprev = useu && prev_stored;
         cl.uout = useu;                   // ignored on the final step (k == 0 writes S)
-        rc = step_with_exchange(cur, sendbuf, Fp, st, (j - 1) & 1, rsplit, part,
+        rc = step_with_exchange(cur, sendbuf, Fp, st, (j - 1) & 1, rsplit, rsplit2, part,
                                 [&](hipStream_t s2, const PhaseArgs* ph) {
                                   return launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr,
                                                      k == 0 ? nullptr : A[j & 1], k == 0 ? sint : nullptr, nullptr,
@@ -444,7 +485,7 @@ struct wg_dist_s {
     } else {
       for (int32_t k = 1; k <= K && !rc; ++k) {
         float* cur = A[(k - 1) & 1];
-        rc = step_with_exchange(cur, sendbuf, Fp, st, (k - 1) & 1, rsplit, part,
+        rc = step_with_exchange(cur, sendbuf, Fp, st, (k - 1) & 1, rsplit, rsplit2, part,
                                 [&](hipStream_t s2, const PhaseArgs* ph) {
                                   return launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr,
                                                      k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
@@ -470,33 +511,42 @@ int wg_dist_unique_id(void* out) {
 
 int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world, const int32_t* send_rows,
                    const int64_t* send_counts, const int64_t* recv_counts, wg_dist_t* out) {
+  return wg_dist_create_tiered(L, unique_id, rank, world, 1, send_rows, send_counts, recv_counts, out);
+}
+
+int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world, int32_t tiers,
+                          const int32_t* send_rows, const int64_t* send_counts, const int64_t* recv_counts,
+                          wg_dist_t* out) {
   if (!out) return fail(WG_ERR_INVALID, "wg_dist_create: out is NULL");
   *out = nullptr;
-  if (!L || world < 1 || rank < 0 || rank >= world || !send_counts || !recv_counts)
-    return fail(WG_ERR_INVALID, "wg_dist_create: bad arguments (rank=%d world=%d)", rank, world);
+  if (!L || world < 1 || rank < 0 || rank >= world || !send_counts || !recv_counts || tiers < 1 || tiers > 2)
+    return fail(WG_ERR_INVALID, "wg_dist_create: bad arguments (rank=%d world=%d tiers=%d)", rank, world, tiers);
   auto* D = new wg_dist_s();
   D->L = L;
   D->rank = rank;
   D->world = world;
+  D->tiers = tiers;
   D->n_own = L->n_rows;
   D->n_cols = L->n_cols;
-  D->send_cnt.assign(send_counts, send_counts + world);
-  D->recv_cnt.assign(recv_counts, recv_counts + world);
-  D->send_off.assign(world + 1, 0);
-  D->recv_off.assign(world + 1, 0);
-  for (int q = 0; q < world; ++q) {
-    if (D->send_cnt[q] < 0 || D->recv_cnt[q] < 0) {
+  const int64_t nc = (int64_t)tiers * world;
+  D->send_cnt.assign(send_counts, send_counts + nc);
+  D->recv_cnt.assign(recv_counts, recv_counts + nc);
+  D->send_off.assign(nc + 1, 0);
+  D->recv_off.assign(nc + 1, 0);
+  for (int64_t i = 0; i < nc; ++i) {
+    if (D->send_cnt[i] < 0 || D->recv_cnt[i] < 0) {
       delete D;
-      return fail(WG_ERR_INVALID, "wg_dist_create: negative count for peer %d", q);
+      return fail(WG_ERR_INVALID, "wg_dist_create: negative count for (tier %d, peer %d)", (int)(i / world),
+                  (int)(i % world));
     }
-    D->send_off[q + 1] = D->send_off[q] + D->send_cnt[q];
-    D->recv_off[q + 1] = D->recv_off[q] + D->recv_cnt[q];
+    D->send_off[i + 1] = D->send_off[i] + D->send_cnt[i];
+    D->recv_off[i + 1] = D->recv_off[i] + D->recv_cnt[i];
   }
-  D->n_send = D->send_off[world];
-  D->n_halo = D->recv_off[world];
+  D->n_send = D->send_off[nc];
+  D->n_halo = D->recv_off[nc];
   if (D->n_halo > 0 && D->n_own + D->n_halo == L->n_cols) {
-    // the halo groups (one per peer, each in descending degree: wats_hip/dist.py) for the F = 1
-    // hub plan of a shard; plans built before this point are dropped
+    // the halo groups (one per (tier, peer), each in descending degree: wats_hip/dist.py) for
+    // the F = 1 hub plan of a shard; plans built before this point are dropped
     L->halo_off.assign(D->recv_off.begin(), D->recv_off.end());
     release_lds1(L);
   }
@@ -516,7 +566,8 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
               hipEventCreateWithFlags(&D->fork, hipEventDisableTiming) != hipSuccess ||
               hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess ||
               hipEventCreateWithFlags(&D->xfork, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&D->xjoin, hipEventDisableTiming) != hipSuccess))
+              hipEventCreateWithFlags(&D->xjoin, hipEventDisableTiming) != hipSuccess ||
+              hipEventCreateWithFlags(&D->xtier, hipEventDisableTiming) != hipSuccess))
     rc = fail(WG_ERR_HIP, "wg_dist_create: stream/event");
   if (!rc && unique_id) {  // NULL: no RCCL communicator (one-sided IPC exchange, wg_dist_ipc_*)
     ncclUniqueId id;
@@ -655,8 +706,8 @@ int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src)
   if (int rc = dmalloc(&D->peer_flags, (size_t)D->world)) return rc;
   WG_HIP_TRY(hipMemcpy(D->peer_flags, pf.data(), sizeof(int64_t*) * D->world, hipMemcpyHostToDevice));
   std::vector<int32_t> owner(D->n_halo);
-  for (int q = 0; q < D->world; ++q)
-    for (int64_t i = D->recv_off[q]; i < D->recv_off[q + 1]; ++i) owner[i] = q;
+  for (int64_t g = 0; g < (int64_t)D->tiers * D->world; ++g)
+    for (int64_t i = D->recv_off[g]; i < D->recv_off[g + 1]; ++i) owner[i] = (int32_t)(g % D->world);
   if (D->n_halo > 0) {
     if (int rc = dmalloc(&D->halo_owner, (size_t)D->n_halo)) return rc;
     if (int rc = dmalloc(&D->halo_src, (size_t)D->n_halo)) return rc;
@@ -692,7 +743,7 @@ int wg_dist_info(wg_dist_t D, int64_t* out) {
   out[4] = D->world;
   out[5] = D->ipc ? 1 : (D->comm ? 2 : 0);
   out[6] = D->exec ? 1 : 0;
-  out[7] = 0;
+  out[7] = D->tiers;
   return WG_OK;
 }
 

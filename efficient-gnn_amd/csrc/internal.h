@@ -183,6 +183,8 @@ struct wg_laplacian_s {
                               // graph agrees, so a row-sharded chain may exchange u = b * dinv)
   double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
   int32_t* rsplit = nullptr;  // [n_rows] first halo entry of each row (two-phase steps), lazily built
+  int32_t* rsplit2 = nullptr;  // [n_rows] first entry with column >= rsplit2_at (two halo tiers)
+  int64_t rsplit2_at = -1;
   std::vector<int64_t> halo_off;  // row shard: halo columns [n_rows + halo_off[q], n_rows + halo_off[q+1])
                                   // come from peer q, each group in descending degree (wg_dist_create)
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
@@ -223,18 +225,22 @@ struct ClenArgs {
 // Two-phase step (the row-sharded chain overlaps the halo exchange with phase 1): phase 1
 // sums each row's own-column entries [row start, rsplit[row]) into part (float64, row
 // stride F, no epilogue); phase 2 sums the halo entries [rsplit[row], row end), adds part
-// and runs the step's epilogue.  phase 0 = the whole row in one launch.
+// and runs the step's epilogue.  phase 0 = the whole row in one launch.  Two halo tiers:
+// phase 3 adds the tier-0 entries [rsplit[row], rsplit2[row]) into part (between 1 and 2),
+// and phase 2 sums [rsplit2[row], row end).
 struct PhaseArgs {
   int phase = 0;
-  const int32_t* rsplit = nullptr;  // [n_rows] first entry with column >= n_rows (rows column-sorted)
-  double* part = nullptr;           // [n_rows][F]
+  const int32_t* rsplit = nullptr;   // [n_rows] first entry with column >= n_rows (rows column-sorted)
+  const int32_t* rsplit2 = nullptr;  // [n_rows] first tier-1 halo entry (two tiers), else nullptr
+  double* part = nullptr;            // [n_rows][F]
 };
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
                 float* S_out = nullptr, const ClenArgs* cl = nullptr, const PhaseArgs* ph = nullptr);
-// rsplit for two-phase steps: per internal row, the first entry whose column is a halo
-// column (>= n_rows); built once (synchronous), nullptr when rows are not column-sorted
-int get_row_split(wg_laplacian_s* L, const int32_t** out);
+// per internal row, the first entry whose column is >= split (n_rows: the first halo entry;
+// n_rows + the tier-0 halo rows: the first tier-1 entry); built once per split (synchronous),
+// nullptr when rows are not column-sorted
+int get_row_split(wg_laplacian_s* L, int64_t split, const int32_t** out);
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef,
                     float* S, float* H, hipStream_t stream, int64_t ldi = 0);  // ldi: internal row stride (0 = F)
 // the internal signal width of an F-column chain: odd / 4-unaligned F >= 3 is

@@ -519,7 +519,7 @@ wg_laplacian_s::~wg_laplacian_s() {
   for (auto& kv : plans) kv.second.release();
   wg::release_lds1(this);
   for (void* p : {(void*)rowptr, (void*)col, (void*)val, (void*)iso, (void*)perm, (void*)iperm, (void*)rowsum,
-                  (void*)ws, (void*)dinv, (void*)rsplit})
+                  (void*)ws, (void*)dinv, (void*)rsplit, (void*)rsplit2})
     (void)hipFree(p);
 }
 

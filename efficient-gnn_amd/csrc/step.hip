@@ -79,8 +79,11 @@ struct StepArgs {
   // two-phase step (row-sharded chain, exchange overlapped): phase 1 sums each row's entries
   // [e0, rsplit[row]) (the own columns) into part[row] (float64, row stride ld); phase 2 sums
   // [rsplit[row], e1) (the halo columns), adds part[row] and runs the epilogue.  0 = whole row.
+  // Two halo tiers: phase 3 adds [rsplit[row], rsplit2[row]) (tier 0) into part between them,
+  // and phase 2 sums [rsplit2[row], e1).
   int32_t phase;
   const int32_t* rsplit;
+  const int32_t* rsplit2;
   double* part;
   int32_t probe;  // timing probe (knob "probe"): gathers only -- no epilogue operands, acc stored to xk
 };
@@ -89,17 +92,32 @@ struct StepArgs {
 __device__ __forceinline__ void phase_range(const StepArgs& a, int64_t row, int32_t& e0, int32_t& e1) {
   if (a.phase == 0) return;
   const int32_t sp = a.rsplit[row];
-  if (a.phase == 1) e1 = min(e1, sp);
-  else e0 = max(e0, sp);
+  if (a.phase == 1) {
+    e1 = min(e1, sp);
+  } else if (a.phase == 3) {
+    e0 = max(e0, sp);
+    e1 = min(e1, a.rsplit2[row]);
+  } else {
+    e0 = max(e0, a.rsplit2 ? a.rsplit2[row] : sp);
+  }
   if (e1 < e0) e1 = e0;
 }
 
-// phase 1: the row's own-column sum goes to part (no epilogue); phase 2: add it before the epilogue
+// phases 1 and 3 end in part (no epilogue)
+__device__ __forceinline__ bool to_part(const StepArgs& a) { return a.phase == 1 || a.phase == 3; }
+
+// phase 1: the row's own-column sum goes to part; phase 3 adds its tier-0 sum; phase 2 adds
+// part before the epilogue (a fixed order: own, tier 0, tier 1)
 template <int VEC>
 __device__ __forceinline__ void part_store(const StepArgs& a, int64_t row, int fs, const double (&acc)[VEC]) {
   double* p = a.part + row * a.ld + (int64_t)fs * VEC;
+  if (a.phase == 3) {
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) p[j] = acc[j];
+    for (int j = 0; j < VEC; ++j) p[j] = p[j] + acc[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) p[j] = acc[j];
+  }
 }
 
 template <int VEC>
@@ -586,7 +604,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     const bool active = team < tpw && row < seg.end;
     EpiIn<VEC> in;
     if (active) {
-      if (ns == 0 && a.phase != 1) epi_prefetch<VEC>(a, row, fs, in);
+      if (ns == 0 && !to_part(a)) epi_prefetch<VEC>(a, row, fs, in);
       int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
       phase_range(a, row, e0, e1);
       if constexpr (VEC == 1 && !HOT) {
@@ -598,7 +616,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
     if (active && ns == 0) {
-      if (a.phase == 1) {
+      if (to_part(a)) {
         part_store<VEC>(a, row, fs, acc);
       } else {
         if (a.phase == 2) part_add<VEC>(a, row, fs, acc);
@@ -629,7 +647,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
   const int sg = lane / LF;
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
-  if (seg.mode == 1 && threadIdx.x < LF && a.phase != 1) epi_prefetch<VEC>(a, row, threadIdx.x, in);
+  if (seg.mode == 1 && threadIdx.x < LF && !to_part(a)) epi_prefetch<VEC>(a, row, threadIdx.x, in);
   if constexpr (VEC == 1 && !HOT) {
     if (a.vidx && LF == 1) {
       // chunk-aligned ranges: for split chunks e0 is a multiple of CH (>= 4) from the row start, so
@@ -657,7 +675,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       for (int j = 0; j < VEC; ++j) acc[j] += red[(w * LF + t) * VEC + j];
     }
     if (seg.mode == 1) {
-      if (a.phase == 1) {
+      if (to_part(a)) {
         part_store<VEC>(a, row, t, acc);
       } else {
         if (a.phase == 2) part_add<VEC>(a, row, t, acc);
@@ -689,7 +707,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     if (s_last && threadIdx.x < LF) {
       const int t = threadIdx.x;
       EpiIn<VEC> in2;
-      if (a.phase != 1) epi_prefetch<VEC>(a, row, t, in2);
+      if (!to_part(a)) epi_prefetch<VEC>(a, row, t, in2);
       double sum[VEC];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) sum[j] = 0.0;
@@ -698,7 +716,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
 #pragma unroll
         for (int j = 0; j < VEC; ++j) sum[j] += __hip_atomic_load(pp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (a.phase == 1) {
+      if (to_part(a)) {
         part_store<VEC>(a, row, t, sum);
       } else {
         if (a.phase == 2) part_add<VEC>(a, row, t, sum);
@@ -758,7 +776,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
   const int2 rc = rowchunks[row];
   const int width = LF * VEC;
   EpiIn<VEC> in;
-  if (a.phase != 1) epi_prefetch<VEC>(a, row, fs, in);
+  if (!to_part(a)) epi_prefetch<VEC>(a, row, fs, in);
   double acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
@@ -767,7 +785,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] += p[j];
   }
-  if (a.phase == 1) {
+  if (to_part(a)) {
     part_store<VEC>(a, row, fs, acc);
     return;
   }
@@ -1241,8 +1259,8 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out,
                 const ClenArgs* cl, const PhaseArgs* ph) {
   if (L->n_rows == 0) return WG_OK;
-  if (ph && ph->phase != 0 && (!ph->rsplit || !ph->part || S_out))
-    return fail(WG_ERR_INVALID, "launch_step: a two-phase step needs rsplit and part (and no fused finalize)");
+  if (ph && ph->phase != 0 && (!ph->rsplit || !ph->part || S_out || (ph->phase == 3 && !ph->rsplit2)))
+    return fail(WG_ERR_INVALID, "launch_step: a phased step needs rsplit (phase 3: rsplit2), part, no fused finalize");
   if (int rc = prof_mark(L, stream, true)) return rc;
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H, S_out});
   int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
@@ -1288,8 +1306,9 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     if (ph && ph->phase != 0) {
       a.phase = ph->phase;
       a.rsplit = ph->rsplit;
+      a.rsplit2 = ph->rsplit2;
       a.part = ph->part + f0;
-      if (a.phase == 1) {  // nothing but the sums: no epilogue operands, no stores of T / S / H
+      if (a.phase == 1 || a.phase == 3) {  // nothing but the sums: no epilogue operands, no T / S / H stores
         a.xk = nullptr;
         a.S = nullptr;
         a.H = nullptr;
@@ -1325,7 +1344,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     else rc = launch_step_vec<1>(*plan, a, stream);
     if (rc) return rc;
   }
-  if (H && !fuse_h && !(ph && ph->phase == 1)) {
+  if (H && !fuse_h && !(ph && (ph->phase == 1 || ph->phase == 3))) {
     hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(L->n_rows, 4)), dim3(kBlock), 0, stream, L->n_rows, F, S, H);
     WG_LAUNCH_CHECK();
   }
@@ -1435,24 +1454,31 @@ __global__ void row_split_kernel(int64_t n, int32_t split, const int32_t* __rest
 }
 }  // namespace
 
-int get_row_split(wg_laplacian_s* L, const int32_t** out) {
+int get_row_split(wg_laplacian_s* L, int64_t split, const int32_t** out) {
   *out = nullptr;
   if (!L->cols_sorted) return WG_OK;
-  if (!L->rsplit) {
+  const bool first = split == L->n_rows;  // the own / halo split; else the halo tier split
+  int32_t*& slot = first ? L->rsplit : L->rsplit2;
+  if (slot && !first && L->rsplit2_at != split) {
+    (void)hipFree(slot);
+    slot = nullptr;
+  }
+  if (!slot) {
     int32_t* p = nullptr;
     if (int rc = dmalloc(&p, (size_t)std::max<int64_t>(1, L->n_rows))) return rc;
     if (L->n_rows > 0) {
       hipLaunchKernelGGL(row_split_kernel, dim3((unsigned)ceil_div(L->n_rows, 256)), dim3(256), 0, nullptr, L->n_rows,
-                         (int32_t)L->n_rows, L->rowptr, L->col, p);
+                         (int32_t)split, L->rowptr, L->col, p);
       const hipError_t e = hipDeviceSynchronize();
       if (e != hipSuccess) {
         (void)hipFree(p);
         return fail(WG_ERR_HIP, "row_split: %s", hipGetErrorString(e));
       }
     }
-    L->rsplit = p;
+    slot = p;
+    if (!first) L->rsplit2_at = split;
   }
-  *out = L->rsplit;
+  *out = slot;
   return WG_OK;
 }
 

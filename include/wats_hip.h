@@ -264,6 +264,15 @@ int wg_dist_unique_id(void* id_out /* 128 bytes, host */);
 int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world,
                    const int32_t* send_rows, const int64_t* send_counts_host,
                    const int64_t* recv_counts_host, wg_dist_t* out);
+/* The same with the halo in `tiers` (1 or 2) tiers: send_counts / recv_counts
+ * hold tiers * world entries, tier-major ([t * world + q]); the halo columns
+ * and send_rows are ordered (tier, peer).  Tier 0 holds every peer's
+ * highest-degree rows: it is exchanged first, and each step's entries on those
+ * columns run (on a second stream) while tier 1 is exchanged.  tiers = 1 is
+ * wg_dist_create. */
+int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world, int32_t tiers,
+                          const int32_t* send_rows, const int64_t* send_counts_host,
+                          const int64_t* recv_counts_host, wg_dist_t* out);
 int wg_dist_destroy(wg_dist_t D);
 int wg_dist_set_graph(wg_dist_t D, int32_t enable);
 int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K, double s, float* S,
@@ -272,7 +281,7 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
  * each step's halo exchange with the step's own-column half (two-phase
  * steps: 2 step launches per Chebyshev step), [1] own rows, [2] halo rows,
  * [3] rows sent, [4] world, [5] exchange (1 IPC, 2 RCCL, 0 none), [6] 1 if a
- * captured hipGraph exists, [7] 0. */
+ * captured hipGraph exists, [7] halo tiers. */
 int wg_dist_info(wg_dist_t D, int64_t* out8_host);
 /* Total time (ms) and count of the halo exchanges (pack + RCCL, or the IPC
  * pull) recorded while profiling was enabled on the shard's handle; resets. */
