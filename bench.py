@@ -93,7 +93,7 @@ def parse():
                          "sharded config only, as 'sharded_<config>_<exchange>'")
     ap.add_argument("--halo-tiers", type=int, default=None,
                     help="sharded runs: halo tiers (1, or 2: the hot halo rows exchanged first and their entries "
-                         "summed while the rest is in flight); default: 2 at N > 1, 1 at N = 1")
+                         "summed while the rest is in flight, with two-phase steps); default 1")
     ap.add_argument("--cold-reps", type=int, default=5,
                     help="chains timed after writing a 512 MiB scratch buffer (cold Infinity Cache / L2); 0 = skip")
     ap.add_argument("--f1-companion", type=int, default=1,
@@ -741,17 +741,6 @@ def main():
                                                     world, rank, device, x, halo_tiers=args.halo_tiers)
             except Exception as exc:  # noqa: BLE001
                 results[f"{cfg}_{x}"] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
-    if mode == "sharded" and world > 1 and args.halo_tiers is None:
-        # the headline's exchange with the halo in one tier: what the two-tier exchange buys
-        cfg = args.scale_config if args.mode == "auto" else args.config
-        try:
-            torch.cuda.empty_cache()
-            results[f"{cfg}_{exchanges[0]}_tiers1"] = run_sharded(cfg, args.K, args.F, args.sharded_steps, 1,
-                                                                  args.seed, args.s, world, rank, device,
-                                                                  exchanges[0], check=False, halo_tiers=1)
-        except Exception as exc:  # noqa: BLE001
-            results[f"{cfg}_{exchanges[0]}_tiers1"] = {"error": f"{type(exc).__name__}: {exc}",
-                                                      "exchange": exchanges[0]}
     if watchdog is not None:
         watchdog.cancel()
     if rank == 0:

@@ -157,6 +157,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value != 0 && value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "fpad must be 0, 4, 8 or 16");
     L->tune.fpad = (int32_t)value;
     return WG_OK;  // launch-time choice (workspace regrows on the next call)
+  } else if (!strcmp(key, "xdelay")) {
+    L->tune.xdelay = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 100000));
+    return WG_OK;  // timing probe of the sharded chain (a captured chain re-captures: tune_gen)
   } else if (!strcmp(key, "overlap")) {
     L->tune.overlap = value ? 1 : 0;
     return WG_OK;  // launch-time choice (a captured chain re-captures: tune_gen)

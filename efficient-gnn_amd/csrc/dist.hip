@@ -136,6 +136,13 @@ __global__ __launch_bounds__(256) void ipc_pull4_kernel(IpcPull p, int slot, int
   }
 }
 
+// timing probe (knob "xdelay"): hold the stream for `ticks` of the 100 MHz constant clock,
+// standing in for link time the one-GPU runs do not have
+__global__ void spin_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 // (signal the previous phase and) wait for the peers; one workgroup
 __global__ void ipc_wait_kernel(IpcPull p, int signal) { ipc_wait(p, signal != 0); }
 
@@ -265,6 +272,16 @@ struct wg_dist_s {
   // The profiling events span the first tier's start to the last tier's end.
   int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot = 0, int tier = -1) {
     const int t0 = tier < 0 ? 0 : tier, t1 = tier < 0 ? tiers - 1 : tier;
+    if (int rc = transfer(ext, sendbuf, F, st, slot, t0, t1)) return rc;
+    if (L->tune.xdelay > 0 && n_halo > 0) {  // timing probe: the tiers' share of the simulated link time
+      const int64_t rows = recv_off[(size_t)(t1 + 1) * world] - recv_off[(size_t)t0 * world];
+      hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, (uint64_t)(100.0 * L->tune.xdelay * rows / n_halo));
+      WG_LAUNCH_CHECK();
+    }
+    return WG_OK;
+  }
+
+  int transfer(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot, int t0, int t1) {
     const bool first = t0 == 0, last = t1 == tiers - 1;
     if (ipc && world == 1) return WG_OK;  // no peers: nothing to wait for or pull
     if (ipc) {

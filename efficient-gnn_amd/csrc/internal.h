@@ -150,8 +150,11 @@ struct Tuning {
   int32_t hub_vidx = 0;      // hub teams: 1 = 16-B column loads, 4 consecutive entries per lane (s26, 8M R-MAT: 1725 vs 1299 us, off)
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
-  int32_t overlap = 1;       // row-sharded chain: two-phase steps overlapping the halo exchange (dist.hip)
+  int32_t overlap = 0;       // row-sharded chain: two-phase steps overlapping the halo exchange (dist.hip);
+                             // off by default: the split costs more than it hides
   int32_t probe = 0;         // timing only: gathers + one output stream, no epilogue (results wrong)
+  int32_t xdelay = 0;        // timing only: microseconds of simulated link time added to each sharded-chain
+                             // exchange (split over the halo tiers by rows; one spinning wave on the stream)
   int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple
 };
 

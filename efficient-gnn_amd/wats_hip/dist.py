@@ -285,10 +285,11 @@ class ShardedWavelet:
     ``exchange="host"``: that collective on host copies (gloo) -- lets several
     ranks share one GPU in tests (RCCL refuses two ranks on one device).
 
-    ``halo_tiers`` (default: 2 with peers, else 1) and ``hot_frac``: the halo
-    in a hot tier (the ``hot_frac`` most referenced halo rows) and a cold one;
-    the native chain exchanges the hot tier first and sums its entries while
-    the cold tier is in flight (:func:`build_halo_plan`, csrc/dist.hip).
+    ``halo_tiers`` (default 1) and ``hot_frac``: the halo in a hot tier (the
+    ``hot_frac`` most referenced halo rows) and a cold one; with two-phase
+    steps (``L.tune(overlap=1)``) the native chain exchanges the hot tier first
+    and sums its entries while the cold tier is in flight
+    (:func:`build_halo_plan`, csrc/dist.hip).
     """
 
     def __init__(self, indptr_local, indices_global, values_local, n_global: int, bounds, group=None,
@@ -317,11 +318,10 @@ class ShardedWavelet:
         w_global = allreduce_column_degree(colsum, diag, group)
         del colsum, diag
         _trace("column degrees done; halo plan")
-        # two halo tiers by default with peers: on R-MAT shards the 10 % most referenced halo
-        # rows carry ~72 % of the halo entries (Reddit-size, 8 ranks), so their
-        # entries run while the other 90 % of the rows are exchanged
+        # one halo tier by default: the hot tier only pays with the two-phase steps (tuning
+        # key "overlap"), which cost more than they hide on the measured shards
         if halo_tiers is None:
-            halo_tiers = 2 if world > 1 else 1
+            halo_tiers = 1
         self.plan = build_halo_plan(indptr_local, indices_global, bounds, group, compute_device=self.device,
                                     col_degree=w_global, tiers=halo_tiers, hot_frac=hot_frac)
         p = self.plan

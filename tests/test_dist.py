@@ -157,6 +157,8 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
         # lds 4 (hub teams) with a 256-column hub: the shard's hub mixes its own top columns
         # with every peer group's (halo groups in descending degree), the rest is gathered
         sw.L.tune(lds=lds, **({"lds_cb": 256} if lds == 4 else {}))
+        if exchange == "ipc":
+            sw.L.tune(overlap=1)   # the two-phase steps (off by default) on every IPC case
         q_path = "u" if (F == 1 and sw.u_len() > 0) else "t"
         rng = np.random.default_rng(0)
         X = rng.standard_normal((g.n, F)).astype(np.float32)
@@ -300,7 +302,7 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers):
     w_ext = np.concatenate([deg, deg[J]])
     L = wats_hip.NormalizedLaplacian(n, torch.from_numpy(g.indptr), torch.from_numpy(cols.astype(np.int32)), None,
                                      n_cols=n + J.size, w_cols=torch.from_numpy(w_ext), device="cuda:0")
-    L.tune(lds=lds)
+    L.tune(lds=lds, overlap=1)   # the two-phase steps (off by default)
     lib = _lib.load()
     dev = torch.device("cuda:0")
     caller = torch.from_numpy(J.astype(np.int32)).to(dev)
