@@ -33,6 +33,15 @@ __global__ void pack_rows_kernel(int64_t n, int64_t F, const int32_t* __restrict
   dst[idx] = src[(int64_t)rows[i] * F + (idx - i * F)];
 }
 
+// received rows i (row-block streaming: received contiguously per (block, peer)) -> halo row pos[i]
+__global__ void unpack_rows_kernel(int64_t n, int64_t F, const int32_t* __restrict__ pos, const float* __restrict__ src,
+                                   float* __restrict__ ext_halo) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * F) return;
+  const int64_t i = idx / F;
+  ext_halo[(int64_t)pos[i] * F + (idx - i * F)] = src[idx];
+}
+
 // ---- one-sided exchange over IPC-mapped peer memory (exchange mode "ipc") ----
 // Each rank exposes one allocation: two slots of its extended vector ([own |
 // halo] rows, ping-pong) and `world` int64 flags.  A rank's flag q holds how
@@ -156,6 +165,17 @@ __global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, i
     if (q != rank) __hip_atomic_store(peer_flags[q] + rank, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The exchange stream at the highest priority: a hardware queue of its own (streams of one
+// priority share the process's few queues round-robin, and two streams on one queue run in
+// submission order -- the exchange would not overlap the step kernels at all), and its
+// small kernels go first when both queues have work.
+hipError_t create_exchange_stream(hipStream_t* out) {
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+    return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(out, hipStreamNonBlocking, greatest);
+}
+
 int nccl_try(ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return WG_OK;
   return fail(WG_ERR_HIP, "%s: %s", what, ncclGetErrorString(r));
@@ -199,6 +219,16 @@ struct wg_dist_s {
   hipStream_t xs = nullptr;   // exchange stream
   hipEvent_t xfork = nullptr, xjoin = nullptr, xtier = nullptr;
   bool overlapped = false;    // the last chain ran two-phase steps
+  // row-block streaming (wg_dist_stream_blocks, RCCL): each step runs as nblk launches over
+  // nnz-balanced blocks of internal rows; block b's rows go to the peers (pack, grouped
+  // send / receive, unpack into the halo) on xs while block b+1 computes on st
+  int nblk = 0;
+  bool streamed = false;                        // the last chain streamed its blocks
+  std::vector<int64_t> blk_rows;                // [nblk + 1] internal row bounds
+  int32_t* bsend_rows = nullptr;                // [n_send] internal ids, grouped by (block, peer)
+  int32_t* brecv_pos = nullptr;                 // [n_halo] halo positions, grouped by (block, sender)
+  std::vector<int64_t> bsend_off, brecv_off;    // [nblk * world + 1]
+  std::vector<hipEvent_t> bev;                  // [nblk] block b's rows final (on st)
   hipGraphExec_t exec = nullptr;
   GraphKey key{};
   int warm = 0;  // eager calls made with the current key (the first builds plans / workspace)
@@ -230,6 +260,9 @@ struct wg_dist_s {
     if (xfork) (void)hipEventDestroy(xfork);
     if (xjoin) (void)hipEventDestroy(xjoin);
     if (xtier) (void)hipEventDestroy(xtier);
+    for (hipEvent_t e : bev) (void)hipEventDestroy(e);
+    (void)hipFree(bsend_rows);
+    (void)hipFree(brecv_pos);
     if (cap) (void)hipStreamDestroy(cap);
     if (xs) (void)hipStreamDestroy(xs);
     (void)hipFree(send_rows);
@@ -339,6 +372,76 @@ struct wg_dist_s {
     return last ? mark(st, false) : WG_OK;
   }
 
+  // block b of the vector ext (own rows of block b final) to the peers, and the peers' block b
+  // rows into ext's halo, on stream xs: pack, one grouped send / receive, unpack
+  int exchange_block(int b, float* ext, float* sendbuf, float* recvbuf, int64_t F, hipStream_t xst) {
+    const size_t g0 = (size_t)b * world, g1 = (size_t)(b + 1) * world;
+    const int64_t s0 = bsend_off[g0], s1 = bsend_off[g1], h0 = brecv_off[g0], h1 = brecv_off[g1];
+    if (b == 0)
+      if (int rc = mark(xst, true)) return rc;
+    if (s1 > s0) {
+      hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)ceil_div((s1 - s0) * F, 256)), dim3(256), 0, xst, s1 - s0, F,
+                         bsend_rows + s0, ext, sendbuf + s0 * F);
+      WG_LAUNCH_CHECK();
+    }
+    if (int rc = nccl_try(ncclGroupStart(), "ncclGroupStart")) return rc;
+    for (int q = 0; q < world; ++q) {
+      const size_t i = g0 + q;
+      const int64_t ns = bsend_off[i + 1] - bsend_off[i], nr = brecv_off[i + 1] - brecv_off[i];
+      if (ns > 0)
+        if (int rc = nccl_try(ncclSend(sendbuf + bsend_off[i] * F, (size_t)(ns * F), ncclFloat32, q, comm, xst),
+                              "ncclSend")) {
+          (void)ncclGroupEnd();
+          return rc;
+        }
+      if (nr > 0)
+        if (int rc = nccl_try(ncclRecv(recvbuf + brecv_off[i] * F, (size_t)(nr * F), ncclFloat32, q, comm, xst),
+                              "ncclRecv")) {
+          (void)ncclGroupEnd();
+          return rc;
+        }
+    }
+    if (int rc = nccl_try(ncclGroupEnd(), "ncclGroupEnd")) return rc;
+    if (h1 > h0) {
+      hipLaunchKernelGGL(unpack_rows_kernel, dim3((unsigned)ceil_div((h1 - h0) * F, 256)), dim3(256), 0, xst, h1 - h0,
+                         F, brecv_pos + h0, recvbuf + h0 * F, ext + n_own * F);
+      WG_LAUNCH_CHECK();
+    }
+    if (L->tune.xdelay > 0 && n_halo > 0) {  // timing probe: the block's share of the simulated link time
+      hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, xst,
+                         (uint64_t)(100.0 * L->tune.xdelay * (double)(h1 - h0) / (double)n_halo));
+      WG_LAUNCH_CHECK();
+    }
+    return b == nblk - 1 ? mark(xst, false) : WG_OK;
+  }
+
+  // A streamed step: launch(st, &ph) per row block; when `out` is exchanged next (not the
+  // chain's last step) block b's rows leave on xs as soon as block b's kernel is done, and st
+  // waits for every block's exchange before the next step.  Hazards: the exchange of block b
+  // reads own rows of `out` block b (final) and writes out's halo rows, which this step does
+  // not touch (it reads `cur` and out's own rows of later blocks); xs issues the blocks in
+  // order after the previous step's kernels (bev[0] follows them on st).
+  template <typename StepFn>
+  int streamed_step(float* out, bool send, float* sendbuf, float* recvbuf, int64_t Fp, hipStream_t st,
+                    StepFn&& launch) {
+    if (!send) return launch(st, nullptr);
+    for (int b = 0; b < nblk; ++b) {
+      if (blk_rows[b + 1] > blk_rows[b]) {
+        PhaseArgs pb;
+        pb.block = b;
+        pb.row_begin = blk_rows[b];
+        pb.row_end = blk_rows[b + 1];
+        if (int rc = launch(st, &pb)) return rc;
+      }
+      WG_HIP_TRY(hipEventRecord(bev[b], st));
+      WG_HIP_TRY(hipStreamWaitEvent(xs, bev[b], 0));
+      if (int rc = exchange_block(b, out, sendbuf, recvbuf, Fp, xs)) return rc;
+    }
+    WG_HIP_TRY(hipEventRecord(xjoin, xs));
+    WG_HIP_TRY(hipStreamWaitEvent(st, xjoin, 0));
+    return WG_OK;
+  }
+
   // One Chebyshev step that gathers from `cur` (own rows final, halo rows to be
   // refreshed): without overlap, exchange then the step; with overlap, phase 1
   // (own-column entries, into `part`) forks onto xs while the exchange runs on
@@ -412,9 +515,14 @@ struct wg_dist_s {
         if (int rc = get_row_split(L, n_own + n_hot, &rsplit2)) return rc;
     }
     overlapped = rsplit != nullptr;
+    // row-block streaming: the gather-kernel path over RCCL with peers, in-kernel split-row combine
+    const bool strm = !lp && !rsplit && nblk > 0 && comm && !ipc && K >= 2 && L->tune.inkernel_combine &&
+                      L->reordered;
+    streamed = strm;
+    const size_t rcv = strm ? ((size_t)std::max<int64_t>(n_halo, 1) * Fp + 63) / 64 * 64 : 0;
     const size_t partf = rsplit ? 2 * own : 0;  // float64 row partials (n_own x Fp doubles)
     const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd + (clen ? own : 0) +
-                        partf;
+                        partf + rcv;
     if (ws_floats < need) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       WG_HIP_TRY(hipStreamIsCapturing(st, &cs));
@@ -461,6 +569,7 @@ struct wg_dist_s {
     float* sint = take(own);
     float* sendbuf = take(snd);
     double* part = rsplit ? reinterpret_cast<double*>(take(partf)) : nullptr;  // 256-B aligned (take rounds)
+    float* recvbuf = strm ? take(rcv) : nullptr;
     int rc = WG_OK;
     if (sig) rc = ipc_wait_only(st);
     if (!rc) rc = launch_permute_pad(L, F, Fp, X0, A[0], st);
@@ -492,22 +601,30 @@ struct wg_dist_s {
         cl.uin = useu && j >= 2;          // j == 1 gathers X0 itself
         cl.uprev = useu && prev_stored;
         cl.uout = useu;                   // ignored on the final step (k == 0 writes S)
-        rc = step_with_exchange(cur, sendbuf, Fp, st, (j - 1) & 1, rsplit, rsplit2, part,
-                                [&](hipStream_t s2, const PhaseArgs* ph) {
-                                  return launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr,
-                                                     k == 0 ? nullptr : A[j & 1], k == 0 ? sint : nullptr, nullptr,
-                                                     1.0, 0.0, s2, false, nullptr, &cl, ph);
-                                });
+        auto launch = [&](hipStream_t s2, const PhaseArgs* ph) {
+          return launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr, k == 0 ? nullptr : A[j & 1],
+                             k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, s2, false, nullptr, &cl, ph);
+        };
+        if (strm) {  // phase 1's exchange (X0) whole; each later one streamed by the step before it
+          if (j == 1) rc = exchange(cur, sendbuf, Fp, st, 0);
+          if (!rc) rc = streamed_step(A[j & 1], k > 0, sendbuf, recvbuf, Fp, st, launch);
+        } else {
+          rc = step_with_exchange(cur, sendbuf, Fp, st, (j - 1) & 1, rsplit, rsplit2, part, launch);
+        }
       }
     } else {
       for (int32_t k = 1; k <= K && !rc; ++k) {
         float* cur = A[(k - 1) & 1];
-        rc = step_with_exchange(cur, sendbuf, Fp, st, (k - 1) & 1, rsplit, rsplit2, part,
-                                [&](hipStream_t s2, const PhaseArgs* ph) {
-                                  return launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr,
-                                                     k == K ? nullptr : A[k & 1], sint, nullptr, 1.0,
-                                                     std::exp(-s * (double)k), s2, false, nullptr, nullptr, ph);
-                                });
+        auto launch = [&](hipStream_t s2, const PhaseArgs* ph) {
+          return launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr,
+                             1.0, std::exp(-s * (double)k), s2, false, nullptr, nullptr, ph);
+        };
+        if (strm) {  // step 1's exchange (T_0) whole; each later one streamed by the step before it
+          if (k == 1) rc = exchange(cur, sendbuf, Fp, st, 0);
+          if (!rc) rc = streamed_step(A[k & 1], k < K, sendbuf, recvbuf, Fp, st, launch);
+        } else {
+          rc = step_with_exchange(cur, sendbuf, Fp, st, (k - 1) & 1, rsplit, rsplit2, part, launch);
+        }
       }
     }
     if (!rc && sig) rc = ipc_signal(st);  // phase K
@@ -579,7 +696,7 @@ int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank,
       rc = fail(WG_ERR_HIP, "wg_dist_create: send_rows copy");
   }
   if (!rc && (hipStreamCreateWithFlags(&D->cap, hipStreamNonBlocking) != hipSuccess ||
-              hipStreamCreateWithFlags(&D->xs, hipStreamNonBlocking) != hipSuccess ||
+              create_exchange_stream(&D->xs) != hipSuccess ||
               hipEventCreateWithFlags(&D->fork, hipEventDisableTiming) != hipSuccess ||
               hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess ||
               hipEventCreateWithFlags(&D->xfork, hipEventDisableTiming) != hipSuccess ||
@@ -638,13 +755,19 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   }
   // eager: profiling (per-step events), graphs disabled, or the first call with
   // these arguments (it builds the kernel plans and the workspace)
-  if (!D->use_graph || D->L->prof || D->warm == 0) {
-    const int rc = D->chain(X0, F, K, s, S, H, st);
-    if (!rc) ++D->warm;
-    return rc;
-  }
+  // streamed chains run eagerly (RCCL on the side stream under capture is not used)
+  // Either way the chain runs on the handle's own non-blocking stream (cap), joined to the
+  // caller's: on the legacy null stream the step kernels would wait for every blocking
+  // stream's work, RCCL's included, and never overlap the exchange stream.
   WG_HIP_TRY(hipEventRecord(D->fork, st));
   WG_HIP_TRY(hipStreamWaitEvent(D->cap, D->fork, 0));
+  if (!D->use_graph || D->L->prof || D->warm == 0 || (D->nblk > 0 && D->comm && !D->ipc)) {
+    const int rc = D->chain(X0, F, K, s, S, H, D->cap);
+    if (!rc) ++D->warm;
+    WG_HIP_TRY(hipEventRecord(D->join, D->cap));
+    WG_HIP_TRY(hipStreamWaitEvent(st, D->join, 0));
+    return rc;
+  }
   if (!D->exec) {
     hipGraph_t g = nullptr;
     WG_HIP_TRY(hipStreamBeginCapture(D->cap, hipStreamCaptureModeRelaxed));
@@ -751,9 +874,118 @@ int wg_dist_status(wg_dist_t D, int32_t* timed_out) {
   return WG_OK;
 }
 
+int wg_dist_stream_blocks(wg_dist_t D, int32_t n_blocks) {
+  if (!D || n_blocks < 0 || n_blocks > 64) return fail(WG_ERR_INVALID, "wg_dist_stream_blocks: bad arguments");
+  wg_laplacian_s* L = D->L;
+  if (n_blocks > 0 && (!D->comm || D->ipc || D->tiers != 1))
+    return fail(WG_ERR_UNSUPPORTED, "wg_dist_stream_blocks: needs the RCCL exchange with one halo tier");
+  if (n_blocks > 0 && !L->reordered)
+    return fail(WG_ERR_UNSUPPORTED, "wg_dist_stream_blocks: the operator's rows are not length-ordered");
+  WG_HIP_TRY(hipDeviceSynchronize());
+  if (D->exec) {
+    (void)hipGraphExecDestroy(D->exec);
+    D->exec = nullptr;
+  }
+  D->warm = 0;
+  for (hipEvent_t e : D->bev) (void)hipEventDestroy(e);
+  D->bev.clear();
+  (void)hipFree(D->bsend_rows);
+  (void)hipFree(D->brecv_pos);
+  D->bsend_rows = nullptr;
+  D->brecv_pos = nullptr;
+  D->nblk = 0;
+  if (n_blocks == 0) return WG_OK;
+  const int world = D->world;
+  const int64_t n = D->n_own;
+  // nnz-balanced blocks of internal rows
+  std::vector<int32_t> rp(n + 1);
+  WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+  std::vector<int64_t> bounds(n_blocks + 1, n);
+  bounds[0] = 0;
+  for (int b = 1; b < n_blocks; ++b) {
+    const int64_t target = (int64_t)rp[n] * b / n_blocks;
+    bounds[b] = std::max<int64_t>(bounds[b - 1], std::lower_bound(rp.begin(), rp.end(), (int32_t)target) - rp.begin());
+    bounds[b] = std::min<int64_t>(bounds[b], n);
+  }
+  auto block_of = [&](int32_t row) {
+    return (int)(std::upper_bound(bounds.begin(), bounds.end(), (int64_t)row) - bounds.begin()) - 1;
+  };
+  // my send rows by (block, peer), stable within each peer's list; their block ids to the peers
+  std::vector<int32_t> srows(D->n_send);
+  if (D->n_send)
+    WG_HIP_TRY(hipMemcpy(srows.data(), D->send_rows, sizeof(int32_t) * D->n_send, hipMemcpyDeviceToHost));
+  std::vector<int32_t> sblk(D->n_send);
+  for (int64_t i = 0; i < D->n_send; ++i) sblk[i] = block_of(srows[i]);
+  const size_t ng = (size_t)n_blocks * world;
+  std::vector<int64_t> scnt(ng, 0), rcnt(ng, 0);
+  std::vector<int32_t> bsend;
+  bsend.reserve(D->n_send);
+  for (int b = 0; b < n_blocks; ++b)
+    for (int q = 0; q < world; ++q) {
+      const int64_t before = (int64_t)bsend.size();
+      for (int64_t i = D->send_off[q]; i < D->send_off[q + 1]; ++i)
+        if (sblk[i] == b) bsend.push_back(srows[i]);
+      scnt[(size_t)b * world + q] = (int64_t)bsend.size() - before;
+    }
+  // the block id of every halo row, from its owner (same order as the owner's send list to me)
+  int32_t* d_sblk = nullptr;
+  int32_t* d_rblk = nullptr;
+  int rc = dmalloc(&d_sblk, (size_t)std::max<int64_t>(1, D->n_send));
+  if (!rc) rc = dmalloc(&d_rblk, (size_t)std::max<int64_t>(1, D->n_halo));
+  if (!rc && D->n_send &&
+      hipMemcpy(d_sblk, sblk.data(), sizeof(int32_t) * D->n_send, hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(WG_ERR_HIP, "wg_dist_stream_blocks: copy");
+  if (!rc) rc = nccl_try(ncclGroupStart(), "ncclGroupStart");
+  for (int q = 0; q < world && !rc; ++q) {
+    if (D->send_cnt[q] > 0)
+      rc = nccl_try(ncclSend(d_sblk + D->send_off[q], (size_t)D->send_cnt[q], ncclInt32, q, D->comm, D->xs), "ncclSend");
+    if (!rc && D->recv_cnt[q] > 0)
+      rc = nccl_try(ncclRecv(d_rblk + D->recv_off[q], (size_t)D->recv_cnt[q], ncclInt32, q, D->comm, D->xs), "ncclRecv");
+  }
+  if (!rc) rc = nccl_try(ncclGroupEnd(), "ncclGroupEnd");
+  std::vector<int32_t> rblk(D->n_halo);
+  if (!rc && hipStreamSynchronize(D->xs) != hipSuccess) rc = fail(WG_ERR_HIP, "wg_dist_stream_blocks: sync");
+  if (!rc && D->n_halo &&
+      hipMemcpy(rblk.data(), d_rblk, sizeof(int32_t) * D->n_halo, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(WG_ERR_HIP, "wg_dist_stream_blocks: copy");
+  (void)hipFree(d_sblk);
+  (void)hipFree(d_rblk);
+  if (rc) return rc;
+  // receive positions by (block, sender), stable within each sender's group (the sender's order)
+  std::vector<int32_t> rpos;
+  rpos.reserve(D->n_halo);
+  for (int b = 0; b < n_blocks; ++b)
+    for (int q = 0; q < world; ++q) {
+      const int64_t before = (int64_t)rpos.size();
+      for (int64_t i = D->recv_off[q]; i < D->recv_off[q + 1]; ++i) {
+        if (rblk[i] < 0 || rblk[i] >= n_blocks)
+          return fail(WG_ERR_INVALID, "wg_dist_stream_blocks: peer %d sent block %d (of %d)", q, rblk[i], n_blocks);
+        if (rblk[i] == b) rpos.push_back((int32_t)i);
+      }
+      rcnt[(size_t)b * world + q] = (int64_t)rpos.size() - before;
+    }
+  D->bsend_off.assign(ng + 1, 0);
+  D->brecv_off.assign(ng + 1, 0);
+  for (size_t i = 0; i < ng; ++i) {
+    D->bsend_off[i + 1] = D->bsend_off[i] + scnt[i];
+    D->brecv_off[i + 1] = D->brecv_off[i] + rcnt[i];
+  }
+  if (D->bsend_off[ng] != D->n_send || D->brecv_off[ng] != D->n_halo)
+    return fail(WG_ERR_INVALID, "wg_dist_stream_blocks: block lists do not cover the exchange");
+  if (int rc2 = dmalloc(&D->bsend_rows, (size_t)std::max<int64_t>(1, D->n_send))) return rc2;
+  if (int rc2 = dmalloc(&D->brecv_pos, (size_t)std::max<int64_t>(1, D->n_halo))) return rc2;
+  if (D->n_send) WG_HIP_TRY(hipMemcpy(D->bsend_rows, bsend.data(), sizeof(int32_t) * D->n_send, hipMemcpyHostToDevice));
+  if (D->n_halo) WG_HIP_TRY(hipMemcpy(D->brecv_pos, rpos.data(), sizeof(int32_t) * D->n_halo, hipMemcpyHostToDevice));
+  D->bev.resize(n_blocks);
+  for (auto& e : D->bev) WG_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  D->blk_rows = bounds;
+  D->nblk = n_blocks;
+  return WG_OK;
+}
+
 int wg_dist_info(wg_dist_t D, int64_t* out) {
   if (!D || !out) return fail(WG_ERR_INVALID, "wg_dist_info: NULL argument");
-  out[0] = D->overlapped ? 1 : 0;
+  out[0] = D->overlapped ? 1 : (D->streamed ? 2 : 0);
   out[1] = D->n_own;
   out[2] = D->n_halo;
   out[3] = D->n_send;

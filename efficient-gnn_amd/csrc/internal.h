@@ -65,6 +65,7 @@ struct ChunkDesc {  // one workgroup's share of a split row
 
 struct Plan {
   SegTable tab{};
+  int64_t row0 = 0, row1 = 0;   // the rows planned (row-block plans: a block of internal rows)
   Seg* d_segs = nullptr;        // device copy of tab.s (read with scalar loads)
   int32_t n_chunks = 0;
   int32_t width = 0;            // LF * VEC doubles per partial
@@ -177,7 +178,8 @@ struct wg_laplacian_s {
   int64_t n_closed = 0;       // purely isolated rows at the end: T_k = (-1)^k X0 (closed form)
   wg::Tuning tune;
   int64_t tune_gen = 0;       // bumped by every wg_laplacian_tune: captured chains (dist.hip) re-capture
-  std::map<int, wg::Plan> plans;  // key: (LF * 8 + VEC) * 2 + active_only
+  std::map<int64_t, wg::Plan> plans;  // key: (LF * 8 + VEC) * 2 + active_only (...); row-block plans: + (block + 1) << 32
+  std::vector<int32_t> h_rowptr;      // host copy of the internal row pointers (row-block plans), lazily
   // unweighted graph (every off-diagonal a_ij == 1): L_hat_ij = -dinv_i dinv_j
   // up to scipy's float32 rounding, so the F == 1 LDS kernel reads no values
   bool unit = false;
@@ -210,7 +212,8 @@ int build_operator(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indi
 int sort_row_columns(wg_laplacian_s* L, hipStream_t stream);
 // step.hip
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
-int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out);
+int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, int block = -1, int64_t r0 = 0,
+             int64_t r1 = 0);
 // S_out (finalize fused into the last step; needs S, H and F within one tile):
 // the rows' final S and H go to caller row perm[row] of S_out / H
 // Clenshaw form of the heat sum (wavelet_features): a step computes
@@ -232,6 +235,10 @@ struct ClenArgs {
 // phase 3 adds the tier-0 entries [rsplit[row], rsplit2[row]) into part (between 1 and 2),
 // and phase 2 sums [rsplit2[row], row end).
 struct PhaseArgs {
+  // row block (phase 0 only): the step on internal rows [row_begin, row_end) alone, with its own
+  // plan (block id `block` >= 0); block < 0 = every row
+  int block = -1;
+  int64_t row_begin = 0, row_end = 0;
   int phase = 0;
   const int32_t* rsplit = nullptr;   // [n_rows] first entry with column >= n_rows (rows column-sorted)
   const int32_t* rsplit2 = nullptr;  // [n_rows] first tier-1 halo entry (two tiers), else nullptr

@@ -765,15 +765,17 @@ __global__ __launch_bounds__(NW * 64) void cheb_step_hub_kernel(StepArgs a, cons
 // Split rows: sum each row's chunk partials in chunk order, then the epilogue.
 // Sub-group of LF lanes per row.
 template <int VEC>
-__global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_split, const int2* __restrict__ rowchunks) {
+__global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_split, const int2* __restrict__ rowchunks,
+                                                         int64_t row0) {
   const int lane = threadIdx.x & 63;
   const int LF = a.LF;
   const int G = 64 / LF;
   const int sg = lane / LF;
   const int fs = lane - sg * LF;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + sg;
-  if (sg >= G || row >= n_split) return;
-  const int2 rc = rowchunks[row];
+  const int64_t lr = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + sg;  // split row of the plan
+  if (sg >= G || lr >= n_split) return;
+  const int2 rc = rowchunks[lr];
+  const int64_t row = row0 + lr;
   const int width = LF * VEC;
   EpiIn<VEC> in;
   if (!to_part(a)) epi_prefetch<VEC>(a, row, fs, in);
@@ -1042,7 +1044,7 @@ int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   if (plan.n_split > 0 && !a.arrivals && ((a.seg_mask >> tab.n) & 1)) {
     const int G = 64 / a.LF;
     hipLaunchKernelGGL(combine_kernel<VEC>, dim3((unsigned)ceil_div(plan.n_split, 4 * G)), dim3(kBlock), 0, stream, a,
-                       plan.n_split, plan.rowchunks);
+                       plan.n_split, plan.rowchunks, plan.row0);
     WG_LAUNCH_CHECK();
   }
   return WG_OK;
@@ -1110,25 +1112,60 @@ void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_it
 //   block rows: len <= 4G*block_iter       (one workgroup per row)
 //   split rows: longer                     (one workgroup per CH = 4G*chunk_iter nnz + combine_kernel)
 // Classification is by power-of-two length bucket (rows are sorted by length).
-int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
+//
+// Row-block plans (block >= 0): the same classification over internal rows [r0, r1) only (the
+// row-sharded chain streams each block's rows to the peers while the next block computes,
+// dist.hip); the block's split rows index rowchunks / arrivals from r0.
+int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, int block, int64_t r0, int64_t r1) {
   active_only = active_only && L->reordered;
   const int NW = (L->tune.waves == 16 || L->tune.waves == 8) ? L->tune.waves : 4;
-  const int key = ((LF * 8 + VEC) * 2 + (active_only ? 1 : 0)) * 32 + NW + (L->tune.hot > 0 ? (1 << 28) : 0);
+  const bool ranged = block >= 0;
+  const int64_t key = (int64_t)(((LF * 8 + VEC) * 2 + (active_only ? 1 : 0)) * 32 + NW +
+                                (L->tune.hot > 0 && !ranged ? (1 << 28) : 0)) +
+                      (ranged ? ((int64_t)(block + 1) << 32) : 0);
   auto it = L->plans.find(key);
-  if (it != L->plans.end()) {
+  if (it != L->plans.end() && (!ranged || (it->second.row0 == r0 && it->second.row1 == r1))) {
     *out = &it->second;
     return WG_OK;
   }
+  if (it != L->plans.end()) {  // the block's rows changed: rebuild
+    it->second.release();
+    L->plans.erase(it);
+  }
+  if (ranged && (!L->reordered || r0 < 0 || r1 > L->n_rows || r1 <= r0))
+    return fail(WG_ERR_INVALID, "row-block plan: rows [%lld, %lld) of %lld (reordered %d)", (long long)r0,
+                (long long)r1, (long long)L->n_rows, (int)L->reordered);
   Plan p;
   p.width = LF * VEC;
   p.nw = NW;
-  if (LF == 1 && VEC == 1 && L->tune.hot > 0)
+  if (LF == 1 && VEC == 1 && L->tune.hot > 0 && !ranged)
     p.hot = (int32_t)std::min<int64_t>({(int64_t)L->tune.hot, L->n_cols, (int64_t)((160 * 1024 - NW * 64 * 8) / 4)});
   const int G = 64 / LF;
   const int64_t n = active_only ? L->n_active : L->n_rows;
   unsigned int bucket[kBuckets];
-  for (int b = 0; b < kBuckets; ++b) bucket[b] = L->bucket[b];
-  bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
+  const int64_t base = ranged ? r0 : 0;  // first row of the plan
+  if (!ranged) {
+    for (int b = 0; b < kBuckets; ++b) bucket[b] = L->bucket[b];
+    bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
+  } else {
+    // the block's rows by length bucket (internal rows are in descending length: each bucket's
+    // rows of the block are contiguous, in descending bucket order)
+    if ((int64_t)L->h_rowptr.size() != L->n_rows + 1) {
+      L->h_rowptr.resize(L->n_rows + 1);
+      WG_HIP_TRY(hipMemcpy(L->h_rowptr.data(), L->rowptr, sizeof(int32_t) * (L->n_rows + 1), hipMemcpyDeviceToHost));
+    }
+    for (int b = 0; b < kBuckets; ++b) bucket[b] = 0;
+    int prev = kBuckets;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int32_t l = L->h_rowptr[r + 1] - L->h_rowptr[r];
+      const int b = (l > 1) ? 32 - __builtin_clz((unsigned)(l - 1)) : 0;
+      if (b > prev) return fail(WG_ERR_INVALID, "row-block plan: rows not in descending length at %lld", (long long)r);
+      prev = b;
+      ++bucket[b];
+    }
+  }
+  p.row0 = base;
+  p.row1 = ranged ? r1 : n;
   int iter, block_iter, chunk_iter;
   default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter);
   const int64_t team_max = (int64_t)G * iter;
@@ -1160,7 +1197,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
   int32_t blk = 0;
   if (n_split > 0) {
     std::vector<int32_t> rp(n_split + 1);
-    WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n_split + 1), hipMemcpyDeviceToHost));
+    WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr + base, sizeof(int32_t) * (n_split + 1), hipMemcpyDeviceToHost));
     std::vector<ChunkDesc> ch;
     std::vector<int2> rc(n_split);
     for (int64_t r = 0; r < n_split; ++r) {
@@ -1169,7 +1206,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
       rc[r] = make_int2((int)ch.size(), cnt);
       for (int q = 0; q < cnt; ++q) {
         ChunkDesc d{};
-        d.row = (int32_t)r;
+        d.row = (int32_t)(base + r);
         d.e0 = (int32_t)(rp[r] + q * CH);
         d.e1 = (int32_t)std::min<int64_t>(rp[r + 1], rp[r] + (q + 1) * CH);
         ch.push_back(d);
@@ -1190,18 +1227,18 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out) {
     WG_HIP_TRY(hipMemcpy(p.rowchunks, rc.data(), sizeof(int2) * rc.size(), hipMemcpyHostToDevice));
     t.s[nseg++] = Seg{0, p.n_chunks, 0, G, 2};
     blk = p.n_chunks;
-    snprintf(buf, sizeof(buf), "split rows[0,%lld) chunks=%d CH=%lld (+combine)\n", (long long)n_split, p.n_chunks,
-             (long long)CH);
+    snprintf(buf, sizeof(buf), "split rows[%lld,%lld) chunks=%d CH=%lld (+combine)\n", (long long)base,
+             (long long)(base + n_split), p.n_chunks, (long long)CH);
     p.text += buf;
   }
   if (n_block > 0) {
-    t.s[nseg++] = Seg{(int32_t)n_split, (int32_t)(n_split + n_block), blk, G, 1};
+    t.s[nseg++] = Seg{(int32_t)(base + n_split), (int32_t)(base + n_split + n_block), blk, G, 1};
     blk += (int32_t)n_block;
-    snprintf(buf, sizeof(buf), "block rows[%lld,%lld) (workgroup per row)\n", (long long)n_split,
-             (long long)(n_split + n_block));
+    snprintf(buf, sizeof(buf), "block rows[%lld,%lld) (workgroup per row)\n", (long long)(base + n_split),
+             (long long)(base + n_split + n_block));
     p.text += buf;
   }
-  int32_t row = (int32_t)(n_split + n_block);
+  int32_t row = (int32_t)(base + n_split + n_block);
   const int first_team = nseg;
   for (int b = kBuckets - 1; b >= 0; --b) {
     const int32_t cnt = (int32_t)bucket[b];
@@ -1259,6 +1296,8 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out,
                 const ClenArgs* cl, const PhaseArgs* ph) {
   if (L->n_rows == 0) return WG_OK;
+  if (ph && ph->block >= 0 && (ph->phase != 0 || H || S_out))
+    return fail(WG_ERR_INVALID, "launch_step: a row-block step is a plain step without H or fused finalize");
   if (ph && ph->phase != 0 && (!ph->rsplit || !ph->part || S_out || (ph->phase == 3 && !ph->rsplit2)))
     return fail(WG_ERR_INVALID, "launch_step: a phased step needs rsplit (phase 3: rsplit2), part, no fused finalize");
   if (int rc = prof_mark(L, stream, true)) return rc;
@@ -1271,7 +1310,9 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     const int64_t fw = std::min<int64_t>(max_tile, F - f0);
     const int LF = (int)(fw / vec);
     Plan* plan = nullptr;
-    int rc = get_plan(L, LF, vec, active_only, &plan);
+    const bool ranged = ph && ph->block >= 0;
+    int rc = ranged ? get_plan(L, LF, vec, false, &plan, ph->block, ph->row_begin, ph->row_end)
+                    : get_plan(L, LF, vec, active_only, &plan);
     if (rc) return rc;
     StepArgs a{};
     a.rowptr = L->rowptr;
@@ -1318,8 +1359,9 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     if (a.probe && !a.xk) a.xk = S ? S + f0 : nullptr;  // the final step of a chain stores into S
     a.chunks = plan->chunks;
     a.partial = plan->partial;
-    a.rowchunks = plan->rowchunks;
-    a.arrivals = (L->tune.inkernel_combine && plan->n_split > 0) ? plan->arrivals : nullptr;
+    // split rows index rowchunks / arrivals by internal row; a row-block plan's start at row0
+    a.rowchunks = plan->rowchunks ? plan->rowchunks - plan->row0 : nullptr;
+    a.arrivals = (L->tune.inkernel_combine && plan->n_split > 0) ? plan->arrivals - plan->row0 : nullptr;
     a.seg_mask = L->tune.seg_mask;
     // non-temporal T_k / S stores only for large per-step streams (ogbn-arxiv F=40, 30 MB of
     // T_k + S per step: 40.6 us plain vs 42.0 nt; F=64, 48 MB: 55.3 vs 56.5; Reddit-size F=44,
@@ -1334,7 +1376,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     a.xm1_bytes = (L->n_cols * F - f0) * (int64_t)sizeof(float);
     a.gbuf = (L->tune.gbuf && a.xm1_bytes < ((int64_t)1 << 31)) ? 1 : 0;
     // hub rows: LDS = (hubf + 1) * tile + the block-mode buffer (NW*64*VEC doubles) <= 160 KiB
-    a.hubf = (vec == 4 && a.xm1_bytes < ((int64_t)1 << 31))
+    a.hubf = (vec == 4 && a.xm1_bytes < ((int64_t)1 << 31) && !ranged)
                  ? (int32_t)std::min<int64_t>({(int64_t)L->tune.hubf, L->n_cols,
                                                (int64_t)((160 * 1024 - 64 - plan->nw * 64 * vec * 8) /
                                                          (LF * vec * 4)) - 1})

@@ -285,6 +285,10 @@ class ShardedWavelet:
     ``exchange="host"``: that collective on host copies (gloo) -- lets several
     ranks share one GPU in tests (RCCL refuses two ranks on one device).
 
+    ``stream_blocks`` (``exchange="rccl"``): run each step as that many
+    launches over nnz-balanced row blocks and send every block's rows while
+    the next block computes (``wg_dist_stream_blocks``; 0 = off).
+
     ``halo_tiers`` (default 1) and ``hot_frac``: the halo in a hot tier (the
     ``hot_frac`` most referenced halo rows) and a cold one; with two-phase
     steps (``L.tune(overlap=1)``) the native chain exchanges the hot tier first
@@ -294,7 +298,7 @@ class ShardedWavelet:
 
     def __init__(self, indptr_local, indices_global, values_local, n_global: int, bounds, group=None,
                  exchange: str = "rccl", device=None, max_features: int = 1, halo_tiers=None,
-                 hot_frac: float = 0.1):
+                 hot_frac: float = 0.1, stream_blocks: int = 0):
         from .laplacian import NormalizedLaplacian, require_gpu
         self.device = require_gpu(device)
         self.group = group
@@ -341,8 +345,14 @@ class ShardedWavelet:
         self.profile = False          # record (exchange, step) event pairs per Chebyshev step
         self.events = []
         self._dist = None
+        self.stream_blocks = 0
         if exchange == "rccl":
             self._dist = self._create_native()
+            if stream_blocks and p.tiers == 1:
+                # row-block streaming (collective): each step's exchange trails its compute by a block
+                with torch.cuda.device(self.device):
+                    check(lib.wg_dist_stream_blocks(self._dist, int(stream_blocks)), "dist_stream_blocks")
+                self.stream_blocks = int(stream_blocks)
         elif exchange == "ipc":
             # the shared region is sized for max_features columns (large IPC
             # mappings are slow to set up: keep it to what the chain uses); a
@@ -492,8 +502,12 @@ class ShardedWavelet:
         # two-phase (overlapped) steps record two launches per Chebyshev step (three with
         # two halo tiers)
         inf = self.info()
-        per_step = (3 if inf.get("tiers", 1) == 2 else 2) if inf.get("overlapped") else 1
-        n = max(1, st["launches"] // per_step)
+        if inf.get("overlap_mode") == "blocks":   # K - 1 streamed steps of stream_blocks launches + the last
+            n = 1 + max(0, round((st["launches"] - 1) / self.stream_blocks))
+            per_step = 2
+        else:
+            per_step = (3 if inf.get("tiers", 1) == 2 else 2) if inf.get("overlapped") else 1
+            n = max(1, st["launches"] // per_step)
         return dict(exchange_ms=sum(ex) / max(1, len(ex)), step_ms=st["sum_ms"] / n, max_step_ms=st["max_ms"],
                     launches=st["launches"], overlapped=per_step > 1)
 
@@ -507,6 +521,7 @@ class ShardedWavelet:
         check(_lib.load().wg_dist_info(self._dist, out), "dist_info")
         keys = ("overlapped", "n_own", "n_halo", "n_send", "world", "exchange", "captured", "tiers")
         d = dict(zip(keys, [int(v) for v in out]))
+        d["overlap_mode"] = {0: "none", 1: "phases", 2: "blocks"}.get(d["overlapped"], "?")
         d["overlapped"] = bool(d["overlapped"])
         d["exchange"] = {1: "ipc", 2: "rccl"}.get(d["exchange"], "none")
         return d

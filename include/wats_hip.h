@@ -273,13 +273,22 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
 int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world, int32_t tiers,
                           const int32_t* send_rows, const int64_t* send_counts_host,
                           const int64_t* recv_counts_host, wg_dist_t* out);
+/* Row-block streaming (RCCL exchange, one halo tier; collective): each
+ * Chebyshev step of the gather-kernel chain runs as n_blocks launches over
+ * nnz-balanced blocks of the shard's rows, and block b's rows are sent to the
+ * peers (pack, grouped send / receive, unpack into the halo) on a second
+ * stream while block b+1 computes, so a step's exchange trails its compute by
+ * one block.  Streamed chains run eagerly (no hipGraph).  n_blocks = 0: off.
+ * Every rank passes the same n_blocks. */
+int wg_dist_stream_blocks(wg_dist_t D, int32_t n_blocks);
 int wg_dist_destroy(wg_dist_t D);
 int wg_dist_set_graph(wg_dist_t D, int32_t enable);
 int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K, double s, float* S,
                              float* H, void* stream);
-/* State of the sharded chain, out8_host: [0] 1 if the last chain overlapped
- * each step's halo exchange with the step's own-column half (two-phase
- * steps: 2 step launches per Chebyshev step), [1] own rows, [2] halo rows,
+/* State of the sharded chain, out8_host: [0] how the last chain overlapped
+ * its halo exchanges: 0 not, 1 with each step's own-column half (two-phase
+ * steps: 2 step launches per Chebyshev step), 2 streamed row blocks
+ * (wg_dist_stream_blocks), [1] own rows, [2] halo rows,
  * [3] rows sent, [4] world, [5] exchange (1 IPC, 2 RCCL, 0 none), [6] 1 if a
  * captured hipGraph exists, [7] halo tiers. */
 int wg_dist_info(wg_dist_t D, int64_t* out8_host);

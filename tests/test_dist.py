@@ -275,16 +275,22 @@ def test_native_chain_clenshaw_small_orders(K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,lds,graph,tiers", [(1, 2, 1, 1), (1, 0, 1, 1), (8, 3, 1, 1), (8, 3, 0, 1), (40, 3, 1, 1),
-                                               (40, 3, 1, 2), (8, 3, 0, 2), (1, 0, 1, 2), (1, 2, 1, 2)])
-def test_native_chain_loopback_exchange(F, lds, graph, tiers):
+@pytest.mark.parametrize("F,lds,graph,tiers,blocks,clen", [
+    (1, 2, 1, 1, 0, 1), (1, 0, 1, 1, 0, 1), (8, 3, 1, 1, 0, 1), (8, 3, 0, 1, 0, 1), (40, 3, 1, 1, 0, 1),
+    (40, 3, 1, 2, 0, 1), (8, 3, 0, 2, 0, 1), (1, 0, 1, 2, 0, 1), (1, 2, 1, 2, 0, 1),
+    (40, 3, 1, 1, 4, 1), (8, 3, 1, 1, 3, 0), (1, 0, 1, 1, 4, 1), (1, 0, 1, 1, 2, 0), (1, 2, 1, 1, 4, 1),
+    (12, 3, 1, 1, 1, 1)])
+def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen):
     """The native exchange with real RCCL traffic on one GPU: a one-rank shard
     whose column space is [own | halo] where the halo columns are copies of own
     rows (every entry (i, j) with j % 3 == 0 and (i + j) odd reads the copy).
     Per step the pack kernel + ncclSend/ncclRecv to self must refresh the
     copies, so the result equals the unsharded chain.  tiers = 2: the first
     third of the copies is tier 0 (exchanged first, its entries summed by a
-    third step launch while tier 1 is in flight)."""
+    third step launch while tier 1 is in flight).  blocks > 0: row-block
+    streaming (each step in `blocks` launches, every block's rows sent while
+    the next computes; wg_dist_stream_blocks), with the Clenshaw or the
+    forward chain."""
     import ctypes
     import wats_hip
     from wats_hip import _lib
@@ -302,7 +308,8 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers):
     w_ext = np.concatenate([deg, deg[J]])
     L = wats_hip.NormalizedLaplacian(n, torch.from_numpy(g.indptr), torch.from_numpy(cols.astype(np.int32)), None,
                                      n_cols=n + J.size, w_cols=torch.from_numpy(w_ext), device="cuda:0")
-    L.tune(lds=lds, overlap=1)   # the two-phase steps (off by default)
+    # the two-phase steps (off by default) unless the rows are streamed in blocks
+    L.tune(lds=lds, overlap=0 if blocks else 1, clenshaw=clen)
     lib = _lib.load()
     dev = torch.device("cuda:0")
     caller = torch.from_numpy(J.astype(np.int32)).to(dev)
@@ -315,6 +322,8 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers):
     h = ctypes.c_void_p()
     check(lib.wg_dist_create_tiered(L.handle, uid, 0, 1, tiers, ptr(internal), counts.ctypes.data,
                                     counts.ctypes.data, ctypes.byref(h)), "dist_create")
+    if blocks:
+        check(lib.wg_dist_stream_blocks(h, blocks), "stream_blocks")
     try:
         check(lib.wg_dist_set_graph(h, graph), "set_graph")
         rng = np.random.default_rng(4)
@@ -333,8 +342,9 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers):
         assert_parity(res[0], ref["S"], what=f"loopback F={F} lds={lds} graph={graph}")
         info = (ctypes.c_int64 * 8)()
         check(lib.wg_dist_info(h, info), "dist_info")
-        # the gather-kernel path overlaps the RCCL exchange with the own-column half of each step
-        assert info[0] == (1 if (F > 1 or lds == 0) else 0), list(info)
+        # the gather-kernel path overlaps the RCCL exchange with the own-column half of each step,
+        # or streams its row blocks
+        assert info[0] == ((2 if blocks else 1) if (F > 1 or lds == 0) else 0), list(info)
         assert info[7] == tiers, list(info)
         L.profile_enable(True)
         check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")

@@ -15,6 +15,7 @@ import argparse
 import ctypes
 import os
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "efficient-gnn_amd"))
@@ -64,6 +65,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--graph", type=int, default=1, help="replay the chain as a hipGraph (1) or run it eagerly (0)")
     ap.add_argument("--tiers", default="1,2")
+    ap.add_argument("--blocks", default="", help="comma-separated row-block counts to time streamed (tiers 1)")
     a = ap.parse_args()
     n, nnz_t, K, _ = NAMED_CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -96,7 +98,11 @@ def main():
         H = torch.empty(n_own, a.F, device=dev)
         print(f"tiers {tiers}: shard {a.rank}/{a.world} rows {n_own} halo {halo.size} (tier rows {counts.tolist()}) "
               f"nnz {L.nnz}", flush=True)
-        for overlap in (0, 1):
+        modes = [(o, 0) for o in (0, 1)]
+        if tiers == 1 and a.blocks:
+            modes += [(0, int(x)) for x in a.blocks.split(",")]
+        for overlap, nb in modes:
+            check(lib.wg_dist_stream_blocks(h, nb), "stream_blocks")
             for d in delays:
                 L.tune(overlap=overlap, xdelay=d)
                 run = lambda: check(lib.wg_dist_wavelet_features(h, ptr(X), a.F, K, 0.8, ptr(S), ptr(H), st),
@@ -106,15 +112,17 @@ def main():
                 torch.cuda.synchronize()
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
                 ev[0].record()
+                t0 = time.perf_counter()
                 for i in range(a.reps):
                     run()
                     ev[i + 1].record()
+                host_ms = (time.perf_counter() - t0) * 1e3 / a.reps
                 torch.cuda.synchronize()
                 ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(a.reps))[a.reps // 2]
                 info = (ctypes.c_int64 * 8)()
                 check(lib.wg_dist_info(h, info), "dist_info")
-                r = dict(tiers=tiers, overlap=overlap, xdelay_us=d, chain_ms=ms, us_per_step=ms * 1e3 / K,
-                         overlapped=int(info[0]))
+                r = dict(tiers=tiers, overlap=overlap, blocks=nb, xdelay_us=d, chain_ms=ms, us_per_step=ms * 1e3 / K,
+                         overlapped=int(info[0]), host_ms_per_chain=host_ms)
                 if not a.graph and d == 0:   # eager: the step launches' own durations (every phase)
                     L.profile_enable(True)
                     run()
@@ -127,11 +135,12 @@ def main():
         lib.wg_dist_destroy(h)
         L.close()
         torch.cuda.empty_cache()
-    base = {(r["tiers"], r["overlap"]): r["us_per_step"] for r in res if r["xdelay_us"] == 0}
+    base = {(r["tiers"], r["overlap"], r["blocks"]): r["us_per_step"] for r in res if r["xdelay_us"] == 0}
     print("exposed exchange (us per step over xdelay = 0):")
     for r in res:
-        print(f"  tiers {r['tiers']} overlap {r['overlap']} xdelay {r['xdelay_us']:4d}: "
-              f"{r['us_per_step']:8.1f} us/step, exposed {r['us_per_step'] - base[(r['tiers'], r['overlap'])]:7.1f}")
+        b0 = base[(r["tiers"], r["overlap"], r["blocks"])]
+        print(f"  tiers {r['tiers']} overlap {r['overlap']} blocks {r['blocks']} xdelay {r['xdelay_us']:4d}: "
+              f"{r['us_per_step']:8.1f} us/step, exposed {r['us_per_step'] - b0:7.1f}")
 
 
 if __name__ == "__main__":
