@@ -157,6 +157,12 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value != 0 && value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "fpad must be 0, 4, 8 or 16");
     L->tune.fpad = (int32_t)value;
     return WG_OK;  // launch-time choice (workspace regrows on the next call)
+  } else if (!strcmp(key, "cu_reserve")) {
+    L->tune.cu_reserve = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 128));
+    return WG_OK;  // sharded chain: CUs kept free of the step kernels (the exchange stream's)
+  } else if (!strcmp(key, "xskip")) {
+    L->tune.xskip = value ? 1 : 0;
+    return WG_OK;  // timing probe only: streamed blocks skip pack / RCCL / unpack (results wrong)
   } else if (!strcmp(key, "xdelay")) {
     L->tune.xdelay = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 100000));
     return WG_OK;  // timing probe of the sharded chain (a captured chain re-captures: tune_gen)

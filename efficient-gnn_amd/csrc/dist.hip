@@ -214,6 +214,7 @@ struct wg_dist_s {
   size_t ws_floats = 0;
   bool use_graph = true;
   hipStream_t cap = nullptr;  // capture / replay stream (the caller's may be the null stream)
+  int cap_reserve = 0;        // CUs masked off cap (tuning key "cu_reserve")
   hipEvent_t fork = nullptr, join = nullptr;
   // exchange overlapped with the own-column half of each step (two-phase steps, step.hip)
   hipStream_t xs = nullptr;   // exchange stream
@@ -377,8 +378,16 @@ struct wg_dist_s {
   int exchange_block(int b, float* ext, float* sendbuf, float* recvbuf, int64_t F, hipStream_t xst) {
     const size_t g0 = (size_t)b * world, g1 = (size_t)(b + 1) * world;
     const int64_t s0 = bsend_off[g0], s1 = bsend_off[g1], h0 = brecv_off[g0], h1 = brecv_off[g1];
-    if (b == 0)
+    if (b == nblk - 1)  // blocks go last first
       if (int rc = mark(xst, true)) return rc;
+    if (L->tune.xskip) {  // timing probe: the simulated link time alone
+      if (L->tune.xdelay > 0 && n_halo > 0) {
+        hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, xst,
+                           (uint64_t)(100.0 * L->tune.xdelay * (double)(h1 - h0) / (double)n_halo));
+        WG_LAUNCH_CHECK();
+      }
+      return b == 0 ? mark(xst, false) : WG_OK;
+    }
     if (s1 > s0) {
       hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)ceil_div((s1 - s0) * F, 256)), dim3(256), 0, xst, s1 - s0, F,
                          bsend_rows + s0, ext, sendbuf + s0 * F);
@@ -412,7 +421,7 @@ struct wg_dist_s {
                          (uint64_t)(100.0 * L->tune.xdelay * (double)(h1 - h0) / (double)n_halo));
       WG_LAUNCH_CHECK();
     }
-    return b == nblk - 1 ? mark(xst, false) : WG_OK;
+    return b == 0 ? mark(xst, false) : WG_OK;
   }
 
   // A streamed step: launch(st, &ph) per row block; when `out` is exchanged next (not the
@@ -425,7 +434,10 @@ struct wg_dist_s {
   int streamed_step(float* out, bool send, float* sendbuf, float* recvbuf, int64_t Fp, hipStream_t st,
                     StepFn&& launch) {
     if (!send) return launch(st, nullptr);
-    for (int b = 0; b < nblk; ++b) {
+    // last block first: internal rows are in descending length, so the last nnz-balanced block
+    // holds most of the rows (most of the rows sent) and the first the fewest -- computed last,
+    // its small exchange is the one left exposed (r02_s23 kernel trace)
+    for (int b = nblk - 1; b >= 0; --b) {
       if (blk_rows[b + 1] > blk_rows[b]) {
         PhaseArgs pb;
         pb.block = b;
@@ -743,6 +755,31 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   if (!D->comm && !D->ipc && (D->n_send > 0 || D->n_halo > 0 || D->world > 1))
     return fail(WG_ERR_INVALID, "wg_dist_wavelet_features: no exchange (no RCCL id given and IPC not connected)");
   hipStream_t st = as_stream(stream_);
+  if (D->cap_reserve != D->L->tune.cu_reserve) {
+    // the compute stream with `cu_reserve` CUs (spread over the chip) masked off, so the exchange
+    // stream's kernels find free CUs while a step kernel's backlog is dispatched
+    WG_HIP_TRY(hipDeviceSynchronize());
+    if (D->exec) {
+      (void)hipGraphExecDestroy(D->exec);
+      D->exec = nullptr;
+    }
+    (void)hipStreamDestroy(D->cap);
+    D->cap = nullptr;
+    const int r = D->L->tune.cu_reserve;
+    int dev = 0, n_cu = 0;
+    WG_HIP_TRY(hipGetDevice(&dev));
+    WG_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    if (r > 0 && r < n_cu) {
+      std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
+      for (int c = 0; c < n_cu; ++c)
+        if ((int64_t)(c + 1) * r / n_cu == (int64_t)c * r / n_cu) mask[c / 32] |= 1u << (c % 32);
+      WG_HIP_TRY(hipExtStreamCreateWithCUMask(&D->cap, (uint32_t)mask.size(), mask.data()));
+    } else {
+      WG_HIP_TRY(hipStreamCreateWithFlags(&D->cap, hipStreamNonBlocking));
+    }
+    D->cap_reserve = r;
+    D->warm = 0;
+  }
   const GraphKey key{X0, S, H, F, K, s, D->L->tune_gen};
   if (!(key == D->key)) {
     if (D->exec) {

@@ -154,6 +154,8 @@ struct Tuning {
   int32_t overlap = 0;       // row-sharded chain: two-phase steps overlapping the halo exchange (dist.hip);
                              // off by default: the split costs more than it hides
   int32_t probe = 0;         // timing only: gathers + one output stream, no epilogue (results wrong)
+  int32_t cu_reserve = 0;    // sharded chain: CUs masked off the compute stream (left to the exchange)
+  int32_t xskip = 0;         // timing only: streamed row blocks skip their pack / RCCL / unpack
   int32_t xdelay = 0;        // timing only: microseconds of simulated link time added to each sharded-chain
                              // exchange (split over the halo tiers by rows; one spinning wave on the stream)
   int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple

@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--graph", type=int, default=1, help="replay the chain as a hipGraph (1) or run it eagerly (0)")
     ap.add_argument("--tiers", default="1,2")
     ap.add_argument("--blocks", default="", help="comma-separated row-block counts to time streamed (tiers 1)")
+    ap.add_argument("--xskip", type=int, default=0, help="streamed blocks: the simulated link time only (no RCCL)")
+    ap.add_argument("--cu-reserve", type=int, default=0, help="CUs masked off the step kernels' stream")
     a = ap.parse_args()
     n, nnz_t, K, _ = NAMED_CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -104,7 +106,7 @@ def main():
         for overlap, nb in modes:
             check(lib.wg_dist_stream_blocks(h, nb), "stream_blocks")
             for d in delays:
-                L.tune(overlap=overlap, xdelay=d)
+                L.tune(overlap=overlap, xdelay=d, xskip=a.xskip if nb else 0, cu_reserve=a.cu_reserve)
                 run = lambda: check(lib.wg_dist_wavelet_features(h, ptr(X), a.F, K, 0.8, ptr(S), ptr(H), st),
                                     "dist_wavelet_features")
                 for _ in range(3):
@@ -138,7 +140,7 @@ def main():
     base = {(r["tiers"], r["overlap"], r["blocks"]): r["us_per_step"] for r in res if r["xdelay_us"] == 0}
     print("exposed exchange (us per step over xdelay = 0):")
     for r in res:
-        b0 = base[(r["tiers"], r["overlap"], r["blocks"])]
+        b0 = base.get((r["tiers"], r["overlap"], r["blocks"]), float("nan"))
         print(f"  tiers {r['tiers']} overlap {r['overlap']} blocks {r['blocks']} xdelay {r['xdelay_us']:4d}: "
               f"{r['us_per_step']:8.1f} us/step, exposed {r['us_per_step'] - b0:7.1f}")
 
