@@ -61,7 +61,7 @@ for part in $PARTS; do
     rehearse2)
       WATS_BENCH_PG=gloo WATS_BENCH_DEVICE=0 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
         --nproc-per-node=2 --master-addr=127.0.0.1 --master-port=29611 bench.py --gpus 2 --exchange ipc \
-        --sharded-extra reddit,rmat-8m --out "$OUT/rehearse2.json" > "$OUT/rehearse2.log" 2>&1
+        --sharded-extra reddit --out "$OUT/rehearse2.json" > "$OUT/rehearse2.log" 2>&1
       fatal rehearse2 $?
       ;;
     *)
