@@ -114,6 +114,8 @@ struct Lds1Plan {
   // ranges; the kernel reads remapped columns hcol (hub column -> its LDS slot, any
   // other column c -> c + hub, gathered from u[c])
   int32_t* hcol = nullptr;    // device [nnz + 4]
+  int32_t* hsplit = nullptr;  // device [n]: first entry of each row with column >= hub (plain hub: the
+                              // hub columns are each row's prefix, rows column-sorted)
   int4* hranges = nullptr;    // device [n_hranges]: {u begin, LDS slot begin, length, 0}
   int32_t n_hranges = 0;
   std::string text;
@@ -155,7 +157,9 @@ struct Tuning {
                              // off by default: the split costs more than it hides
   int32_t probe = 0;         // timing only: gathers + one output stream, no epilogue (results wrong)
   int32_t cu_reserve = 0;    // sharded chain: CUs masked off the compute stream (left to the exchange)
-  int32_t xskip = 0;         // timing only: streamed row blocks skip their pack / RCCL / unpack
+  int32_t xskip = 0;
+  int32_t hub_split = 1;     // hub teams on column-sorted rows: hub prefix and tail in separate loops
+  int32_t probe_colmask = 0; // timing only: hub teams fold tail columns into a 2^k-column window (results wrong)         // timing only: streamed row blocks skip their pack / RCCL / unpack
   int32_t xdelay = 0;        // timing only: microseconds of simulated link time added to each sharded-chain
                              // exchange (split over the halo tiers by rows; one spinning wave on the stream)
   int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple

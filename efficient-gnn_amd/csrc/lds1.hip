@@ -53,6 +53,8 @@ struct Lds1Args {
   int32_t gshift;       // mode 4: a tail column c (>= hub) is gathered from u[c - gshift] (0, or hub on a shard)
   int32_t n_hranges;    // mode 4 on a shard: LDS slots filled from these ranges of u (0: slots = u[0, hub))
   const int4* hranges;
+  const int32_t* hsplit;  // mode 4, plain hub: first tail entry of each row (nullable)
+  int32_t colmask;      // timing probe (knob "probe_colmask"): tail columns folded into [hub, hub + colmask]
   const int2* groups;
   const int4* wgs;
   const float* u_in;   // u_{k-1}, n_cols (padded to a multiple of 32)
@@ -189,7 +191,9 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   const int32_t* __restrict__ col = a.gcol;
   const int32_t* __restrict__ rp = a.brp;
   const int32_t gs = a.gshift;
+  const int32_t cm = a.colmask;
   auto x_of = [&](int32_t c) {
+    if (cm) c = c >= H ? H + ((c - H) & cm) : c;  // timing probe only (results wrong)
     const float xl = u[min(c, H)];
     const uint32_t off = c >= H ? (uint32_t)(c - gs) * 4u : kDrop;
     const float xg = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
@@ -213,7 +217,11 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
       const int32_t e0 = rp[row], e1 = rp[row + 1];
       for (int32_t qq = (e0 & ~3) + 4 * q; qq < e1; qq += 4 * ln) {
         const int4 c4 = *reinterpret_cast<const int4*>(col + qq);
-        const int32_t cc[4] = {c4.x, c4.y, c4.z, c4.w};
+        int32_t cc[4] = {c4.x, c4.y, c4.z, c4.w};
+        if (cm) {  // timing probe only (results wrong)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cc[j] = cc[j] >= H ? H + ((cc[j] - H) & cm) : cc[j];
+        }
         float x[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -225,6 +233,35 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc += (double)x[j];
       }
+    } else if (act && a.hsplit) {
+      // hub columns are each row's prefix [e0, es): LDS reads only, then the tail with global
+      // loads only -- no dropped-offset loads through the address path for hub entries and
+      // no LDS reads for tail ones; each lane adds its entries in the same order as x_of's loop
+      const int32_t e1 = rp[row + 1];
+      const int32_t es = a.hsplit[row];
+      int32_t e = rp[row] + q;
+      for (; e + 3 * ln < es; e += 4 * ln) {
+        const int32_t c0 = col[e], c1 = col[e + ln], c2 = col[e + 2 * ln], c3 = col[e + 3 * ln];
+        const float x0 = u[c0], x1 = u[c1], x2 = u[c2], x3 = u[c3];
+        acc += (double)x0;
+        acc += (double)x1;
+        acc += (double)x2;
+        acc += (double)x3;
+      }
+      for (; e < es; e += ln) acc += (double)u[col[e]];
+      auto xg = [&](int32_t c) {
+        if (cm) c = H + ((c - H) & cm);  // timing probe only (results wrong)
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(c - gs) * 4u, 0, 0));
+      };
+      for (; e + 3 * ln < e1; e += 4 * ln) {
+        const int32_t c0 = col[e], c1 = col[e + ln], c2 = col[e + 2 * ln], c3 = col[e + 3 * ln];
+        const float x0 = xg(c0), x1 = xg(c1), x2 = xg(c2), x3 = xg(c3);
+        acc += (double)x0;
+        acc += (double)x1;
+        acc += (double)x2;
+        acc += (double)x3;
+      }
+      for (; e < e1; e += ln) acc += (double)xg(col[e]);
     } else if (act) {
       const int32_t e1 = rp[row + 1];
       int32_t e = rp[row] + q;
@@ -243,6 +280,20 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   }
 }
 
+
+// first entry of each row whose column is >= hub (rows sorted by column)
+__global__ void hub_split_kernel(int32_t n, int32_t hub, const int32_t* __restrict__ rowptr,
+                                 const int32_t* __restrict__ col, int32_t* __restrict__ out) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t lo = rowptr[i], hi = rowptr[i + 1];
+  while (lo < hi) {
+    const int32_t mid = lo + ((hi - lo) >> 1);
+    if (col[mid] < hub) lo = mid + 1;
+    else hi = mid;
+  }
+  out[i] = lo;
+}
 
 // a row shard's hub plan: column c -> its LDS slot when it is a hub column, else c + hub.
 // g (device, 3 * ng + 1 ints): [0, ng] halo group offsets, [ng + 1, 2 ng] hub length per
@@ -893,9 +944,10 @@ int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cn
 
 void Lds1Plan::release() {
   for (void* p : {(void*)brp, (void*)bcol, (void*)groups, (void*)wgs, (void*)part, (void*)chunk, (void*)pos,
-                  (void*)wdesc, (void*)wblock, (void*)hcol, (void*)hranges})
+                  (void*)wdesc, (void*)wblock, (void*)hcol, (void*)hranges, (void*)hsplit})
     (void)hipFree(p);
   hcol = nullptr;
+  hsplit = nullptr;
   hranges = nullptr;
   n_hranges = 0;
   chunk = nullptr;
@@ -1040,6 +1092,16 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
     WG_HIP_TRY(hipMemcpy(h.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
     int rc = build_groups(L, p, h, 1, L->tune.hub_iter);
     if (!rc && L->n_cols > L->n_rows && !L->halo_off.empty() && !active_only) rc = build_shard_hub(L, p, nnz_rows);
+    if (!rc && !p->hcol && L->cols_sorted && L->tune.hub_split) {
+      // plain hub on column-sorted rows: each row's hub entries are a prefix
+      rc = dmalloc(&p->hsplit, (size_t)n);
+      if (!rc) {
+        hipLaunchKernelGGL(hub_split_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, nullptr, (int32_t)n,
+                           p->hub, L->rowptr, L->col, p->hsplit);
+        const hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) rc = fail(WG_ERR_HIP, "hub_split: %s", hipGetErrorString(e));
+      }
+    }
     if (rc) {
       p->release();
       delete p;
@@ -1167,6 +1229,8 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
     a.u_bytes = (int32_t)(p->ulen * 4);
     a.gshift = p->hcol ? p->hub : 0;
     a.n_hranges = p->n_hranges;
+    a.hsplit = L->tune.hub_vidx ? nullptr : p->hsplit;
+    a.colmask = L->tune.probe_colmask > 0 ? (int32_t)((1u << L->tune.probe_colmask) - 1u) : 0;
     a.hranges = p->hranges;
     if (vx) hipLaunchKernelGGL(cheb_hub1_kernel<true>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
     else hipLaunchKernelGGL(cheb_hub1_kernel<false>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
