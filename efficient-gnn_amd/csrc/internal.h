@@ -158,7 +158,8 @@ struct Tuning {
   int32_t probe = 0;         // timing only: gathers + one output stream, no epilogue (results wrong)
   int32_t cu_reserve = 0;    // sharded chain: CUs masked off the compute stream (left to the exchange)
   int32_t xskip = 0;
-  int32_t hub_split = 1;     // hub teams on column-sorted rows: hub prefix and tail in separate loops
+  int32_t hub_split = 0;     // hub teams on column-sorted rows: hub prefix and tail in separate loops
+                             // (8M R-MAT K=32: 1388 vs 1184 us per step interleaved, r02_s29: off)
   int32_t probe_colmask = 0; // timing only: hub teams fold tail columns into a 2^k-column window (results wrong)         // timing only: streamed row blocks skip their pack / RCCL / unpack
   int32_t xdelay = 0;        // timing only: microseconds of simulated link time added to each sharded-chain
                              // exchange (split over the halo tiers by rows; one spinning wave on the stream)
