@@ -160,6 +160,11 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "cu_reserve")) {
     L->tune.cu_reserve = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 128));
     return WG_OK;  // sharded chain: CUs kept free of the step kernels (the exchange stream's)
+  } else if (!strcmp(key, "hub_pipe")) {
+    L->tune.hub_pipe = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "hub_sell")) {
+    L->tune.hub_sell = value ? 1 : 0;  // plan-time choice (the LDS plans are rebuilt)
   } else if (!strcmp(key, "hub_split")) {
     L->tune.hub_split = value ? 1 : 0;  // plan-time choice (the LDS plans are rebuilt)
   } else if (!strcmp(key, "probe_colmask")) {

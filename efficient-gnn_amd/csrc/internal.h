@@ -96,6 +96,12 @@ struct Lds1Plan {
   int32_t* brp = nullptr;     // device [nb * n + 1]: block b row r = [brp[b*n+r], brp[b*n+r+1])
   uint16_t* bcol = nullptr;   // device [nnz + 8]: local column ids
   int2* groups = nullptr;     // device: {first row, rows | lanes-per-row << 16}
+  // mode 4 (plain hub, tuning key "hub_sell"): the column ids in SELL-64 order -- per row
+  // group, slot i * 64 + lane holds the id lane's team member reads in its i-th turn (pad:
+  // kPadCol, lds1.hip), so every id load of a wave is one coalesced 256-B read
+  int2* gsell = nullptr;      // device [n_groups]: {first 64-slot line, turns}
+  int32_t* csell = nullptr;   // device [64 * lines]
+  char sell_note[64] = "";
   int4* wgs = nullptr;        // device [n_wg]: {block, first group, end group, 0}
   float* part = nullptr;      // device: teams [nb * n] block partial sums (nb > 1); windows [n_pairs]
   // mode 2 (windows): (row, block) segments padded to 8-id chunks, bit 15 of a
@@ -160,6 +166,9 @@ struct Tuning {
   int32_t xskip = 0;
   int32_t hub_split = 0;     // hub teams on column-sorted rows: hub prefix and tail in separate loops
                              // (8M R-MAT K=32: 1388 vs 1184 us per step interleaved, r02_s29: off)
+  int32_t hub_pipe = 0;      // hub teams: software-pipelined column ids and epilogue prefetch
+                             // (8M R-MAT K=32: 1224 vs 1197 us per step, r02_s31: off)
+  int32_t hub_sell = 1;      // hub teams on plain hubs: column ids in SELL-64 order (coalesced id loads)
   int32_t probe_colmask = 0; // timing only: hub teams fold tail columns into a 2^k-column window (results wrong)         // timing only: streamed row blocks skip their pack / RCCL / unpack
   int32_t xdelay = 0;        // timing only: microseconds of simulated link time added to each sharded-chain
                              // exchange (split over the halo tiers by rows; one spinning wave on the stream)

@@ -54,6 +54,9 @@ struct Lds1Args {
   int32_t n_hranges;    // mode 4 on a shard: LDS slots filled from these ranges of u (0: slots = u[0, hub))
   const int4* hranges;
   const int32_t* hsplit;  // mode 4, plain hub: first tail entry of each row (nullable)
+  const int2* gsell;    // mode 4, SELL-64 ids: per group {first 64-slot line, turns} (nullable)
+  const int32_t* csell;
+  int32_t pipe;         // mode 4: software-pipelined column ids + epilogue prefetch (tuning key "hub_pipe")
   int32_t colmask;      // timing probe (knob "probe_colmask"): tail columns folded into [hub, hub + colmask]
   const int2* groups;
   const int4* wgs;
@@ -73,6 +76,34 @@ struct Lds1Args {
   double alpha0;
   double alpha_k;
 };
+
+// the epilogue's row operands, loaded before the row's gathers so their latency overlaps them
+struct Lds1Pre {
+  double di;
+  float xo, x2, s;
+  bool iso;
+};
+__device__ __forceinline__ Lds1Pre lds1_pre(const Lds1Args& a, int32_t row) {
+  Lds1Pre p;
+  p.di = a.dinv[row];
+  p.xo = a.xm1[row];
+  p.iso = a.iso[row] != 0;
+  p.x2 = a.k == 1 ? 0.0f : a.xm2[row];
+  p.s = (a.S && a.k != 1) ? a.S[row] : 0.0f;
+  return p;
+}
+// lds1_epilogue with the operands already loaded (same arithmetic, same order)
+__device__ __forceinline__ void lds1_finish(const Lds1Args& a, int32_t row, double acc, const Lds1Pre& p) {
+  double off = -p.di * acc;
+  if (p.iso) off -= (double)p.xo;  // L_hat_ii = -1
+  const double t = (a.k == 1) ? off : 2.0 * off - (double)p.x2;
+  if (a.xk) __builtin_nontemporal_store((float)t, a.xk + row);
+  if (a.u_out) a.u_out[row] = (float)(t * p.di);
+  if (a.S) {
+    const double s = (a.k == 1) ? a.alpha0 * (double)p.xo + a.alpha_k * t : (double)p.s + a.alpha_k * t;
+    __builtin_nontemporal_store((float)s, a.S + row);
+  }
+}
 
 // T_k,i = 2 (L_hat T_{k-1})_i - T_{k-2,i}  (k == 1: T_1 = L_hat T_0), S, u_k.
 __device__ __forceinline__ void lds1_epilogue(const Lds1Args& a, int32_t row, double acc) {
@@ -95,6 +126,11 @@ __device__ __forceinline__ void lds1_epilogue(const Lds1Args& a, int32_t row, do
 }
 
 extern __shared__ float g_u_lds[];
+
+// a padding column id for the hub teams' x_of: LDS slot min(c, hub) = the zero slot, and the
+// tail gather's byte offset (c - gshift) * 4 wraps past the buffer's extent (< 2^31 bytes), so
+// the raw buffer load returns 0 -- a pad adds exactly 0.0
+constexpr int32_t kPadCol = 0x7fffffff;
 
 template <bool DIRECT>
 __global__ __launch_bounds__(kLdsThreads) void cheb_lds1_kernel(Lds1Args a) {
@@ -233,6 +269,22 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc += (double)x[j];
       }
+    } else if (act && a.csell) {
+      // SELL-64 ids: turn i of this lane is slot (line + i) * 64 + lane -- the same entries in
+      // the same order as the CSR walk below (pads: kPadCol, adding 0.0)
+      const int2 gs = a.gsell[g];
+      const int32_t* __restrict__ cs = a.csell + (int64_t)gs.x * 64 + lane;
+      int32_t i = 0;
+      for (; i + 3 < gs.y; i += 4) {
+        const int32_t c0 = cs[(int64_t)i * 64], c1 = cs[(int64_t)(i + 1) * 64], c2 = cs[(int64_t)(i + 2) * 64],
+                      c3 = cs[(int64_t)(i + 3) * 64];
+        const float x0 = x_of(c0), x1 = x_of(c1), x2 = x_of(c2), x3 = x_of(c3);
+        acc += (double)x0;
+        acc += (double)x1;
+        acc += (double)x2;
+        acc += (double)x3;
+      }
+      for (; i < gs.y; ++i) acc += (double)x_of(cs[(int64_t)i * 64]);
     } else if (act && a.hsplit) {
       // hub columns are each row's prefix [e0, es): LDS reads only, then the tail with global
       // loads only -- no dropped-offset loads through the address path for hub entries and
@@ -262,6 +314,31 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
         acc += (double)x3;
       }
       for (; e < e1; e += ln) acc += (double)xg(col[e]);
+    } else if (act && a.pipe) {
+      // software-pipelined: the next batch's 4 column ids load while this batch's gathers are
+      // in flight (one dependent round trip per batch, not two), and the epilogue's operands
+      // load first; a lane adds its entries in the same order (masked slots add 0.0)
+      const int32_t e0 = rp[row], e1 = rp[row + 1];
+      const int32_t last = max(e1 - 1, e0);
+      const Lds1Pre pre = lds1_pre(a, row);  // every lane of the team (no load behind a branch)
+      int32_t e = e0 + q;
+      int32_t c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = col[min(e + j * ln, last)];
+      while (e < e1) {
+        float x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = x_of(e + j * ln < e1 ? c[j] : kPadCol);
+        const int32_t en = e + 4 * ln;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = col[min(en + j * ln, last)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += (double)x[j];
+        e = en;
+      }
+      for (int o = ln >> 1; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
+      if (q == 0) lds1_finish(a, row, acc, pre);
+      continue;
     } else if (act) {
       const int32_t e1 = rp[row + 1];
       int32_t e = rp[row] + q;
@@ -280,6 +357,26 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   }
 }
 
+
+// SELL-64 ids of the hub teams: one wave per row group; lane = team * ln + q takes entries
+// rp[row] + q + i * ln, i < turns (pads: kPadCol)
+__global__ void sell_fill_kernel(int32_t n_groups, const int2* __restrict__ groups, const int2* __restrict__ gsell,
+                                 const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                 int32_t* __restrict__ out) {
+  const int32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (g >= n_groups) return;
+  const int2 gd = groups[g], gs = gsell[g];
+  const int nrows = gd.y & 0xffff, ln = gd.y >> 16;
+  const int team = lane / ln, q = lane % ln;
+  const int32_t row = gd.x + team;
+  const int32_t e0 = team < nrows ? rowptr[row] + q : 0, e1 = team < nrows ? rowptr[row + 1] : 0;
+  int32_t* dst = out + (int64_t)gs.x * 64 + lane;
+  for (int32_t i = 0; i < gs.y; ++i) {
+    const int32_t e = e0 + i * ln;
+    dst[(int64_t)i * 64] = e < e1 ? col[e] : kPadCol;
+  }
+}
 
 // first entry of each row whose column is >= hub (rows sorted by column)
 __global__ void hub_split_kernel(int32_t n, int32_t hub, const int32_t* __restrict__ rowptr,
@@ -944,10 +1041,13 @@ int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cn
 
 void Lds1Plan::release() {
   for (void* p : {(void*)brp, (void*)bcol, (void*)groups, (void*)wgs, (void*)part, (void*)chunk, (void*)pos,
-                  (void*)wdesc, (void*)wblock, (void*)hcol, (void*)hranges, (void*)hsplit})
+                  (void*)wdesc, (void*)wblock, (void*)hcol, (void*)hranges, (void*)hsplit, (void*)gsell,
+                  (void*)csell})
     (void)hipFree(p);
   hcol = nullptr;
   hsplit = nullptr;
+  gsell = nullptr;
+  csell = nullptr;
   hranges = nullptr;
   n_hranges = 0;
   chunk = nullptr;
@@ -1092,6 +1192,43 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
     WG_HIP_TRY(hipMemcpy(h.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
     int rc = build_groups(L, p, h, 1, L->tune.hub_iter);
     if (!rc && L->n_cols > L->n_rows && !L->halo_off.empty() && !active_only) rc = build_shard_hub(L, p, nnz_rows);
+    if (!rc && !p->hcol && L->tune.hub_sell && p->n_groups > 0) {
+      // SELL-64 ids: turns per group = the longest team row / team width
+      std::vector<int2> gr(p->n_groups), gs(p->n_groups);
+      if (hipMemcpy(gr.data(), p->groups, sizeof(int2) * p->n_groups, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(WG_ERR_HIP, "hub sell: copy");
+      int64_t lines = 0;
+      for (int32_t g = 0; g < p->n_groups && !rc; ++g) {
+        const int nrows = gr[g].y & 0xffff, ln = gr[g].y >> 16;
+        int64_t turns = 0;
+        for (int t = 0; t < nrows; ++t) {
+          const int64_t len = h[gr[g].x + t + 1] - h[gr[g].x + t];
+          turns = std::max<int64_t>(turns, ceil_div(len, ln));
+        }
+        gs[g] = make_int2((int32_t)lines, (int32_t)turns);
+        lines += turns;
+      }
+      if (!rc && lines * 64 >= ((int64_t)1 << 31)) rc = WG_ERR_UNSUPPORTED;  // stay on the CSR walk
+      if (!rc) rc = dmalloc(&p->gsell, (size_t)p->n_groups);
+      if (!rc) rc = dmalloc(&p->csell, (size_t)std::max<int64_t>(1, lines * 64));
+      if (!rc && hipMemcpy(p->gsell, gs.data(), sizeof(int2) * p->n_groups, hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail(WG_ERR_HIP, "hub sell: copy");
+      if (!rc) {
+        hipLaunchKernelGGL(sell_fill_kernel, dim3((unsigned)ceil_div(p->n_groups, 4)), dim3(256), 0, nullptr,
+                           p->n_groups, p->groups, p->gsell, L->rowptr, L->col, p->csell);
+        const hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) rc = fail(WG_ERR_HIP, "hub sell: %s", hipGetErrorString(e));
+      }
+      if (rc == WG_ERR_UNSUPPORTED) {
+        (void)hipFree(p->gsell);
+        (void)hipFree(p->csell);
+        p->gsell = nullptr;
+        p->csell = nullptr;
+        rc = WG_OK;
+      }
+      snprintf(p->sell_note, sizeof(p->sell_note), " sell_lines=%lld (ids %.2fx nnz)", (long long)lines,
+               (double)lines * 64 / std::max<int64_t>(1, nnz_rows));
+    }
     if (!rc && !p->hcol && L->cols_sorted && L->tune.hub_split) {
       // plain hub on column-sorted rows: each row's hub entries are a prefix
       rc = dmalloc(&p->hsplit, (size_t)n);
@@ -1108,8 +1245,8 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
       return rc;
     }
     char buf[256];
-    snprintf(buf, sizeof(buf), "lds1: hub teams rows=%lld cols=%lld nnz=%d hub=%d groups=%d workgroups=%d ranges=%d\n",
-             (long long)n, (long long)n_cols, nnz_rows, p->hub, p->n_groups, p->n_wg, p->n_hranges);
+    snprintf(buf, sizeof(buf), "lds1: hub teams rows=%lld cols=%lld nnz=%d hub=%d groups=%d workgroups=%d ranges=%d%s\n",
+             (long long)n, (long long)n_cols, nnz_rows, p->hub, p->n_groups, p->n_wg, p->n_hranges, p->sell_note);
     p->text = buf;
     L->lds1[slot] = p;
     *out = p;
@@ -1230,6 +1367,9 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
     a.gshift = p->hcol ? p->hub : 0;
     a.n_hranges = p->n_hranges;
     a.hsplit = L->tune.hub_vidx ? nullptr : p->hsplit;
+    a.pipe = L->tune.hub_pipe;
+    a.gsell = L->tune.hub_vidx ? nullptr : p->gsell;
+    a.csell = L->tune.hub_vidx ? nullptr : p->csell;
     a.colmask = L->tune.probe_colmask > 0 ? (int32_t)((1u << L->tune.probe_colmask) - 1u) : 0;
     a.hranges = p->hranges;
     if (vx) hipLaunchKernelGGL(cheb_hub1_kernel<true>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);

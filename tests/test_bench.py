@@ -64,6 +64,28 @@ def test_bench_multi_rank_headline_rehearsal():
     assert d["replicas"]["value"] > 0
 
 
+@pytest.mark.gpu
+def test_bench_multi_rank_picks_the_faster_exchange():
+    """N > 1 with two exchanges: the headline is timed with both and the line is
+    the faster one whose check passed; the other is attached in full."""
+    env = dict(os.environ, WATS_BENCH_PG="gloo", WATS_BENCH_DEVICE="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={30500 + os.getpid() % 1000}", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--scale-config", "pubmed", "--F", "8",
+           "--exchange", "ipc,host", "--sharded-extra", "none", "--config", "pubmed", "--replicas", "0"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    cmp = d["exchange_compare"]
+    assert set(cmp) == {"ipc", "host"} and all(v["check_ok"] for v in cmp.values()), cmp
+    best = max(cmp, key=lambda x: cmp[x]["value"])
+    assert d["config"]["exchange"] == best and d["value"] == cmp[best]["value"]
+    other = "host" if best == "ipc" else "ipc"
+    assert d[f"sharded_pubmed_{other}"]["value"] == cmp[other]["value"]
+
+
 def test_byte_models_cpu():
     """bench.py's byte models (no GPU): SURVEY 8(d)'s forward-recurrence B_step
     and the Clenshaw form, which drops the S read + write (8 B) and adds the

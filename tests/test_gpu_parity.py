@@ -392,8 +392,10 @@ def test_clenshaw_value_free_directed_selfloops(seed):
                                    dict(lds=4), dict(lds=4, lds_cb=1024), dict(lds=4, lds_cb=32),
                                    dict(lds=4, lds_cb=4096, hub_iter=2, lds_wg=7), dict(lds=4, lds_cb=1024, lds_wg=1),
                                    dict(lds=4, lds_cb=2048, hub_iter=64), dict(lds=4, lds_cb=1024, hub_vidx=0),
-                                   dict(lds=4, lds_cb=512, hub_vidx=1, hub_iter=1), dict(lds=4, lds_cb=1024, hub_split=1),
-                                   dict(lds=4, lds_cb=2048, hub_split=1, hub_iter=3)])
+                                   dict(lds=4, lds_cb=512, hub_vidx=1, hub_iter=1), dict(lds=4, lds_cb=1024, hub_split=1, hub_sell=0),
+                                   dict(lds=4, lds_cb=2048, hub_split=1, hub_iter=3, hub_sell=0),
+                                   dict(lds=4, hub_sell=0), dict(lds=4, lds_cb=4096, hub_pipe=1, hub_sell=0),
+                                   dict(lds=4, lds_cb=2048, hub_iter=3), dict(lds=4, lds_cb=1024, hub_iter=64, lds_wg=3)])
 def test_lds1_plans_f1(knobs):
     """The LDS kernel (one and many column blocks, every team width, any
     workgroup split) and the gather kernel it replaces agree with the oracle."""
