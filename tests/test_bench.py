@@ -38,6 +38,8 @@ def test_bench_line_schema_small():
         assert k in c, k
     assert c["check"]["ok"], c["check"]          # the benchmarked S vs the C oracle (all columns)
     assert "connected_companion" not in d          # only for the ogbn-arxiv headline
+    assert d["prologue"]["create_ms"] > 0 and d["prologue"]["log1p_degree_ms"] > 0
+    assert d["cpu_baseline"]["prologue_s"] > 0
     for key in ("sharded", "sharded_pubmed_rccl"):
         sh = d[key]
         assert "error" not in sh, sh
