@@ -207,7 +207,7 @@ def _rel_err(got, ref) -> float:
 
 # ----------------------------------------------------------------------------- row-sharded runs
 def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl",
-                median_reps: int = 0, check: bool = True, halo_tiers=None):
+                median_reps: int = 0, check: bool = True, halo_tiers=None, min_time: float = 0.0):
     """One graph (generated identically on every rank, on the GPU) split into
     nnz-balanced row blocks; per Chebyshev step one halo exchange (`exchange`:
     RCCL send/recv or IPC pull in the native chain, or torch
@@ -249,6 +249,18 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         run()
         torch.cuda.synchronize(device)
     _log(f"sharded {config} ({exchange}): warm")
+    if min_time > 0:
+        # extras: at least min_time s of chains in the timed region -- a few 1-ms chains (Reddit
+        # F = 1) read 2x slow on one ms-scale hiccup (profiles/r02/s36_bench: 5 chains 2.19 ms
+        # each vs 1.03 alone, s37).  The headline times exactly the driver's steps.
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        run()
+        torch.cuda.synchronize(device)
+        one = time.perf_counter() - t1
+        if world > 1:
+            one = _allreduce(one, dist.ReduceOp.MAX, device)
+        steps = max(steps, min(200, int(min_time / max(one, 1e-6))))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -811,7 +823,7 @@ def main():
             try:
                 torch.cuda.empty_cache()
                 results[key] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
-                                           device, x, halo_tiers=args.halo_tiers)
+                                           device, x, halo_tiers=args.halo_tiers, min_time=0.2)
             except Exception as exc:  # noqa: BLE001
                 results[key] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
     if mode == "sharded" and len(exchanges) > 1:
@@ -825,7 +837,7 @@ def main():
             try:
                 torch.cuda.empty_cache()
                 results[f"{cfg}_{x}"] = run_sharded(cfg, args.K, args.F, args.sharded_steps, 1, args.seed, args.s,
-                                                    world, rank, device, x, halo_tiers=args.halo_tiers)
+                                                    world, rank, device, x, halo_tiers=args.halo_tiers, min_time=0.2)
             except Exception as exc:  # noqa: BLE001
                 results[f"{cfg}_{x}"] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
     if watchdog is not None:
