@@ -1101,10 +1101,13 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter) {
   const bool wide = G <= 16;
   const bool big = nnz >= (int64_t)1 << 20;
-  *iter = t.iter > 0 ? t.iter : (wide ? (big ? 192 : 24) : (G == 64 && big ? 8 : 16));
+  // from 8 M nonzeros: longer team runs and 256-iteration split-row chunks (Reddit-size F=41,
+  // width 48: 1400 vs 1434 us per step; its 8-way shard, 14.3 M nonzeros: 195-200 vs 207-211
+  // with the 1-16 M defaults, profiles/r02/s39-s40)
+  const bool large = nnz >= (int64_t)1 << 23;
+  *iter = t.iter > 0 ? t.iter : (wide ? (large ? 384 : big ? 192 : 24) : (G == 64 && big ? 8 : 16));
   *block_iter = t.block_iter > 0 ? t.block_iter : (wide ? 256 : 32);
-  const bool huge = nnz >= (int64_t)1 << 24;
-  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (huge ? 128 : big ? 64 : 32) : 16);
+  *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (wide ? (large ? 256 : big ? 64 : 32) : 16);
 }
 
 // Build (once per tile shape) the segment table and the split-row chunk table.
