@@ -120,7 +120,7 @@ def _cpu_worker(rank, world, port, kind, K, F, q, tiers=1):
 
 
 @pytest.mark.parametrize("world,kind,tiers", [(2, "rmat", 1), (3, "rmat", 1), (2, "weighted", 1), (3, "rmat", 2),
-                                              (2, "weighted", 2)])
+                                              (2, "weighted", 2), (8, "rmat", 1), (8, "rmat", 2)])
 def test_sharded_chain_cpu_gloo(world, kind, tiers):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
