@@ -185,7 +185,8 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
     (2, "rmat", 1, 2, "ipc", 1), (4, "rmat", 1, 2, "ipc", 1), (2, "rmat", 1, 0, "ipc", 1), (3, "rmat", 40, 2, "ipc", 1),
     (2, "weighted", 4, 2, "ipc", 1), (3, "weighted", 1, 2, "ipc", 1), (2, "rmat", 1, 4, "ipc", 1), (2, "rmat", 1, 4, "host", 1),
     (3, "rmat", 40, 2, "ipc", 2), (2, "weighted", 4, 2, "ipc", 2), (4, "rmat", 1, 2, "ipc", 2),
-    (3, "rmat", 8, 2, "host", 2)])
+    (3, "rmat", 8, 2, "host", 2), (8, "rmat", 40, 2, "ipc", 1), (8, "rmat", 1, 2, "ipc", 1),
+    (8, "weighted", 4, 2, "ipc", 2)])
 def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiers):
     """Several ranks on one GPU: the Python exchange over gloo host copies, or
     the native chain with the one-sided IPC exchange (ranks pull from each
