@@ -189,6 +189,12 @@ def cpu_baseline(g, K, F, s, X, seconds, S_gpu):
                       f"matvecs, {t_total:.1f} s")
     t0 = time.perf_counter()
     S_ref, _ = C.graph_wavelet_features(g.indptr, g.indices, g.values, X, K, s, threads=16, return_H=False)
+    t_c = time.perf_counter() - t0
+    # a second CPU figure beside the reference's own (single-threaded scipy) path: the C
+    # restatement (float64, OpenMP over rows, 16 threads = the box's CPU share) on the same pass
+    out["c_oracle_16_threads"] = {"value": nnz * K / t_c, "unit": "edges*K/s", "cores": 16, "seconds": t_c,
+                                  "what": "oracle/wats_chain.c: the same pass (chain + heat sum + L1 norm), "
+                                          "float64, rows split over 16 OpenMP threads"}
     err = _rel_err(S_gpu, S_ref)
     out["check"] = {"max_rel_err": err, "tol": CHECK_TOL, "ok": bool(err <= CHECK_TOL),
                     "what": f"the benchmarked pass's S (all {F} columns, this signal) vs the C restatement of the "
