@@ -193,7 +193,7 @@ def cpu_baseline(g, K, F, s, X, seconds, S_gpu):
     # a second CPU figure beside the reference's own (single-threaded scipy) path: the C
     # restatement (float64, OpenMP over rows, 16 threads = the box's CPU share) on the same pass
     out["c_oracle_16_threads"] = {"value": nnz * K / t_c, "unit": "edges*K/s", "cores": 16, "seconds": t_c,
-                                  "what": "oracle/wats_chain.c: the same pass (chain + heat sum + L1 norm), "
+                                  "what": "oracle/wats_chain.c: the same pass (its own Laplacian build included, chain, heat sum, L1 norm), "
                                           "float64, rows split over 16 OpenMP threads"}
     err = _rel_err(S_gpu, S_ref)
     out["check"] = {"max_rel_err": err, "tol": CHECK_TOL, "ok": bool(err <= CHECK_TOL),
