@@ -33,6 +33,25 @@ __global__ void pack_rows_kernel(int64_t n, int64_t F, const int32_t* __restrict
   dst[idx] = src[(int64_t)rows[i] * F + (idx - i * F)];
 }
 
+// the same with 16-B lanes (F % 4 == 0, 16-B aligned rows: every padded chain vector)
+__global__ void pack_rows4_kernel(int64_t n, int64_t F4, const int32_t* __restrict__ rows, const float4* __restrict__ src,
+                                  float4* __restrict__ dst) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * F4) return;
+  const int64_t i = idx / F4;
+  dst[idx] = src[(int64_t)rows[i] * F4 + (idx - i * F4)];
+}
+
+// pack rows[0, n) of src (F floats per row) into dst, 16-B lanes when the width allows
+void launch_pack(int64_t n, int64_t F, const int32_t* rows, const float* src, float* dst, hipStream_t st) {
+  if (n <= 0) return;
+  if (F % 4 == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0 && (reinterpret_cast<uintptr_t>(dst) % 16) == 0)
+    hipLaunchKernelGGL(pack_rows4_kernel, dim3((unsigned)ceil_div(n * (F / 4), 256)), dim3(256), 0, st, n, F / 4, rows,
+                       reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst));
+  else
+    hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)ceil_div(n * F, 256)), dim3(256), 0, st, n, F, rows, src, dst);
+}
+
 // received rows i (row-block streaming: received contiguously per (block, peer)) -> halo row pos[i]
 __global__ void unpack_rows_kernel(int64_t n, int64_t F, const int32_t* __restrict__ pos, const float* __restrict__ src,
                                    float* __restrict__ ext_halo) {
@@ -344,8 +363,7 @@ struct wg_dist_s {
     if (first) {
       if (int rc = mark(st, true)) return rc;
       if (n_send > 0) {
-        hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)ceil_div(n_send * F, 256)), dim3(256), 0, st, n_send, F,
-                           send_rows, ext, sendbuf);
+        launch_pack(n_send, F, send_rows, ext, sendbuf, st);
         WG_LAUNCH_CHECK();
       }
     }
@@ -389,8 +407,7 @@ struct wg_dist_s {
       return b == 0 ? mark(xst, false) : WG_OK;
     }
     if (s1 > s0) {
-      hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)ceil_div((s1 - s0) * F, 256)), dim3(256), 0, xst, s1 - s0, F,
-                         bsend_rows + s0, ext, sendbuf + s0 * F);
+      launch_pack(s1 - s0, F, bsend_rows + s0, ext, sendbuf + s0 * F, xst);
       WG_LAUNCH_CHECK();
     }
     if (int rc = nccl_try(ncclGroupStart(), "ncclGroupStart")) return rc;
