@@ -293,6 +293,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         if world > 1:
             med = _allreduce(med, dist.ReduceOp.MAX, device)
     # kernel / exchange attribution: one more pass, eager, with HIP events (outside the timed region)
+    dinfo = sw.info()   # after the timed chains: was the chain replayed as a hipGraph?
     sw.profile_start()
     run()
     prof = sw.profile_collect()
@@ -346,6 +347,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                      "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
                      "avg_exchange_us": prof["exchange_ms"] * 1e3,
                      "exchange_overlapped": prof.get("overlapped", False),
+                     "graph_replayed": bool(dinfo.get("captured")) if dinfo else None,
                      "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
                      "nominal_8d_bytes": b_8d,

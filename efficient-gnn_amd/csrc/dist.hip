@@ -184,16 +184,10 @@ __global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, i
     if (q != rank) __hip_atomic_store(peer_flags[q] + rank, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The exchange stream at the highest priority: a hardware queue of its own (streams of one
-// priority share the process's few queues round-robin, and two streams on one queue run in
-// submission order -- the exchange would not overlap the step kernels at all), and its
-// small kernels go first when both queues have work.
-hipError_t create_exchange_stream(hipStream_t* out) {
-  int least = 0, greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
-    return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
-  return hipStreamCreateWithPriority(out, hipStreamNonBlocking, greatest);
-}
+// The exchange stream, at normal priority: a highest-priority stream made every later
+// handle's step kernels in the process about 2x slower (Reddit F=1 sharded chain 2.2 vs
+// 1.02 ms, F=41 23.5 vs 22.4 ms; profiles/r02/s53_stream_priority.log) and bought nothing.
+hipError_t create_exchange_stream(hipStream_t* out) { return hipStreamCreateWithFlags(out, hipStreamNonBlocking); }
 
 int nccl_try(ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return WG_OK;
