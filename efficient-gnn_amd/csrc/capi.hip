@@ -180,6 +180,15 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "overlap")) {
     L->tune.overlap = value ? 1 : 0;
     return WG_OK;  // launch-time choice (a captured chain re-captures: tune_gen)
+  } else if (!strcmp(key, "tiles")) {
+    if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "tiles must be -1 (auto), 0 or 1");
+    L->tune.tiles = (int32_t)value;
+  } else if (!strcmp(key, "tile_th")) {
+    if (value < 1 || value > 2048) return fail(WG_ERR_INVALID, "tile_th must be in [1, 2048]");
+    L->tune.tile_th = (int32_t)value;
+  } else if (!strcmp(key, "tile_max")) {
+    if (value < 1 || value > 1 << 20) return fail(WG_ERR_INVALID, "tile_max must be in [1, 2^20]");
+    L->tune.tile_max = (int32_t)value;
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;
   } else {
@@ -218,6 +227,8 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
   snprintf(buf, sizeof(buf), "F=%lld VEC=%d LF=%d segments=%d blocks=%d active_rows=%lld closed_form_rows=%lld\n",
            (long long)F, vec, LF, p->tab.n, p->tab.total_blocks, (long long)L->n_active, (long long)L->n_closed);
   g_text = buf + p->text;
+  for (int i = 1; i >= 0; --i)  // the hybrid step's plan, once a chain has built it
+    if (L->tiles[i]) g_text += L->tiles[i]->text;
   if (F == 1) {
     Lds1Plan* lp = nullptr;
     if (!get_lds1_plan(L, true, &lp) && lp) g_text += lp->text;

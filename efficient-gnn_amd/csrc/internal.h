@@ -130,6 +130,29 @@ struct Lds1Plan {
   int64_t u_floats() const { return mode == 4 ? ulen : (int64_t)lchunks * nb * 32; }
 };
 
+// Hybrid step (tiles.hip) for wide signals on large unweighted graphs: internal rows in
+// blocks of 64, columns in tiles of 32; each (row block, column tile) pair holding at
+// least tile_th entries is a dense block, summed on the matrix cores from its 64 row
+// masks of 32 bits; the rest of each row (its "tail") sits at the end of the row's range
+// in tcol and is summed by the step kernel's phase 2, which adds the blocks' sums (part).
+struct TilePlan {
+  int64_t n_plan = 0;          // rows planned: [0, n_plan)
+  int64_t col_limit = 0;       // column rows a block may read (rows >= col_limit of the tile read as 0)
+  int32_t n_blocks = 0, n_items = 0, n_multi = 0, n_slots = 0;
+  int64_t dense_nnz = 0;       // entries inside dense blocks
+  int32_t* bct = nullptr;      // device [n_blocks]: column tile of each block
+  uint32_t* bmask = nullptr;   // device [n_blocks][64]: row masks (bit k = column 32 * tile + k)
+  int4* items = nullptr;       // device [n_items]: {row block, first block, end block, slot or -1}
+  int4* multi = nullptr;       // device [n_multi]: {row block, first slot, slots, 0}
+  int32_t* tcol = nullptr;     // device [nnz]: each row's tail entries at the end of its range
+  int32_t* tsplit = nullptr;   // device [n_rows]: first tail entry of each row
+  int32_t width = 0;           // doubles per row of part / slots
+  double* part = nullptr;      // device [n_rows][width]
+  double* slots = nullptr;     // device [n_slots][64][width]
+  std::string text;
+  void release();
+};
+
 struct Tuning {
   // 0 = shape-dependent default (see default_knobs in step.hip)
   int32_t iter = 0;          // team mode: target nonzeros per lane sub-group
@@ -173,6 +196,10 @@ struct Tuning {
   int32_t xdelay = 0;        // timing only: microseconds of simulated link time added to each sharded-chain
                              // exchange (split over the halo tiers by rows; one spinning wave on the stream)
   int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple
+  int32_t tiles = -1;        // hybrid step (tiles.hip): -1 = auto (unweighted, width % 16 == 0, >= 8 M nonzeros,
+                             // >= 30 % of the entries in dense blocks), 0 = off, 1 = whenever it applies
+  int32_t tile_th = 64;      // entries that make a 64 x 32 (row block, column tile) pair a dense block
+  int32_t tile_max = 128;    // dense blocks per workgroup (longer row blocks split over slots)
 };
 
 }  // namespace wg
@@ -210,6 +237,8 @@ struct wg_laplacian_s {
                                   // come from peer q, each group in descending degree (wg_dist_create)
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
   bool lds1_failed[2] = {false, false};        // not applicable (too many blocks): use the gather kernel
+  wg::TilePlan* tiles[2] = {nullptr, nullptr};  // [active_only] hybrid step plans (released with lds1)
+  bool tiles_failed[2] = {false, false};
   // workspace for wg_wavelet_features
   float* ws = nullptr;
   size_t ws_floats = 0;
@@ -259,6 +288,10 @@ struct PhaseArgs {
   const int32_t* rsplit = nullptr;   // [n_rows] first entry with column >= n_rows (rows column-sorted)
   const int32_t* rsplit2 = nullptr;  // [n_rows] first tier-1 halo entry (two tiers), else nullptr
   double* part = nullptr;            // [n_rows][F]
+  // hybrid step (internal to launch_step): phase 2 over the tail columns `col`, adding part only
+  // to rows with dense entries (rsplit[row] > rowptr[row])
+  const int32_t* col = nullptr;
+  int part_cond = 0;
 };
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
@@ -283,6 +316,12 @@ int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* sr
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);
 int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start);
+// tiles.hip: the hybrid step's plan (*out = nullptr: not applicable) and its dense-block pass,
+// which writes part = sum over the dense entries of u_j (value-free steps) for the planned rows
+bool tiles_wanted(const wg_laplacian_s* L, int64_t F);
+int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out);
+int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream);
+void release_tiles(wg_laplacian_s* L);
 // lds1.hip
 int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out);  // *out = nullptr: not applicable
 void release_lds1(wg_laplacian_s* L);

@@ -1062,6 +1062,7 @@ void Lds1Plan::release() {
 }
 
 void release_lds1(wg_laplacian_s* L) {
+  release_tiles(L);  // the hybrid step's plans are invalidated by the same events
   for (int i = 0; i < 2; ++i) {
     if (L->lds1[i]) {
       L->lds1[i]->release();

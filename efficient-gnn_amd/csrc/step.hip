@@ -86,6 +86,7 @@ struct StepArgs {
   const int32_t* rsplit2;
   double* part;
   int32_t probe;  // timing probe (knob "probe"): gathers only -- no epilogue operands, acc stored to xk
+  int32_t part_cond;  // hybrid step (tiles.hip): phase 2 adds part only to rows with dense entries
 };
 
 // the entry range of a row (or of a split-row chunk) this launch's phase covers
@@ -122,6 +123,7 @@ __device__ __forceinline__ void part_store(const StepArgs& a, int64_t row, int f
 
 template <int VEC>
 __device__ __forceinline__ void part_add(const StepArgs& a, int64_t row, int fs, double (&acc)[VEC]) {
+  if (a.part_cond && a.rsplit[row] == a.rowptr[row]) return;  // no dense entries: no part written
   const double* p = a.part + row * a.ld + (int64_t)fs * VEC;
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] += p[j];
@@ -1304,6 +1306,22 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
   if (ph && ph->phase != 0 && (!ph->rsplit || !ph->part || S_out || (ph->phase == 3 && !ph->rsplit2)))
     return fail(WG_ERR_INVALID, "launch_step: a phased step needs rsplit (phase 3: rsplit2), part, no fused finalize");
   if (int rc = prof_mark(L, stream, true)) return rc;
+  // hybrid step (tiles.hip): the value-free Clenshaw steps of wide signals on large unweighted
+  // graphs sum their dense blocks on the matrix cores into part, then run phase 2 over the tail
+  PhaseArgs hyb;
+  if (cl && cl->uin && !(ph && (ph->phase != 0 || ph->block >= 0)) && !L->tune.probe && tiles_wanted(L, F)) {
+    TilePlan* tp = nullptr;
+    if (int rc = get_tile_plan(L, active_only, F, &tp)) return rc;
+    if (tp) {
+      if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
+      hyb.phase = 2;
+      hyb.rsplit = tp->tsplit;
+      hyb.part = tp->part;
+      hyb.col = tp->tcol;
+      hyb.part_cond = 1;
+      ph = &hyb;
+    }
+  }
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H, S_out});
   int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
   if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
@@ -1319,7 +1337,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     if (rc) return rc;
     StepArgs a{};
     a.rowptr = L->rowptr;
-    a.col = L->col;
+    a.col = (ph && ph->col) ? ph->col : L->col;
     a.val = L->val;
     a.iso = L->iso;
     a.xm1 = xm1 + f0;
@@ -1352,6 +1370,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       a.rsplit = ph->rsplit;
       a.rsplit2 = ph->rsplit2;
       a.part = ph->part + f0;
+      a.part_cond = ph->part_cond;
       if (a.phase == 1 || a.phase == 3) {  // nothing but the sums: no epilogue operands, no T / S / H stores
         a.xk = nullptr;
         a.S = nullptr;

@@ -1,0 +1,402 @@
+// tiles.hip -- the hybrid Chebyshev step for wide signals on large unweighted
+// graphs: the dense part of L_hat on the matrix cores.
+//
+// On an unweighted graph the value-free Clenshaw step sums u_j = b_j * dinv_j
+// over each row's columns (step.hip, reference calibration/WATS.py:32-36).  In
+// descending-degree order the hub columns form dense blocks: on the Reddit-size
+// R-MAT graph the (64-row block, 32-column tile) pairs holding >= 64 entries
+// carry 78 % of the 114.6 M entries.  The gather kernel pays two or three L2
+// line requests per entry (a 192-B row of u each); a dense block instead reads
+// its 32 rows of u once (6 KB, coalesced), shared by the 64 rows of the block.
+//
+//   part[row] = sum over the row's dense entries of u_j      (this file)
+//   step      = phase 2 of cheb_step_kernel over the tail entries, + part, epilogue
+//
+// The block sum is a 64 x 32 by 32 x W product A.U with A a 0/1 matrix (exact in
+// bf16).  U is split exactly into three bf16 pieces, u = hi + mid + lo
+// (truncations: hi = u with the low 16 bits cleared, mid likewise of u - hi, and
+// lo = u - hi - mid has at most 8 significant bits), so every product is exact
+// and each v_mfma_f32_16x16x32_bf16 adds 32 of them in float32; each block's
+// float32 sum (<= 96 exact terms) is added to a float64 accumulator.  Results
+// differ from the all-float64 gather kernel only by that float32 rounding of
+// each block sum (tests/test_gpu_parity.py, test_tiles_*).
+//
+// Workgroup = 4 waves = one row block (or a share of a long row block's dense
+// blocks: those write float64 slots that tiles_combine_kernel sums in order).
+// Per dense block: the 256 lanes load the 32 x W tile of u (float4, L2), split it
+// into the three bf16 pieces in an LDS image [piece][32 rows][W] (double-
+// buffered: the next tile's loads are in flight while this one is multiplied),
+// and each wave multiplies its 16 rows: A fragments from a byte -> 8 x bf16
+// lookup table indexed by the row mask, B fragments by the transposed LDS read
+// ds_read_b64_tr_b16 (two per fragment), three MFMAs (lo, mid, hi) per 16 columns.
+#include <algorithm>
+#include <cstring>
+
+#include "internal.h"
+
+namespace wg {
+namespace {
+
+constexpr int kTR = 64;  // rows per row block (4 waves x 16)
+constexpr int kTC = 32;  // columns per tile (the MFMA's K)
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct TileArgs {
+  const float* u;        // gathered vector (rows = columns of L_hat), row stride ld
+  int64_t ld;
+  int64_t col_limit;     // rows of u that exist (tile rows beyond read as 0)
+  int64_t n_plan;        // rows of part written
+  const int32_t* bct;
+  const uint32_t* bmask;
+  const int4* items;
+  double* part;          // [rows][ld]
+  double* slots;         // [slot][64][W]
+};
+
+// u = hi + mid + lo exactly, each piece a bf16 (the high half of a float32)
+__device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const uint32_t hb = __float_as_uint(x) & 0xFFFF0000u;
+  const float r1 = x - __uint_as_float(hb);
+  const uint32_t mb = __float_as_uint(r1) & 0xFFFF0000u;
+  const float r2 = r1 - __uint_as_float(mb);
+  h = hb >> 16;
+  m = mb >> 16;
+  l = __float_as_uint(r2) >> 16;
+}
+
+template <int NFB>
+__global__ __launch_bounds__(256) void cheb_tiles_kernel(TileArgs t) {
+  constexpr int W = 16 * NFB;          // signal width
+  constexpr int NV = kTC * W / 4;      // float4 per tile
+  constexpr int PER = (NV + 255) / 256;
+  __shared__ uint4 lut[256];                           // byte -> 8 bf16 (bit j ? 1.0 : 0) in element j
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][3][kTC][W];  // [buffer][piece hi/mid/lo][k][f]
+  const int tid = threadIdx.x;
+  {
+    uint32_t d[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      d[q] = (((tid >> (2 * q)) & 1) ? 0x3F80u : 0u) | (((tid >> (2 * q + 1)) & 1) ? 0x3F800000u : 0u);
+    lut[tid] = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+  const int4 it = t.items[blockIdx.x];
+  const int64_t rb = it.x;
+  const int lane = tid & 63, wave = tid >> 6;
+
+  float4 x[PER];
+  auto load_tile = [&](int32_t b) {
+    const int64_t r0 = (int64_t)t.bct[b] * kTC;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = tid + i * 256;
+      x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (v < NV) {
+        const int kk = v / (W / 4), f = (v % (W / 4)) * 4;
+        if (r0 + kk < t.col_limit) x[i] = *reinterpret_cast<const float4*>(t.u + (r0 + kk) * t.ld + f);
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int v = tid + i * 256;
+      if (v < NV) {
+        const int kk = v / (W / 4), f = (v % (W / 4)) * 4;
+        uint32_t h[4], m[4], l[4];
+        split3(x[i].x, h[0], m[0], l[0]);
+        split3(x[i].y, h[1], m[1], l[1]);
+        split3(x[i].z, h[2], m[2], l[2]);
+        split3(x[i].w, h[3], m[3], l[3]);
+        *reinterpret_cast<uint2*>(&img[buf][0][kk][f]) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        *reinterpret_cast<uint2*>(&img[buf][1][kk][f]) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+        *reinterpret_cast<uint2*>(&img[buf][2][kk][f]) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+      }
+    }
+  };
+
+  double acc[NFB][4];
+#pragma unroll
+  for (int fb = 0; fb < NFB; ++fb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[fb][i] = 0.0;
+
+  // transposed-read address of this lane: group g = lane >> 4 reads rows 8g + q (+4), q = (lane & 15) >> 2,
+  // columns 4 (lane & 3) .. +3 of each 16-column block
+  const int trow = 8 * (lane >> 4) + ((lane & 15) >> 2);
+  const int tcolo = 4 * (lane & 3);
+  const int mrow = 16 * wave + (lane & 15);  // this lane's A row (of the block)
+  const int mshift = 8 * (lane >> 4);        // its byte of the 32-bit row mask
+
+  if (it.y < it.z) {
+    load_tile(it.y);
+    store_tile(0);
+  }
+  for (int32_t b = it.y; b < it.z; ++b) {
+    const int buf = (b - it.y) & 1;
+    __syncthreads();  // tile b staged; buffer buf ^ 1 no longer read
+    if (b + 1 < it.z) load_tile(b + 1);
+    const uint32_t m = t.bmask[(int64_t)b * kTR + mrow];
+    const uint4 av = lut[(m >> mshift) & 0xFFu];
+    const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+#pragma unroll
+    for (int fb = 0; fb < NFB; ++fb) {
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 2; p >= 0; --p) {  // lo, mid, hi
+        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)(&img[buf][p][trow][16 * fb + tcolo]));
+        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)(&img[buf][p][trow + 4][16 * fb + tcolo]));
+        const s16x8 bv = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bv), c, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[fb][i] += (double)c[i];
+    }
+    if (b + 1 < it.z) store_tile(buf ^ 1);
+  }
+  // D layout of 16x16x32: column = lane & 15, row = 4 (lane >> 4) + i
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = 16 * wave + 4 * (lane >> 4) + i;
+    const int64_t row = rb * kTR + rl;
+    if (it.w < 0 && row >= t.n_plan) continue;
+    double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * kTR + rl) * W;
+#pragma unroll
+    for (int fb = 0; fb < NFB; ++fb) dst[16 * fb + (lane & 15)] = acc[fb][i];
+  }
+}
+
+// row blocks split over several workgroups: part = their slots summed in slot order
+template <int W>
+__global__ __launch_bounds__(256) void tiles_combine_kernel(const int4* __restrict__ multi, const double* __restrict__ slots,
+                                                            double* __restrict__ part, int64_t ld, int64_t n_plan) {
+  const int4 mt = multi[blockIdx.x];
+  for (int e = threadIdx.x; e < kTR * W; e += 256) {
+    const int rl = e / W, f = e - rl * W;
+    const int64_t row = (int64_t)mt.x * kTR + rl;
+    if (row >= n_plan) break;
+    double s = 0.0;
+    for (int q = 0; q < mt.z; ++q) s += slots[((int64_t)(mt.y + q) * kTR + rl) * W + f];
+    part[row * ld + f] = s;
+  }
+}
+
+template <typename T>
+int upload(T** d, const std::vector<T>& h) {
+  if (int rc = dmalloc(d, h.size())) return rc;
+  if (!h.empty()) WG_HIP_TRY(hipMemcpy(*d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  return WG_OK;
+}
+
+int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
+  const int64_t n = L->n_rows, nnz = L->nnz;
+  const int64_t n_plan = active_only ? L->n_active : n;
+  const int64_t col_limit = active_only ? L->n_active : L->n_cols;  // closed-form rows are never gathered
+  const int th = std::max(1, L->tune.tile_th);
+  const int tmax = std::max(1, L->tune.tile_max);
+  std::vector<int32_t> rp(n + 1), col(nnz);
+  WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+  WG_HIP_TRY(hipMemcpy(col.data(), L->col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+  const int64_t n_ct = ceil_div(L->n_cols, kTC);
+  std::vector<int32_t> cnt(n_ct, 0), sel(n_ct, -1), touched, tmp;
+  std::vector<int32_t> bct, tcol(col), tsplit(n);
+  std::vector<uint32_t> bmask;
+  std::vector<int4> items, multi;
+  int32_t n_slots = 0;
+  int64_t dense = 0;
+  for (int64_t r = n_plan; r < n; ++r) tsplit[r] = rp[r];
+  const int64_t n_rb = ceil_div(n_plan, kTR);
+  for (int64_t rb = 0; rb < n_rb; ++rb) {
+    const int64_t r0 = rb * kTR, r1 = std::min<int64_t>(r0 + kTR, n_plan);
+    touched.clear();
+    for (int64_t r = r0; r < r1; ++r)
+      for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
+        const int32_t c = col[e];
+        if (c < 0 || c >= col_limit) return fail(WG_ERR_INVALID, "tiles: column %d of row %lld outside [0, %lld)", c,
+                                                 (long long)r, (long long)col_limit);
+        if (cnt[c / kTC]++ == 0) touched.push_back(c / kTC);
+      }
+    std::sort(touched.begin(), touched.end());
+    const int32_t first = (int32_t)bct.size();
+    for (int32_t ct : touched)
+      if (cnt[ct] >= th) {
+        sel[ct] = (int32_t)bct.size();
+        bct.push_back(ct);
+      }
+    bmask.resize(bct.size() * kTR, 0u);
+    for (int64_t r = r0; r < r1; ++r) {
+      tmp.clear();
+      for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
+        const int32_t c = col[e];
+        const int32_t s = sel[c / kTC];
+        if (s >= 0) {
+          uint32_t& w = bmask[(size_t)s * kTR + (r - r0)];
+          const uint32_t bit = 1u << (c % kTC);
+          if (w & bit) return fail(WG_ERR_INVALID, "tiles: duplicate column %d in row %lld", c, (long long)r);
+          w |= bit;
+          ++dense;
+        } else {
+          tmp.push_back(c);
+        }
+      }
+      tsplit[r] = rp[r + 1] - (int32_t)tmp.size();
+      std::copy(tmp.begin(), tmp.end(), tcol.begin() + tsplit[r]);
+    }
+    for (int32_t ct : touched) {
+      cnt[ct] = 0;
+      sel[ct] = -1;
+    }
+    const int32_t nb = (int32_t)bct.size() - first;
+    if (nb == 0) continue;  // every entry is tail: phase 2 adds no part for these rows
+    const int32_t k = (nb + tmax - 1) / tmax;
+    if (k == 1) {
+      items.push_back(make_int4((int)rb, first, first + nb, -1));
+    } else {
+      for (int32_t q = 0; q < k; ++q)
+        items.push_back(make_int4((int)rb, first + (int32_t)((int64_t)nb * q / k), first + (int32_t)((int64_t)nb * (q + 1) / k),
+                                  n_slots + q));
+      multi.push_back(make_int4((int)rb, n_slots, k, 0));
+      n_slots += k;
+    }
+  }
+  p->n_plan = n_plan;
+  p->col_limit = col_limit;
+  p->n_blocks = (int32_t)bct.size();
+  p->n_items = (int32_t)items.size();
+  p->n_multi = (int32_t)multi.size();
+  p->n_slots = n_slots;
+  p->dense_nnz = dense;
+  int rc = upload(&p->bct, bct);
+  if (!rc) rc = upload(&p->bmask, bmask);
+  if (!rc) rc = upload(&p->items, items);
+  if (!rc) rc = upload(&p->multi, multi);
+  if (!rc) rc = upload(&p->tcol, tcol);
+  if (!rc) rc = upload(&p->tsplit, tsplit);
+  if (rc) return rc;
+  char buf[256];
+  snprintf(buf, sizeof(buf), "tiles: %d dense blocks (64x32, >= %d entries) hold %lld of %lld entries (%.1f %%); %d items, %d split row blocks\n",
+           p->n_blocks, th, (long long)dense, (long long)nnz, nnz ? 100.0 * dense / nnz : 0.0, p->n_items, p->n_multi);
+  p->text = buf;
+  return WG_OK;
+}
+
+}  // namespace
+
+void TilePlan::release() {
+  (void)hipFree(bct);
+  (void)hipFree(bmask);
+  (void)hipFree(items);
+  (void)hipFree(multi);
+  (void)hipFree(tcol);
+  (void)hipFree(tsplit);
+  (void)hipFree(part);
+  (void)hipFree(slots);
+  bct = nullptr;
+  bmask = nullptr;
+  items = nullptr;
+  multi = nullptr;
+  tcol = nullptr;
+  tsplit = nullptr;
+  part = nullptr;
+  slots = nullptr;
+  width = 0;
+}
+
+void release_tiles(wg_laplacian_s* L) {
+  for (int i = 0; i < 2; ++i) {
+    if (L->tiles[i]) {
+      L->tiles[i]->release();
+      delete L->tiles[i];
+      L->tiles[i] = nullptr;
+    }
+    L->tiles_failed[i] = false;
+  }
+}
+
+bool tiles_wanted(const wg_laplacian_s* L, int64_t F) {
+  if (L->tune.tiles == 0 || !L->unit || !L->reordered || F % 16 != 0 || F > 64) return false;
+  return L->tune.tiles == 1 || L->nnz >= ((int64_t)8 << 20);
+}
+
+int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out) {
+  *out = nullptr;
+  active_only = active_only && L->reordered;
+  const int ai = active_only ? 1 : 0;
+  if (L->tiles_failed[ai]) return WG_OK;
+  if (!L->tiles[ai]) {
+    auto* p = new TilePlan();
+    int rc = build_tile_plan(L, active_only, p);
+    if (rc) {
+      p->release();
+      delete p;
+      return rc;
+    }
+    // auto: worth it only when the dense blocks carry a good share of the entries
+    if (p->n_blocks == 0 || (L->tune.tiles < 0 && p->dense_nnz * 10 < L->nnz * 3)) {
+      p->release();
+      delete p;
+      L->tiles_failed[ai] = true;
+      return WG_OK;
+    }
+    L->tiles[ai] = p;
+  }
+  TilePlan* p = L->tiles[ai];
+  if (p->width < F) {  // part / slots for this width
+    (void)hipFree(p->part);
+    (void)hipFree(p->slots);
+    p->part = nullptr;
+    p->slots = nullptr;
+    p->width = 0;
+    int rc = dmalloc(&p->part, (size_t)std::max<int64_t>(1, L->n_rows) * F);
+    if (!rc) rc = dmalloc(&p->slots, (size_t)std::max(1, p->n_slots) * kTR * F);
+    if (rc) return rc;
+    p->width = (int32_t)F;
+  }
+  *out = p;
+  return WG_OK;
+}
+
+int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream) {
+  if (F % 16 != 0 || F > 64 || F > p->width || (reinterpret_cast<uintptr_t>(u) & 15))
+    return fail(WG_ERR_INVALID, "launch_tiles: width %lld (need a multiple of 16 <= %d, 16-B aligned u)", (long long)F,
+                std::min(64, (int)p->width));
+  TileArgs t{};
+  t.u = u;
+  t.ld = F;
+  t.col_limit = p->col_limit;
+  t.n_plan = p->n_plan;
+  t.bct = p->bct;
+  t.bmask = p->bmask;
+  t.items = p->items;
+  t.part = p->part;
+  t.slots = p->slots;
+  if (p->n_items > 0) {
+    const dim3 grid(p->n_items), block(256);
+    switch (F / 16) {
+      case 1: hipLaunchKernelGGL(cheb_tiles_kernel<1>, grid, block, 0, stream, t); break;
+      case 2: hipLaunchKernelGGL(cheb_tiles_kernel<2>, grid, block, 0, stream, t); break;
+      case 3: hipLaunchKernelGGL(cheb_tiles_kernel<3>, grid, block, 0, stream, t); break;
+      default: hipLaunchKernelGGL(cheb_tiles_kernel<4>, grid, block, 0, stream, t); break;
+    }
+    WG_LAUNCH_CHECK();
+  }
+  if (p->n_multi > 0) {
+    const dim3 grid(p->n_multi), block(256);
+    switch (F / 16) {
+      case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
+      case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
+      case 3: hipLaunchKernelGGL(tiles_combine_kernel<48>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
+      default: hipLaunchKernelGGL(tiles_combine_kernel<64>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
+    }
+    WG_LAUNCH_CHECK();
+  }
+  return WG_OK;
+}
+
+}  // namespace wg

@@ -276,12 +276,12 @@ def test_native_chain_clenshaw_small_orders(K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,lds,graph,tiers,blocks,clen", [
-    (1, 2, 1, 1, 0, 1), (1, 0, 1, 1, 0, 1), (8, 3, 1, 1, 0, 1), (8, 3, 0, 1, 0, 1), (40, 3, 1, 1, 0, 1),
-    (40, 3, 1, 2, 0, 1), (8, 3, 0, 2, 0, 1), (1, 0, 1, 2, 0, 1), (1, 2, 1, 2, 0, 1),
-    (40, 3, 1, 1, 4, 1), (8, 3, 1, 1, 3, 0), (1, 0, 1, 1, 4, 1), (1, 0, 1, 1, 2, 0), (1, 2, 1, 1, 4, 1),
-    (12, 3, 1, 1, 1, 1)])
-def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen):
+@pytest.mark.parametrize("F,lds,graph,tiers,blocks,clen,tiles", [
+    (1, 2, 1, 1, 0, 1, 0), (1, 0, 1, 1, 0, 1, 0), (8, 3, 1, 1, 0, 1, 0), (8, 3, 0, 1, 0, 1, 0), (40, 3, 1, 1, 0, 1, 0),
+    (40, 3, 1, 2, 0, 1, 0), (8, 3, 0, 2, 0, 1, 0), (1, 0, 1, 2, 0, 1, 0), (1, 2, 1, 2, 0, 1, 0),
+    (40, 3, 1, 1, 4, 1, 0), (8, 3, 1, 1, 3, 0, 0), (1, 0, 1, 1, 4, 1, 0), (1, 0, 1, 1, 2, 0, 0), (1, 2, 1, 1, 4, 1, 0),
+    (12, 3, 1, 1, 1, 1, 0), (48, 3, 1, 1, 0, 1, 1), (41, 3, 0, 1, 0, 1, 1), (48, 3, 1, 2, 0, 1, 1)])
+def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen, tiles):
     """The native exchange with real RCCL traffic on one GPU: a one-rank shard
     whose column space is [own | halo] where the halo columns are copies of own
     rows (every entry (i, j) with j % 3 == 0 and (i + j) odd reads the copy).
@@ -291,7 +291,8 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen):
     third step launch while tier 1 is in flight).  blocks > 0: row-block
     streaming (each step in `blocks` launches, every block's rows sent while
     the next computes; wg_dist_stream_blocks), with the Clenshaw or the
-    forward chain."""
+    forward chain.  tiles = 1: the hybrid step (csrc/tiles.hip, dense blocks on the
+    matrix cores) over the [own | halo] column space, exchange-then-step."""
     import ctypes
     import wats_hip
     from wats_hip import _lib
@@ -310,7 +311,9 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen):
     L = wats_hip.NormalizedLaplacian(n, torch.from_numpy(g.indptr), torch.from_numpy(cols.astype(np.int32)), None,
                                      n_cols=n + J.size, w_cols=torch.from_numpy(w_ext), device="cuda:0")
     # the two-phase steps (off by default) unless the rows are streamed in blocks
-    L.tune(lds=lds, overlap=0 if blocks else 1, clenshaw=clen)
+    L.tune(lds=lds, overlap=0 if (blocks or tiles) else 1, clenshaw=clen)
+    if tiles:
+        L.tune(tiles=1, tile_th=8, tile_max=4)
     lib = _lib.load()
     dev = torch.device("cuda:0")
     caller = torch.from_numpy(J.astype(np.int32)).to(dev)
@@ -345,7 +348,10 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen):
         check(lib.wg_dist_info(h, info), "dist_info")
         # the gather-kernel path overlaps the RCCL exchange with the own-column half of each step,
         # or streams its row blocks
-        assert info[0] == ((2 if blocks else 1) if (F > 1 or lds == 0) else 0), list(info)
+        if tiles:
+            assert "tiles:" in L.describe(F), L.describe(F)
+        else:
+            assert info[0] == ((2 if blocks else 1) if (F > 1 or lds == 0) else 0), list(info)
         assert info[7] == tiers, list(info)
         L.profile_enable(True)
         check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")

@@ -1,0 +1,101 @@
+"""The hybrid step (csrc/tiles.hip): dense (64-row, 32-column) blocks of an
+unweighted graph summed on the matrix cores (three exact bf16 pieces of u per
+block, float32 MFMA sums added in float64), the tail entries by the step
+kernel's phase 2.  Checked against the oracle (reference calibration/WATS.py:29-74)
+and against the all-gather chain (tiles = 0) on the same inputs."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_parity
+from oracle import wats_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import wats_hip  # noqa: E402
+from wats_hip import NormalizedLaplacian  # noqa: E402
+from wats_hip.graphgen import connect_isolated, random_graph, rmat_graph  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _run(L, X, k, **knobs):
+    L.tune(**knobs)
+    return wats_hip.graph_wavelet_features(L, k=k, X0=torch.from_numpy(X), return_S=True)
+
+
+def _close(a, b, what, tol=2e-6):
+    a, b = _np(a).astype(np.float64), _np(b).astype(np.float64)
+    scale = np.max(np.abs(b), axis=0) + 1e-30
+    err = np.max(np.abs(a - b), axis=0) / scale
+    assert np.all(err <= tol), f"{what}: hybrid vs gather max norm-wise err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("F", [16, 41, 48, 64, 32])
+@pytest.mark.parametrize("k", [1, 2, 3, 16])
+def test_tiles_vs_oracle_and_gather(F, k):
+    """Every dense-block threshold / split shape against the oracle and the
+    all-gather chain: tile_th 1 (every touched block dense), 8, 64; tile_max 1
+    and 3 (long row blocks over many slots, combined in order)."""
+    g = rmat_graph(4000, 120000, seed=F + k)
+    A = g.to_scipy()
+    X = np.random.default_rng(F * 31 + k).standard_normal((g.n, F)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=k, s=0.8, X0=X, return_all=True)
+    L = NormalizedLaplacian.from_graph(g)
+    H0, S0 = _run(L, X, k, tiles=0)
+    for knobs in (dict(tile_th=64, tile_max=128), dict(tile_th=8, tile_max=3), dict(tile_th=1, tile_max=1)):
+        H1, S1 = _run(L, X, k, tiles=1, **knobs)
+        if k >= 2:
+            assert "tiles:" in L.describe(F), f"hybrid step not planned: {L.describe(F)}"
+        assert_parity(_np(S1), ref["S"], what=f"F={F} K={k} {knobs} S")
+        assert_parity(_np(H1), ref["H"], what=f"F={F} K={k} {knobs} H")
+        _close(S1, S0, f"F={F} K={k} {knobs} S")
+
+
+def test_tiles_isolated_rows_and_no_closed_form():
+    """Closed-form rows (never gathered) next to dense hubs, and the same graph with
+    every isolated node attached (no closed-form rows: all rows in the chain)."""
+    g = rmat_graph(6000, 150000, seed=5)
+    for gg in (g, connect_isolated(g, seed=1)):
+        A = gg.to_scipy()
+        X = np.random.default_rng(7).standard_normal((gg.n, 48)).astype(np.float32)
+        ref = O.graph_wavelet_features(A, k=8, s=0.8, X0=X, return_all=True)
+        L = NormalizedLaplacian.from_graph(gg)
+        H0, S0 = _run(L, X, 8, tiles=0)
+        H1, S1 = _run(L, X, 8, tiles=1, tile_th=16)
+        assert "tiles:" in L.describe(48)
+        assert_parity(_np(S1), ref["S"], what="S")
+        assert_parity(_np(H1), ref["H"], what="H")
+        _close(S1, S0, "S")
+
+
+def test_tiles_deterministic():
+    g = rmat_graph(4000, 120000, seed=9)
+    X = np.random.default_rng(1).standard_normal((g.n, 48)).astype(np.float32)
+    L = NormalizedLaplacian.from_graph(g)
+    _, S1 = _run(L, X, 16, tiles=1, tile_th=8, tile_max=2)
+    _, S2 = _run(L, X, 16)
+    assert torch.equal(S1, S2), "the hybrid chain must be bitwise reproducible"
+
+
+def test_tiles_not_taken_for_weighted_or_narrow():
+    """Weighted graphs (values read) and widths that are not a multiple of 16 keep
+    the gather kernel."""
+    g = random_graph(2000, 0.02, seed=3, directed=False, weighted=True)
+    X = np.random.default_rng(2).standard_normal((g.n, 48)).astype(np.float32)
+    L = NormalizedLaplacian.from_graph(g)
+    _run(L, X, 4, tiles=1)
+    assert "tiles:" not in L.describe(48)
+    g = rmat_graph(4000, 120000, seed=2)
+    X = np.random.default_rng(2).standard_normal((g.n, 8)).astype(np.float32)
+    L = NormalizedLaplacian.from_graph(g)
+    _run(L, X, 4, tiles=1)
+    assert "tiles:" not in L.describe(8)
