@@ -186,6 +186,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "tile_th")) {
     if (value < 1 || value > 2048) return fail(WG_ERR_INVALID, "tile_th must be in [1, 2048]");
     L->tune.tile_th = (int32_t)value;
+  } else if (!strcmp(key, "tiles_overlap")) {
+    L->tune.tiles_overlap = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_max")) {
     if (value < 1 || value > 1 << 20) return fail(WG_ERR_INVALID, "tile_max must be in [1, 2^20]");
     L->tune.tile_max = (int32_t)value;
@@ -311,7 +314,10 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   // workspace: T ping-pong (2) + internal S [+ u ping-pong, padded to whole column blocks], 256-B aligned
   const size_t stride = ((size_t)n * Fp + 63) / 64 * 64;
   const size_t ustride = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
-  const size_t need = 3 * stride + 2 * ustride;
+  // the hybrid step (tiles.hip) gathers the first step's X0 value-free too, as u_0 = X0 * dinv
+  const bool u0 = !lp && L->tune.clenshaw && K >= 1 && L->unit && L->tune.uscale && !L->tune.gbuf &&
+                  L->tune.hubf == 0 && L->tune.hot == 0 && tiles_wanted(L, Fp);
+  const size_t need = (u0 ? 4 : 3) * stride + 2 * ustride;
   if (L->ws_floats < need) {
     WG_HIP_TRY(hipStreamSynchronize(stream));
     (void)hipFree(L->ws);
@@ -366,14 +372,17 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     // unweighted graphs: every stored b_k as u_k = b_k * dinv, so the gathers read no CSR values
     // (L_hat b = -dinv_i sum_j u_j); X0 itself stays unscaled (the first step reads the values)
     const int useu = (L->unit && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 && L->tune.hot == 0) ? 1 : 0;
+    float* ub = u0 ? L->ws + 3 * stride : nullptr;  // u_0 = X0 * dinv (active rows)
+    if (u0 && (rc = launch_scale_rows(L, L->n_active, Fp, b0, ub, stream))) return rc;
     for (int32_t k = K - 1; k >= 1; --k) {
       float* out = bk2 ? bk2 : bufs[nb++];
       const double ck = c[k] - (bk2 == nullptr && k + 2 == K ? c[K] : 0.0);  // implicit b_{k+2} = c_K X0
       ClenArgs cl{b0, ck, cacc, 0};
-      cl.uin = useu && bk1 != b0;
+      cl.uin = useu && (bk1 != b0 || u0);
       cl.uprev = useu && bk2 != nullptr;
       cl.uout = useu;
-      rc = launch_step(L, 2, Fp, bk1, bk2, out, nullptr, nullptr, 1.0, 0.0, stream, /*active_only=*/true, nullptr, &cl);
+      rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? ub : bk1, bk2, out, nullptr, nullptr, 1.0, 0.0, stream,
+                       /*active_only=*/true, nullptr, &cl);
       if (rc) return rc;
       bk2 = const_cast<float*>(bk1 == b0 ? nullptr : bk1);
       bk1 = out;
@@ -382,9 +391,9 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     // final: S = c_0 X0 + L_hat b_1 - b_2 (K == 1: L_hat b_1 = c_1 L_hat X0; K == 2: b_2 = c_2 X0)
     const double c0 = c[0] - (K == 2 ? c[2] : 0.0);
     ClenArgs cl{b0, c0, K == 1 ? c[1] : 1.0, 1};
-    cl.uin = useu && bk1 != b0;
+    cl.uin = useu && (bk1 != b0 || u0);
     cl.uprev = useu && K >= 3;
-    rc = launch_step(L, 2, Fp, bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
+    rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? ub : bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
                      1.0, 0.0, stream, /*active_only=*/true, fuse_fin ? S : nullptr, &cl);
     if (rc) return rc;
   } else {

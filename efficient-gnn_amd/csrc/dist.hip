@@ -614,6 +614,10 @@ struct wg_dist_s {
       // DESIGN.md 4.1) and the halo rows exchanged are u rows; X0 (phase 1) stays unscaled
       const int useu = (L->unit && L->values_null && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 &&
                         L->tune.hot == 0) ? 1 : 0;
+      // the hybrid step (tiles.hip): phase 1 exchanges and gathers u_0 = X0 * dinv (own rows scaled
+      // in place; x0 keeps X0) value-free like every later phase
+      const bool u0 = useu && tiles_wanted(L, Fp);
+      if (!rc && u0) rc = launch_scale_rows(L, n_own, Fp, x0, A[0], st);
       for (int32_t j = 1; j <= K && !rc; ++j) {
         const int32_t k = K - j;  // this phase computes b_k (k = 0: the final S)
         float* cur = A[(j - 1) & 1];
@@ -621,7 +625,7 @@ struct wg_dist_s {
         const double ck = c[k] - (j == 2 ? c[K] : 0.0);
         const double cacc = (j == 1) ? (k == 0 ? c[K] : 2.0 * c[K]) : (k == 0 ? 1.0 : 2.0);
         ClenArgs cl{x0, ck, cacc, k == 0 ? 1 : 0};
-        cl.uin = useu && j >= 2;          // j == 1 gathers X0 itself
+        cl.uin = useu && (j >= 2 || u0);  // j == 1 gathers X0 itself, or u_0
         cl.uprev = useu && prev_stored;
         cl.uout = useu;                   // ignored on the final step (k == 0 writes S)
         auto launch = [&](hipStream_t s2, const PhaseArgs* ph) {

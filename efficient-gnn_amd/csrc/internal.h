@@ -133,8 +133,8 @@ struct Lds1Plan {
 // Hybrid step (tiles.hip) for wide signals on large unweighted graphs: internal rows in
 // blocks of 64, columns in tiles of 32; each (row block, column tile) pair holding at
 // least tile_th entries is a dense block, summed on the matrix cores from its 64 row
-// masks of 32 bits; the rest of each row (its "tail") sits at the end of the row's range
-// in tcol and is summed by the step kernel's phase 2, which adds the blocks' sums (part).
+// masks of 32 bits; the rest of each row (its "tail") comes first in the row's range of
+// tcol and is gathered by the step kernel (phases 4, or 1 + 6), which adds the blocks' sums.
 struct TilePlan {
   int64_t n_plan = 0;          // rows planned: [0, n_plan)
   int64_t col_limit = 0;       // column rows a block may read (rows >= col_limit of the tile read as 0)
@@ -144,10 +144,11 @@ struct TilePlan {
   uint32_t* bmask = nullptr;   // device [n_blocks][64]: row masks (bit k = column 32 * tile + k)
   int4* items = nullptr;       // device [n_items]: {row block, first block, end block, slot or -1}
   int4* multi = nullptr;       // device [n_multi]: {row block, first slot, slots, 0}
-  int32_t* tcol = nullptr;     // device [nnz]: each row's tail entries at the end of its range
-  int32_t* tsplit = nullptr;   // device [n_rows]: first tail entry of each row
-  int32_t width = 0;           // doubles per row of part / slots
-  double* part = nullptr;      // device [n_rows][width]
+  int32_t* tcol = nullptr;     // device [nnz]: each row's tail entries first (the rest of its range unused)
+  int32_t* tsplit = nullptr;   // device [n_rows]: end of each row's tail (== row end: no dense entries)
+  int32_t width = 0;           // doubles per row of part / part2 / slots
+  double* part = nullptr;      // device [n_rows][width]: the dense blocks' sums
+  double* part2 = nullptr;     // device [n_rows][width]: the tail sums (tiles_overlap)
   double* slots = nullptr;     // device [n_slots][64][width]
   std::string text;
   void release();
@@ -200,6 +201,7 @@ struct Tuning {
                              // >= 30 % of the entries in dense blocks), 0 = off, 1 = whenever it applies
   int32_t tile_th = 64;      // entries that make a 64 x 32 (row block, column tile) pair a dense block
   int32_t tile_max = 128;    // dense blocks per workgroup (longer row blocks split over slots)
+  int32_t tiles_overlap = 1; // hybrid step: the tail gathers on a side stream beside the dense blocks
 };
 
 }  // namespace wg
@@ -239,6 +241,8 @@ struct wg_laplacian_s {
   bool lds1_failed[2] = {false, false};        // not applicable (too many blocks): use the gather kernel
   wg::TilePlan* tiles[2] = {nullptr, nullptr};  // [active_only] hybrid step plans (released with lds1)
   bool tiles_failed[2] = {false, false};
+  hipStream_t side = nullptr;                   // hybrid step: the tail gathers' stream (tiles_overlap)
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
   // workspace for wg_wavelet_features
   float* ws = nullptr;
   size_t ws_floats = 0;
@@ -288,10 +292,10 @@ struct PhaseArgs {
   const int32_t* rsplit = nullptr;   // [n_rows] first entry with column >= n_rows (rows column-sorted)
   const int32_t* rsplit2 = nullptr;  // [n_rows] first tier-1 halo entry (two tiers), else nullptr
   double* part = nullptr;            // [n_rows][F]
-  // hybrid step (internal to launch_step): phase 2 over the tail columns `col`, adding part only
-  // to rows with dense entries (rsplit[row] > rowptr[row])
+  // hybrid step (internal to launch_step, tiles.hip): phases 1 / 4 / 6 over the tail-first
+  // column array `col` (rsplit = each row's tail end); part2 = the dense blocks' sums (phase 6)
   const int32_t* col = nullptr;
-  int part_cond = 0;
+  const double* part2 = nullptr;
 };
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
@@ -322,6 +326,10 @@ bool tiles_wanted(const wg_laplacian_s* L, int64_t F);
 int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out);
 int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream);
 void release_tiles(wg_laplacian_s* L);
+int side_stream(wg_laplacian_s* L);  // creates L->side and its fork / join events once
+// u = x * dinv for rows [0, n) of an F-wide signal (in place allowed): the hybrid chain's first
+// step gathers u_0 = X0 * dinv value-free like every later step
+int launch_scale_rows(wg_laplacian_s* L, int64_t n, int64_t F, const float* x, float* u, hipStream_t stream);
 // lds1.hip
 int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out);  // *out = nullptr: not applicable
 void release_lds1(wg_laplacian_s* L);

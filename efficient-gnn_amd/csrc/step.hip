@@ -86,15 +86,22 @@ struct StepArgs {
   const int32_t* rsplit2;
   double* part;
   int32_t probe;  // timing probe (knob "probe"): gathers only -- no epilogue operands, acc stored to xk
-  int32_t part_cond;  // hybrid step (tiles.hip): phase 2 adds part only to rows with dense entries
+  // hybrid step (tiles.hip; col = the tail-first column array, rsplit = each row's tail end):
+  // phase 4 sums the tail [e0, rsplit[row]), adds part (the dense blocks' sums) to rows with
+  // dense entries and runs the epilogue; with the dense blocks overlapped, phase 1 sums the
+  // tail into part on a side stream and phase 6 (no entries) adds part + part2 (the blocks'
+  // sums, rows with dense entries) and runs the epilogue
+  const double* part2;
 };
 
 // the entry range of a row (or of a split-row chunk) this launch's phase covers
 __device__ __forceinline__ void phase_range(const StepArgs& a, int64_t row, int32_t& e0, int32_t& e1) {
   if (a.phase == 0) return;
   const int32_t sp = a.rsplit[row];
-  if (a.phase == 1) {
+  if (a.phase == 1 || a.phase == 4) {
     e1 = min(e1, sp);
+  } else if (a.phase == 6) {
+    e1 = e0;
   } else if (a.phase == 3) {
     e0 = max(e0, sp);
     e1 = min(e1, a.rsplit2[row]);
@@ -123,8 +130,21 @@ __device__ __forceinline__ void part_store(const StepArgs& a, int64_t row, int f
 
 template <int VEC>
 __device__ __forceinline__ void part_add(const StepArgs& a, int64_t row, int fs, double (&acc)[VEC]) {
-  if (a.part_cond && a.rsplit[row] == a.rowptr[row]) return;  // no dense entries: no part written
-  const double* p = a.part + row * a.ld + (int64_t)fs * VEC;
+  const int64_t off = row * a.ld + (int64_t)fs * VEC;
+  if (a.phase >= 4) {  // hybrid step: the blocks' sums only for rows with dense entries
+    const bool dense = a.rsplit[row] != a.rowptr[row + 1];
+    if (a.phase == 6) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += a.part[off + j];
+    }
+    const double* p2 = a.phase == 6 ? a.part2 : a.part;
+    if (dense) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += p2[off + j];
+    }
+    return;
+  }
+  const double* p = a.part + off;
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] += p[j];
 }
@@ -621,7 +641,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       if (to_part(a)) {
         part_store<VEC>(a, row, fs, acc);
       } else {
-        if (a.phase == 2) part_add<VEC>(a, row, fs, acc);
+        if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, fs, acc);
         step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
       }
     }
@@ -680,7 +700,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       if (to_part(a)) {
         part_store<VEC>(a, row, t, acc);
       } else {
-        if (a.phase == 2) part_add<VEC>(a, row, t, acc);
+        if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, t, acc);
         step_epilogue<VEC>(a, row, t, acc, in, 0);
       }
     } else {
@@ -721,7 +741,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       if (to_part(a)) {
         part_store<VEC>(a, row, t, sum);
       } else {
-        if (a.phase == 2) part_add<VEC>(a, row, t, sum);
+        if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, t, sum);
         step_epilogue<VEC>(a, row, t, sum, in2, 0);
       }
     }
@@ -793,7 +813,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
     part_store<VEC>(a, row, fs, acc);
     return;
   }
-  if (a.phase == 2) part_add<VEC>(a, row, fs, acc);
+  if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, fs, acc);
   step_epilogue<VEC>(a, row, fs, acc, in, sg * LF);
 }
 
@@ -1306,113 +1326,138 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
   if (ph && ph->phase != 0 && (!ph->rsplit || !ph->part || S_out || (ph->phase == 3 && !ph->rsplit2)))
     return fail(WG_ERR_INVALID, "launch_step: a phased step needs rsplit (phase 3: rsplit2), part, no fused finalize");
   if (int rc = prof_mark(L, stream, true)) return rc;
-  // hybrid step (tiles.hip): the value-free Clenshaw steps of wide signals on large unweighted
-  // graphs sum their dense blocks on the matrix cores into part, then run phase 2 over the tail
-  PhaseArgs hyb;
-  if (cl && cl->uin && !(ph && (ph->phase != 0 || ph->block >= 0)) && !L->tune.probe && tiles_wanted(L, F)) {
-    TilePlan* tp = nullptr;
-    if (int rc = get_tile_plan(L, active_only, F, &tp)) return rc;
-    if (tp) {
-      if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
-      hyb.phase = 2;
-      hyb.rsplit = tp->tsplit;
-      hyb.part = tp->part;
-      hyb.col = tp->tcol;
-      hyb.part_cond = 1;
-      ph = &hyb;
-    }
-  }
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H, S_out});
   int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
   if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
   const bool fuse_h = (H != nullptr) && F <= max_tile;
   if (S_out && !(fuse_h && S)) return fail(WG_ERR_INVALID, "launch_step: fused finalize needs one tile and S");
-  for (int64_t f0 = 0; f0 < F; f0 += max_tile) {
-    const int64_t fw = std::min<int64_t>(max_tile, F - f0);
-    const int LF = (int)(fw / vec);
-    Plan* plan = nullptr;
-    const bool ranged = ph && ph->block >= 0;
-    int rc = ranged ? get_plan(L, LF, vec, false, &plan, ph->block, ph->row_begin, ph->row_end)
-                    : get_plan(L, LF, vec, active_only, &plan);
-    if (rc) return rc;
-    StepArgs a{};
-    a.rowptr = L->rowptr;
-    a.col = (ph && ph->col) ? ph->col : L->col;
-    a.val = L->val;
-    a.iso = L->iso;
-    a.xm1 = xm1 + f0;
-    a.xm2 = xm2 ? xm2 + f0 : nullptr;
-    a.xk = xk ? xk + f0 : nullptr;
-    a.S = S ? S + f0 : nullptr;
-    a.H = fuse_h ? H + f0 : nullptr;
-    a.out_perm = S_out ? L->perm : nullptr;
-    a.S_out = S_out;
-    a.ld = F;
-    a.LF = LF;
-    a.k = k;
-    a.alpha0 = alpha0;
-    a.alpha_k = alpha_k;
-    if (cl) {  // Clenshaw: the generic (k >= 2) paths, S written only by the final step
-      a.k = 2;
-      a.clen = cl->final_ ? 2 : 1;
-      a.x0 = cl->x0 + f0;
-      a.ck = cl->ck;
-      a.cacc = cl->cacc;
-      if (!cl->final_) a.S = nullptr;
-      a.dinv = L->dinv;
-      a.uin = cl->uin;
-      a.uprev = cl->uprev;
-      a.uout = cl->final_ ? 0 : cl->uout;
-      if (a.uin) a.val = nullptr;  // unweighted: the gathered u needs no values
-    }
-    if (ph && ph->phase != 0) {
-      a.phase = ph->phase;
-      a.rsplit = ph->rsplit;
-      a.rsplit2 = ph->rsplit2;
-      a.part = ph->part + f0;
-      a.part_cond = ph->part_cond;
-      if (a.phase == 1 || a.phase == 3) {  // nothing but the sums: no epilogue operands, no T / S / H stores
-        a.xk = nullptr;
-        a.S = nullptr;
-        a.H = nullptr;
+  auto tiles_loop = [&](hipStream_t stream, const PhaseArgs* ph) -> int {
+    for (int64_t f0 = 0; f0 < F; f0 += max_tile) {
+      const int64_t fw = std::min<int64_t>(max_tile, F - f0);
+      const int LF = (int)(fw / vec);
+      Plan* plan = nullptr;
+      const bool ranged = ph && ph->block >= 0;
+      int rc = ranged ? get_plan(L, LF, vec, false, &plan, ph->block, ph->row_begin, ph->row_end)
+                      : get_plan(L, LF, vec, active_only, &plan);
+      if (rc) return rc;
+      StepArgs a{};
+      a.rowptr = L->rowptr;
+      a.col = (ph && ph->col) ? ph->col : L->col;
+      a.val = L->val;
+      a.iso = L->iso;
+      a.xm1 = xm1 + f0;
+      a.xm2 = xm2 ? xm2 + f0 : nullptr;
+      a.xk = xk ? xk + f0 : nullptr;
+      a.S = S ? S + f0 : nullptr;
+      a.H = fuse_h ? H + f0 : nullptr;
+      a.out_perm = S_out ? L->perm : nullptr;
+      a.S_out = S_out;
+      a.ld = F;
+      a.LF = LF;
+      a.k = k;
+      a.alpha0 = alpha0;
+      a.alpha_k = alpha_k;
+      if (cl) {  // Clenshaw: the generic (k >= 2) paths, S written only by the final step
+        a.k = 2;
+        a.clen = cl->final_ ? 2 : 1;
+        a.x0 = cl->x0 + f0;
+        a.ck = cl->ck;
+        a.cacc = cl->cacc;
+        if (!cl->final_) a.S = nullptr;
+        a.dinv = L->dinv;
+        a.uin = cl->uin;
+        a.uprev = cl->uprev;
+        a.uout = cl->final_ ? 0 : cl->uout;
+        if (a.uin) a.val = nullptr;  // unweighted: the gathered u needs no values
       }
+      if (ph && ph->phase != 0) {
+        a.phase = ph->phase;
+        a.rsplit = ph->rsplit;
+        a.rsplit2 = ph->rsplit2;
+        a.part = ph->part + f0;
+        a.part2 = ph->part2;
+        if (a.phase == 1 || a.phase == 3) {  // nothing but the sums: no epilogue operands, no T / S / H stores
+          a.xk = nullptr;
+          a.S = nullptr;
+          a.H = nullptr;
+        }
+      }
+      a.probe = L->tune.probe;
+      if (a.probe && !a.xk) a.xk = S ? S + f0 : nullptr;  // the final step of a chain stores into S
+      a.chunks = plan->chunks;
+      a.partial = plan->partial;
+      // split rows index rowchunks / arrivals by internal row; a row-block plan's start at row0
+      a.rowchunks = plan->rowchunks ? plan->rowchunks - plan->row0 : nullptr;
+      a.arrivals = (L->tune.inkernel_combine && plan->n_split > 0) ? plan->arrivals - plan->row0 : nullptr;
+      a.seg_mask = L->tune.seg_mask;
+      // non-temporal T_k / S stores only for large per-step streams (ogbn-arxiv F=40, 30 MB of
+      // T_k + S per step: 40.6 us plain vs 42.0 nt; F=64, 48 MB: 55.3 vs 56.5; Reddit-size F=44,
+      // 82 MB: 1773 plain vs 1738 nt)
+      const int64_t stream_rows = (active_only && L->reordered) ? L->n_active : L->n_rows;
+      a.nt = L->tune.nt >= 0 ? L->tune.nt : ((stream_rows * F * 8 <= ((int64_t)64 << 20)) ? 0 : 4);
+      a.bcast = L->tune.bcast;
+      // F == 1 gathers on large graphs: int4 index loads and narrower teams (8M R-MAT 8-way
+      // shard: 275.7 us per step with vidx + iter 8 vs 296.9 without; ogbn-arxiv-size F=1:
+      // vidx 12.3 vs 11.5, so only from 16 M nonzeros)
+      a.vidx = L->tune.vidx >= 0 ? L->tune.vidx : (L->nnz >= ((int64_t)16 << 20) ? 1 : 0);
+      a.xm1_bytes = (L->n_cols * F - f0) * (int64_t)sizeof(float);
+      a.gbuf = (L->tune.gbuf && a.xm1_bytes < ((int64_t)1 << 31)) ? 1 : 0;
+      // hub rows: LDS = (hubf + 1) * tile + the block-mode buffer (NW*64*VEC doubles) <= 160 KiB
+      a.hubf = (vec == 4 && a.xm1_bytes < ((int64_t)1 << 31) && !ranged)
+                   ? (int32_t)std::min<int64_t>({(int64_t)L->tune.hubf, L->n_cols,
+                                                 (int64_t)((160 * 1024 - 64 - plan->nw * 64 * vec * 8) /
+                                                           (LF * vec * 4)) - 1})
+                   : 0;
+      if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
+      else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
+      else rc = launch_step_vec<1>(*plan, a, stream);
+      if (rc) return rc;
     }
-    a.probe = L->tune.probe;
-    if (a.probe && !a.xk) a.xk = S ? S + f0 : nullptr;  // the final step of a chain stores into S
-    a.chunks = plan->chunks;
-    a.partial = plan->partial;
-    // split rows index rowchunks / arrivals by internal row; a row-block plan's start at row0
-    a.rowchunks = plan->rowchunks ? plan->rowchunks - plan->row0 : nullptr;
-    a.arrivals = (L->tune.inkernel_combine && plan->n_split > 0) ? plan->arrivals - plan->row0 : nullptr;
-    a.seg_mask = L->tune.seg_mask;
-    // non-temporal T_k / S stores only for large per-step streams (ogbn-arxiv F=40, 30 MB of
-    // T_k + S per step: 40.6 us plain vs 42.0 nt; F=64, 48 MB: 55.3 vs 56.5; Reddit-size F=44,
-    // 82 MB: 1773 plain vs 1738 nt)
-    const int64_t stream_rows = (active_only && L->reordered) ? L->n_active : L->n_rows;
-    a.nt = L->tune.nt >= 0 ? L->tune.nt : ((stream_rows * F * 8 <= ((int64_t)64 << 20)) ? 0 : 4);
-    a.bcast = L->tune.bcast;
-    // F == 1 gathers on large graphs: int4 index loads and narrower teams (8M R-MAT 8-way
-    // shard: 275.7 us per step with vidx + iter 8 vs 296.9 without; ogbn-arxiv-size F=1:
-    // vidx 12.3 vs 11.5, so only from 16 M nonzeros)
-    a.vidx = L->tune.vidx >= 0 ? L->tune.vidx : (L->nnz >= ((int64_t)16 << 20) ? 1 : 0);
-    a.xm1_bytes = (L->n_cols * F - f0) * (int64_t)sizeof(float);
-    a.gbuf = (L->tune.gbuf && a.xm1_bytes < ((int64_t)1 << 31)) ? 1 : 0;
-    // hub rows: LDS = (hubf + 1) * tile + the block-mode buffer (NW*64*VEC doubles) <= 160 KiB
-    a.hubf = (vec == 4 && a.xm1_bytes < ((int64_t)1 << 31) && !ranged)
-                 ? (int32_t)std::min<int64_t>({(int64_t)L->tune.hubf, L->n_cols,
-                                               (int64_t)((160 * 1024 - 64 - plan->nw * 64 * vec * 8) /
-                                                         (LF * vec * 4)) - 1})
-                 : 0;
-    if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
-    else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
-    else rc = launch_step_vec<1>(*plan, a, stream);
-    if (rc) return rc;
+    return WG_OK;
+  };
+  auto finish = [&]() -> int {
+    if (H && !fuse_h && !(ph && (ph->phase == 1 || ph->phase == 3))) {
+      hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(L->n_rows, 4)), dim3(kBlock), 0, stream, L->n_rows, F, S, H);
+      WG_LAUNCH_CHECK();
+    }
+    return prof_mark(L, stream, false);
+  };
+  // hybrid step (tiles.hip): the value-free Clenshaw steps of wide signals on large unweighted
+  // graphs sum their dense blocks on the matrix cores (part) and gather only each row's tail:
+  // either after the blocks (phase 4), or -- tiles_overlap -- the tail into part2 on a side
+  // stream while the blocks run, then an epilogue-only launch (phase 6)
+  if (cl && cl->uin && !(ph && (ph->phase != 0 || ph->block >= 0)) && !L->tune.probe && tiles_wanted(L, F)) {
+    TilePlan* tp = nullptr;
+    if (int rc = get_tile_plan(L, active_only, F, &tp)) return rc;
+    if (tp) {
+      PhaseArgs hyb;
+      hyb.rsplit = tp->tsplit;
+      hyb.col = tp->tcol;
+      if (L->tune.tiles_overlap) {
+        if (int rc = side_stream(L)) return rc;
+        PhaseArgs p1 = hyb;
+        p1.phase = 1;
+        p1.part = tp->part2;
+        WG_HIP_TRY(hipEventRecord(L->side_fork, stream));
+        WG_HIP_TRY(hipStreamWaitEvent(L->side, L->side_fork, 0));
+        if (int rc = tiles_loop(L->side, &p1)) return rc;
+        WG_HIP_TRY(hipEventRecord(L->side_join, L->side));
+        if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
+        WG_HIP_TRY(hipStreamWaitEvent(stream, L->side_join, 0));
+        hyb.phase = 6;
+        hyb.part = tp->part2;
+        hyb.part2 = tp->part;
+      } else {
+        if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
+        hyb.phase = 4;
+        hyb.part = tp->part;
+      }
+      if (int rc = tiles_loop(stream, &hyb)) return rc;
+      return finish();
+    }
   }
-  if (H && !fuse_h && !(ph && (ph->phase == 1 || ph->phase == 3))) {
-    hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(L->n_rows, 4)), dim3(kBlock), 0, stream, L->n_rows, F, S, H);
-    WG_LAUNCH_CHECK();
-  }
-  return prof_mark(L, stream, false);
+  if (int rc = tiles_loop(stream, ph)) return rc;
+  return finish();
 }
 
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef, float* S,

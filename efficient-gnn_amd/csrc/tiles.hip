@@ -10,7 +10,9 @@
 // its 32 rows of u once (6 KB, coalesced), shared by the 64 rows of the block.
 //
 //   part[row] = sum over the row's dense entries of u_j      (this file)
-//   step      = phase 2 of cheb_step_kernel over the tail entries, + part, epilogue
+//   step      = cheb_step_kernel over the tail entries (each row's tail first in
+//               tcol), + part, epilogue: phase 4 after the blocks, or (tiles_overlap)
+//               phase 1 into part2 on a side stream beside them, then phase 6
 //
 // The block sum is a 64 x 32 by 32 x W product A.U with A a 0/1 matrix (exact in
 // bf16).  U is split exactly into three bf16 pieces, u = hi + mid + lo
@@ -39,6 +41,9 @@ namespace {
 
 constexpr int kTR = 64;  // rows per row block (4 waves x 16)
 constexpr int kTC = 32;  // columns per tile (the MFMA's K)
+#ifndef TILES_MIN_WAVES
+#define TILES_MIN_WAVES 1
+#endif
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -70,7 +75,7 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 }
 
 template <int NFB>
-__global__ __launch_bounds__(256) void cheb_tiles_kernel(TileArgs t) {
+__global__ __launch_bounds__(256, TILES_MIN_WAVES) void cheb_tiles_kernel(TileArgs t) {
   constexpr int W = 16 * NFB;          // signal width
   constexpr int NV = kTC * W / 4;      // float4 per tile
   constexpr int PER = (NV + 255) / 256;
@@ -173,18 +178,38 @@ __global__ __launch_bounds__(256) void cheb_tiles_kernel(TileArgs t) {
 }
 
 // row blocks split over several workgroups: part = their slots summed in slot order
+// (blockIdx.y = the split row block, blockIdx.x = 256 of its 64 * W sums; the slot loads
+// are independent, four in flight per thread)
 template <int W>
 __global__ __launch_bounds__(256) void tiles_combine_kernel(const int4* __restrict__ multi, const double* __restrict__ slots,
                                                             double* __restrict__ part, int64_t ld, int64_t n_plan) {
-  const int4 mt = multi[blockIdx.x];
-  for (int e = threadIdx.x; e < kTR * W; e += 256) {
-    const int rl = e / W, f = e - rl * W;
-    const int64_t row = (int64_t)mt.x * kTR + rl;
-    if (row >= n_plan) break;
-    double s = 0.0;
-    for (int q = 0; q < mt.z; ++q) s += slots[((int64_t)(mt.y + q) * kTR + rl) * W + f];
-    part[row * ld + f] = s;
+  const int4 mt = multi[blockIdx.y];
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= kTR * W) return;
+  const int rl = e / W, f = e - rl * W;
+  const int64_t row = (int64_t)mt.x * kTR + rl;
+  if (row >= n_plan) return;
+  const double* p = slots + ((int64_t)mt.y * kTR + rl) * W + f;
+  constexpr int64_t step = (int64_t)kTR * W;
+  double s = 0.0;
+  int q = 0;
+  for (; q + 4 <= mt.z; q += 4) {
+    const double v0 = p[q * step], v1 = p[(q + 1) * step], v2 = p[(q + 2) * step], v3 = p[(q + 3) * step];
+    s += v0;
+    s += v1;
+    s += v2;
+    s += v3;
   }
+  for (; q < mt.z; ++q) s += p[q * step];
+  part[row * ld + f] = s;
+}
+
+// u = x * dinv row-wise (float64 product rounded once, as the step epilogue stores u)
+__global__ void scale_rows_kernel(int64_t n, int64_t F, const float* __restrict__ x, const double* __restrict__ dinv,
+                                  float* __restrict__ u) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * F) return;
+  u[i] = (float)((double)x[i] * dinv[i / F]);
 }
 
 template <typename T>
@@ -210,7 +235,7 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   std::vector<int4> items, multi;
   int32_t n_slots = 0;
   int64_t dense = 0;
-  for (int64_t r = n_plan; r < n; ++r) tsplit[r] = rp[r];
+  for (int64_t r = n_plan; r < n; ++r) tsplit[r] = rp[r + 1];  // unplanned rows: all tail
   const int64_t n_rb = ceil_div(n_plan, kTR);
   for (int64_t rb = 0; rb < n_rb; ++rb) {
     const int64_t r0 = rb * kTR, r1 = std::min<int64_t>(r0 + kTR, n_plan);
@@ -245,15 +270,15 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
           tmp.push_back(c);
         }
       }
-      tsplit[r] = rp[r + 1] - (int32_t)tmp.size();
-      std::copy(tmp.begin(), tmp.end(), tcol.begin() + tsplit[r]);
+      tsplit[r] = rp[r] + (int32_t)tmp.size();
+      std::copy(tmp.begin(), tmp.end(), tcol.begin() + rp[r]);
     }
     for (int32_t ct : touched) {
       cnt[ct] = 0;
       sel[ct] = -1;
     }
     const int32_t nb = (int32_t)bct.size() - first;
-    if (nb == 0) continue;  // every entry is tail: phase 2 adds no part for these rows
+    if (nb == 0) continue;  // every entry is tail: no part is added to these rows
     const int32_t k = (nb + tmax - 1) / tmax;
     if (k == 1) {
       items.push_back(make_int4((int)rb, first, first + nb, -1));
@@ -296,6 +321,7 @@ void TilePlan::release() {
   (void)hipFree(tcol);
   (void)hipFree(tsplit);
   (void)hipFree(part);
+  (void)hipFree(part2);
   (void)hipFree(slots);
   bct = nullptr;
   bmask = nullptr;
@@ -304,6 +330,7 @@ void TilePlan::release() {
   tcol = nullptr;
   tsplit = nullptr;
   part = nullptr;
+  part2 = nullptr;
   slots = nullptr;
   width = 0;
 }
@@ -317,6 +344,23 @@ void release_tiles(wg_laplacian_s* L) {
     }
     L->tiles_failed[i] = false;
   }
+}
+
+int launch_scale_rows(wg_laplacian_s* L, int64_t n, int64_t F, const float* x, float* u, hipStream_t stream) {
+  if (n <= 0) return WG_OK;
+  if (n > L->n_cols) return fail(WG_ERR_INVALID, "launch_scale_rows: %lld rows > %lld columns", (long long)n,
+                                 (long long)L->n_cols);
+  hipLaunchKernelGGL(scale_rows_kernel, dim3((unsigned)ceil_div(n * F, 256)), dim3(256), 0, stream, n, F, x, L->dinv, u);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
+int side_stream(wg_laplacian_s* L) {
+  if (L->side) return WG_OK;
+  WG_HIP_TRY(hipStreamCreateWithFlags(&L->side, hipStreamNonBlocking));
+  WG_HIP_TRY(hipEventCreateWithFlags(&L->side_fork, hipEventDisableTiming));
+  WG_HIP_TRY(hipEventCreateWithFlags(&L->side_join, hipEventDisableTiming));
+  return WG_OK;
 }
 
 bool tiles_wanted(const wg_laplacian_s* L, int64_t F) {
@@ -349,11 +393,14 @@ int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out
   TilePlan* p = L->tiles[ai];
   if (p->width < F) {  // part / slots for this width
     (void)hipFree(p->part);
+    (void)hipFree(p->part2);
     (void)hipFree(p->slots);
     p->part = nullptr;
+    p->part2 = nullptr;
     p->slots = nullptr;
     p->width = 0;
     int rc = dmalloc(&p->part, (size_t)std::max<int64_t>(1, L->n_rows) * F);
+    if (!rc) rc = dmalloc(&p->part2, (size_t)std::max<int64_t>(1, L->n_rows) * F);
     if (!rc) rc = dmalloc(&p->slots, (size_t)std::max(1, p->n_slots) * kTR * F);
     if (rc) return rc;
     p->width = (int32_t)F;
@@ -387,7 +434,7 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
     WG_LAUNCH_CHECK();
   }
   if (p->n_multi > 0) {
-    const dim3 grid(p->n_multi), block(256);
+    const dim3 grid((unsigned)ceil_div(kTR * F, 256), p->n_multi), block(256);
     switch (F / 16) {
       case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
       case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;

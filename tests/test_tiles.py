@@ -44,7 +44,8 @@ def _close(a, b, what, tol=2e-6):
 def test_tiles_vs_oracle_and_gather(F, k):
     """Every dense-block threshold / split shape against the oracle and the
     all-gather chain: tile_th 1 (every touched block dense), 8, 64; tile_max 1
-    and 3 (long row blocks over many slots, combined in order)."""
+    and 3 (long row blocks over many slots, combined in order); the first step
+    gathers u_0 = X0 * dinv value-free (K = 1: the only step)."""
     g = rmat_graph(4000, 120000, seed=F + k)
     A = g.to_scipy()
     X = np.random.default_rng(F * 31 + k).standard_normal((g.n, F)).astype(np.float32)
@@ -52,12 +53,15 @@ def test_tiles_vs_oracle_and_gather(F, k):
     L = NormalizedLaplacian.from_graph(g)
     H0, S0 = _run(L, X, k, tiles=0)
     for knobs in (dict(tile_th=64, tile_max=128), dict(tile_th=8, tile_max=3), dict(tile_th=1, tile_max=1)):
-        H1, S1 = _run(L, X, k, tiles=1, **knobs)
-        if k >= 2:
-            assert "tiles:" in L.describe(F), f"hybrid step not planned: {L.describe(F)}"
+        H1, S1 = _run(L, X, k, tiles=1, tiles_overlap=1, **knobs)
+        assert "tiles:" in L.describe(F), f"hybrid step not planned: {L.describe(F)}"
         assert_parity(_np(S1), ref["S"], what=f"F={F} K={k} {knobs} S")
         assert_parity(_np(H1), ref["H"], what=f"F={F} K={k} {knobs} H")
         _close(S1, S0, f"F={F} K={k} {knobs} S")
+        # the tail beside the blocks (phase 1 on a side stream + phase 6) or after them (phase 4):
+        # the same sums in the same order
+        H2, S2 = _run(L, X, k, tiles_overlap=0)
+        assert torch.equal(S1, S2) and torch.equal(H1, H2), f"F={F} K={k} {knobs}: overlap changed the bits"
 
 
 def test_tiles_isolated_rows_and_no_closed_form():
