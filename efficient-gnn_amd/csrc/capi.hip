@@ -189,6 +189,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "tiles_overlap")) {
     L->tune.tiles_overlap = value ? 1 : 0;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "tile_rows")) {
+    if (value != 64 && value != 128) return fail(WG_ERR_INVALID, "tile_rows must be 64 or 128");
+    L->tune.tile_rows = (int32_t)value;
   } else if (!strcmp(key, "tile_max")) {
     if (value < 1 || value > 1 << 20) return fail(WG_ERR_INVALID, "tile_max must be in [1, 2^20]");
     L->tune.tile_max = (int32_t)value;

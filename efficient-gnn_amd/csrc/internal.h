@@ -137,11 +137,12 @@ struct Lds1Plan {
 // tcol and is gathered by the step kernel (phases 4, or 1 + 6), which adds the blocks' sums.
 struct TilePlan {
   int64_t n_plan = 0;          // rows planned: [0, n_plan)
+  int32_t rows = 64;           // rows per row block (64 or 128: 4 or 8 waves of 16 rows)
   int64_t col_limit = 0;       // column rows a block may read (rows >= col_limit of the tile read as 0)
   int32_t n_blocks = 0, n_items = 0, n_multi = 0, n_slots = 0;
   int64_t dense_nnz = 0;       // entries inside dense blocks
   int32_t* bct = nullptr;      // device [n_blocks]: column tile of each block
-  uint32_t* bmask = nullptr;   // device [n_blocks][64]: row masks (bit k = column 32 * tile + k)
+  uint32_t* bmask = nullptr;   // device [n_blocks][rows]: row masks (bit k = column 32 * tile + k)
   int4* items = nullptr;       // device [n_items]: {row block, first block, end block, slot or -1}
   int4* multi = nullptr;       // device [n_multi]: {row block, first slot, slots, 0}
   int32_t* tcol = nullptr;     // device [nnz]: each row's tail entries first (the rest of its range unused)
@@ -149,7 +150,7 @@ struct TilePlan {
   int32_t width = 0;           // doubles per row of part / part2 / slots
   double* part = nullptr;      // device [n_rows][width]: the dense blocks' sums
   double* part2 = nullptr;     // device [n_rows][width]: the tail sums (tiles_overlap)
-  double* slots = nullptr;     // device [n_slots][64][width]
+  double* slots = nullptr;     // device [n_slots][rows][width]
   std::string text;
   void release();
 };
@@ -201,7 +202,9 @@ struct Tuning {
                              // >= 30 % of the entries in dense blocks), 0 = off, 1 = whenever it applies
   int32_t tile_th = 64;      // entries that make a 64 x 32 (row block, column tile) pair a dense block
   int32_t tile_max = 128;    // dense blocks per workgroup (longer row blocks split over slots)
-  int32_t tiles_overlap = 1; // hybrid step: the tail gathers on a side stream beside the dense blocks
+  int32_t tiles_overlap = 0; // hybrid step: the tail gathers on a side stream beside the dense blocks
+                             // (Reddit-size F=41: 1176 vs 1136 us per step sequential, r02_tiles: off)
+  int32_t tile_rows = 128;   // hybrid step: rows per row block (64 or 128)
 };
 
 }  // namespace wg

@@ -39,11 +39,7 @@
 namespace wg {
 namespace {
 
-constexpr int kTR = 64;  // rows per row block (4 waves x 16)
 constexpr int kTC = 32;  // columns per tile (the MFMA's K)
-#ifndef TILES_MIN_WAVES
-#define TILES_MIN_WAVES 1
-#endif
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -74,15 +70,18 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
   l = __float_as_uint(r2) >> 16;
 }
 
-template <int NFB>
-__global__ __launch_bounds__(256, TILES_MIN_WAVES) void cheb_tiles_kernel(TileArgs t) {
+template <int NFB, int NWV>
+__global__ __launch_bounds__(64 * NWV) void cheb_tiles_kernel(TileArgs t) {
+  constexpr int TR = 16 * NWV;         // rows per row block (16 per wave)
+  constexpr int NT = 64 * NWV;         // threads
   constexpr int W = 16 * NFB;          // signal width
   constexpr int NV = kTC * W / 4;      // float4 per tile
-  constexpr int PER = (NV + 255) / 256;
-  __shared__ uint4 lut[256];                           // byte -> 8 bf16 (bit j ? 1.0 : 0) in element j
+  constexpr int PER = (NV + NT - 1) / NT;
+  __shared__ uint4 lut[256];                                          // byte -> 8 bf16 (bit j ? 1.0 : 0)
   __shared__ __attribute__((aligned(16))) uint16_t img[2][3][kTC][W];  // [buffer][piece hi/mid/lo][k][f]
+  __shared__ uint32_t msk[2][TR];                                     // [buffer][row] the block's row masks
   const int tid = threadIdx.x;
-  {
+  if (tid < 256) {
     uint32_t d[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -93,23 +92,27 @@ __global__ __launch_bounds__(256, TILES_MIN_WAVES) void cheb_tiles_kernel(TileAr
   const int64_t rb = it.x;
   const int lane = tid & 63, wave = tid >> 6;
 
-  float4 x[PER];
-  auto load_tile = [&](int32_t b) {
+  // a tile's staged data: PER float4 of u and (tid < TR) one row mask, in a 2-deep register
+  // ring so each tile's loads have two tiles' compute to arrive
+  float4 x0[PER], x1[PER];
+  uint32_t w0 = 0, w1 = 0;
+  auto load = [&](float4 (&x)[PER], uint32_t& w, int32_t b) {
     const int64_t r0 = (int64_t)t.bct[b] * kTC;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int v = tid + i * 256;
+      const int v = tid + i * NT;
       x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (v < NV) {
         const int kk = v / (W / 4), f = (v % (W / 4)) * 4;
         if (r0 + kk < t.col_limit) x[i] = *reinterpret_cast<const float4*>(t.u + (r0 + kk) * t.ld + f);
       }
     }
+    if (tid < TR) w = t.bmask[(int64_t)b * TR + tid];
   };
-  auto store_tile = [&](int buf) {
+  auto store = [&](const float4 (&x)[PER], uint32_t w, int buf) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int v = tid + i * 256;
+      const int v = tid + i * NT;
       if (v < NV) {
         const int kk = v / (W / 4), f = (v % (W / 4)) * 4;
         uint32_t h[4], m[4], l[4];
@@ -122,6 +125,7 @@ __global__ __launch_bounds__(256, TILES_MIN_WAVES) void cheb_tiles_kernel(TileAr
         *reinterpret_cast<uint2*>(&img[buf][2][kk][f]) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
       }
     }
+    if (tid < TR) msk[buf][tid] = w;
   };
 
   double acc[NFB][4];
@@ -136,17 +140,8 @@ __global__ __launch_bounds__(256, TILES_MIN_WAVES) void cheb_tiles_kernel(TileAr
   const int tcolo = 4 * (lane & 3);
   const int mrow = 16 * wave + (lane & 15);  // this lane's A row (of the block)
   const int mshift = 8 * (lane >> 4);        // its byte of the 32-bit row mask
-
-  if (it.y < it.z) {
-    load_tile(it.y);
-    store_tile(0);
-  }
-  for (int32_t b = it.y; b < it.z; ++b) {
-    const int buf = (b - it.y) & 1;
-    __syncthreads();  // tile b staged; buffer buf ^ 1 no longer read
-    if (b + 1 < it.z) load_tile(b + 1);
-    const uint32_t m = t.bmask[(int64_t)b * kTR + mrow];
-    const uint4 av = lut[(m >> mshift) & 0xFFu];
+  auto compute = [&](int buf) {
+    const uint4 av = lut[(msk[buf][mrow] >> mshift) & 0xFFu];
     const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
     for (int fb = 0; fb < NFB; ++fb) {
@@ -163,15 +158,30 @@ __global__ __launch_bounds__(256, TILES_MIN_WAVES) void cheb_tiles_kernel(TileAr
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[fb][i] += (double)c[i];
     }
-    if (b + 1 < it.z) store_tile(buf ^ 1);
+  };
+
+  const int32_t b0 = it.y, n = it.z - it.y;
+  if (n > 0) load(x0, w0, b0);
+  if (n > 1) load(x1, w1, b0 + 1);
+  if (n > 0) store(x0, w0, 0);
+  for (int32_t i = 0; i < n; i += 2) {
+    __syncthreads();  // tile i in buffer 0; buffer 1 no longer read
+    if (i + 2 < n) load(x0, w0, b0 + i + 2);
+    compute(0);
+    if (i + 1 >= n) break;
+    store(x1, w1, 1);
+    __syncthreads();  // tile i + 1 in buffer 1; buffer 0 no longer read
+    if (i + 3 < n) load(x1, w1, b0 + i + 3);
+    compute(1);
+    if (i + 2 < n) store(x0, w0, 0);
   }
   // D layout of 16x16x32: column = lane & 15, row = 4 (lane >> 4) + i
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int rl = 16 * wave + 4 * (lane >> 4) + i;
-    const int64_t row = rb * kTR + rl;
+    const int64_t row = rb * TR + rl;
     if (it.w < 0 && row >= t.n_plan) continue;
-    double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * kTR + rl) * W;
+    double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * TR + rl) * W;
 #pragma unroll
     for (int fb = 0; fb < NFB; ++fb) dst[16 * fb + (lane & 15)] = acc[fb][i];
   }
@@ -182,15 +192,15 @@ __global__ __launch_bounds__(256, TILES_MIN_WAVES) void cheb_tiles_kernel(TileAr
 // are independent, four in flight per thread)
 template <int W>
 __global__ __launch_bounds__(256) void tiles_combine_kernel(const int4* __restrict__ multi, const double* __restrict__ slots,
-                                                            double* __restrict__ part, int64_t ld, int64_t n_plan) {
+                                                            double* __restrict__ part, int64_t ld, int64_t n_plan, int TR) {
   const int4 mt = multi[blockIdx.y];
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= kTR * W) return;
+  if (e >= TR * W) return;
   const int rl = e / W, f = e - rl * W;
-  const int64_t row = (int64_t)mt.x * kTR + rl;
+  const int64_t row = (int64_t)mt.x * TR + rl;
   if (row >= n_plan) return;
-  const double* p = slots + ((int64_t)mt.y * kTR + rl) * W + f;
-  constexpr int64_t step = (int64_t)kTR * W;
+  const double* p = slots + ((int64_t)mt.y * TR + rl) * W + f;
+  const int64_t step = (int64_t)TR * W;
   double s = 0.0;
   int q = 0;
   for (; q + 4 <= mt.z; q += 4) {
@@ -225,6 +235,8 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   const int64_t col_limit = active_only ? L->n_active : L->n_cols;  // closed-form rows are never gathered
   const int th = std::max(1, L->tune.tile_th);
   const int tmax = std::max(1, L->tune.tile_max);
+  const int kTR = L->tune.tile_rows == 128 ? 128 : 64;
+  p->rows = kTR;
   std::vector<int32_t> rp(n + 1), col(nnz);
   WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
   WG_HIP_TRY(hipMemcpy(col.data(), L->col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
@@ -305,8 +317,8 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   if (!rc) rc = upload(&p->tsplit, tsplit);
   if (rc) return rc;
   char buf[256];
-  snprintf(buf, sizeof(buf), "tiles: %d dense blocks (64x32, >= %d entries) hold %lld of %lld entries (%.1f %%); %d items, %d split row blocks\n",
-           p->n_blocks, th, (long long)dense, (long long)nnz, nnz ? 100.0 * dense / nnz : 0.0, p->n_items, p->n_multi);
+  snprintf(buf, sizeof(buf), "tiles: %d dense blocks (%dx32, >= %d entries) hold %lld of %lld entries (%.1f %%); %d items, %d split row blocks\n",
+           p->n_blocks, kTR, th, (long long)dense, (long long)nnz, nnz ? 100.0 * dense / nnz : 0.0, p->n_items, p->n_multi);
   p->text = buf;
   return WG_OK;
 }
@@ -401,7 +413,7 @@ int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out
     p->width = 0;
     int rc = dmalloc(&p->part, (size_t)std::max<int64_t>(1, L->n_rows) * F);
     if (!rc) rc = dmalloc(&p->part2, (size_t)std::max<int64_t>(1, L->n_rows) * F);
-    if (!rc) rc = dmalloc(&p->slots, (size_t)std::max(1, p->n_slots) * kTR * F);
+    if (!rc) rc = dmalloc(&p->slots, (size_t)std::max(1, p->n_slots) * p->rows * F);
     if (rc) return rc;
     p->width = (int32_t)F;
   }
@@ -424,22 +436,27 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
   t.part = p->part;
   t.slots = p->slots;
   if (p->n_items > 0) {
-    const dim3 grid(p->n_items), block(256);
+    const dim3 grid(p->n_items), block(4 * p->rows);
+#define WG_TILES(NFB)                                                                                  \
+  if (p->rows == 128) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 8>), grid, block, 0, stream, t);    \
+  else hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4>), grid, block, 0, stream, t);
     switch (F / 16) {
-      case 1: hipLaunchKernelGGL(cheb_tiles_kernel<1>, grid, block, 0, stream, t); break;
-      case 2: hipLaunchKernelGGL(cheb_tiles_kernel<2>, grid, block, 0, stream, t); break;
-      case 3: hipLaunchKernelGGL(cheb_tiles_kernel<3>, grid, block, 0, stream, t); break;
-      default: hipLaunchKernelGGL(cheb_tiles_kernel<4>, grid, block, 0, stream, t); break;
+      case 1: WG_TILES(1) break;
+      case 2: WG_TILES(2) break;
+      case 3: WG_TILES(3) break;
+      default: WG_TILES(4) break;
     }
+#undef WG_TILES
     WG_LAUNCH_CHECK();
   }
   if (p->n_multi > 0) {
-    const dim3 grid((unsigned)ceil_div(kTR * F, 256), p->n_multi), block(256);
+    const dim3 grid((unsigned)ceil_div(p->rows * F, 256), p->n_multi), block(256);
+    const int TR = p->rows;
     switch (F / 16) {
-      case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
-      case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
-      case 3: hipLaunchKernelGGL(tiles_combine_kernel<48>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
-      default: hipLaunchKernelGGL(tiles_combine_kernel<64>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan); break;
+      case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+      case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+      case 3: hipLaunchKernelGGL(tiles_combine_kernel<48>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+      default: hipLaunchKernelGGL(tiles_combine_kernel<64>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
     }
     WG_LAUNCH_CHECK();
   }
