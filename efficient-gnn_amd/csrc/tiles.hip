@@ -141,7 +141,9 @@ __global__ __launch_bounds__(64 * NWV) void cheb_tiles_kernel(TileArgs t) {
   const int mrow = 16 * wave + (lane & 15);  // this lane's A row (of the block)
   const int mshift = 8 * (lane >> 4);        // its byte of the 32-bit row mask
   auto compute = [&](int buf) {
-    const uint4 av = lut[(msk[buf][mrow] >> mshift) & 0xFFu];
+    const uint32_t mw = msk[buf][mrow];
+    if (!__any(mw != 0u)) return;  // none of the wave's 16 rows has an entry in this tile (wave-uniform)
+    const uint4 av = lut[(mw >> mshift) & 0xFFu];
     const bf16x8 a = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
     for (int fb = 0; fb < NFB; ++fb) {
