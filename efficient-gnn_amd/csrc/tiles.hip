@@ -33,6 +33,7 @@
 // ds_read_b64_tr_b16 (two per fragment), three MFMAs (lo, mid, hi) per 16 columns.
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include "internal.h"
 
@@ -71,7 +72,7 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 }
 
 template <int NFB, int NWV>
-__global__ __launch_bounds__(64 * NWV) void cheb_tiles_kernel(TileArgs t) {
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(TileArgs t) {
   constexpr int TR = 16 * NWV;         // rows per row block (16 per wave)
   constexpr int NT = 64 * NWV;         // threads
   constexpr int W = 16 * NFB;          // signal width
@@ -92,10 +93,10 @@ __global__ __launch_bounds__(64 * NWV) void cheb_tiles_kernel(TileArgs t) {
   const int64_t rb = it.x;
   const int lane = tid & 63, wave = tid >> 6;
 
-  // a tile's staged data: PER float4 of u and (tid < TR) one row mask, in a 2-deep register
-  // ring so each tile's loads have two tiles' compute to arrive
-  float4 x0[PER], x1[PER];
-  uint32_t w0 = 0, w1 = 0;
+  // a tile's staged data: PER float4 of u and (tid < TR) one row mask, in a 3-deep register
+  // ring (set = tile % 3): a tile's loads are issued three tiles before it is multiplied
+  float4 xs[3][PER];
+  uint32_t ws[3] = {0u, 0u, 0u};
   auto load = [&](float4 (&x)[PER], uint32_t& w, int32_t b) {
     const int64_t r0 = (int64_t)t.bct[b] * kTC;
 #pragma unroll
@@ -163,19 +164,31 @@ __global__ __launch_bounds__(64 * NWV) void cheb_tiles_kernel(TileArgs t) {
   };
 
   const int32_t b0 = it.y, n = it.z - it.y;
-  if (n > 0) load(x0, w0, b0);
-  if (n > 1) load(x1, w1, b0 + 1);
-  if (n > 0) store(x0, w0, 0);
-  for (int32_t i = 0; i < n; i += 2) {
-    __syncthreads();  // tile i in buffer 0; buffer 1 no longer read
-    if (i + 2 < n) load(x0, w0, b0 + i + 2);
-    compute(0);
-    if (i + 1 >= n) break;
-    store(x1, w1, 1);
-    __syncthreads();  // tile i + 1 in buffer 1; buffer 0 no longer read
-    if (i + 3 < n) load(x1, w1, b0 + i + 3);
-    compute(1);
-    if (i + 2 < n) store(x0, w0, 0);
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (q < n) load(xs[q], ws[q], b0 + q);
+  if (n > 0) store(xs[0], ws[0], 0);
+  // tile j (j % 6 == I): multiplied from LDS buffer I % 2; its register set I % 3 is refilled
+  // with tile j + 3 first; tile j + 1 is split into the other buffer after
+  auto tile = [&](auto I, int32_t j) {
+    constexpr int i = decltype(I)::value;
+    __syncthreads();  // tile j staged; the other buffer no longer read
+    if (j + 3 < n) load(xs[i % 3], ws[i % 3], b0 + j + 3);
+    compute(i % 2);
+    if (j + 1 < n) store(xs[(i + 1) % 3], ws[(i + 1) % 3], (i + 1) % 2);
+  };
+  for (int32_t j = 0; j < n; j += 6) {
+    tile(std::integral_constant<int, 0>{}, j);
+    if (j + 1 >= n) break;
+    tile(std::integral_constant<int, 1>{}, j + 1);
+    if (j + 2 >= n) break;
+    tile(std::integral_constant<int, 2>{}, j + 2);
+    if (j + 3 >= n) break;
+    tile(std::integral_constant<int, 3>{}, j + 3);
+    if (j + 4 >= n) break;
+    tile(std::integral_constant<int, 4>{}, j + 4);
+    if (j + 5 >= n) break;
+    tile(std::integral_constant<int, 5>{}, j + 5);
   }
   // D layout of 16x16x32: column = lane & 15, row = 4 (lane >> 4) + i
 #pragma unroll
