@@ -71,9 +71,9 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
   l = __float_as_uint(r2) >> 16;
 }
 
-template <int NFB, int NWV>
+template <int NFB, int NWV, int RG>
 __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(TileArgs t) {
-  constexpr int TR = 16 * NWV;         // rows per row block (16 per wave)
+  constexpr int TR = 16 * NWV * RG;    // rows per row block (RG groups of 16 per wave)
   constexpr int NT = 64 * NWV;         // threads
   constexpr int W = 16 * NFB;          // signal width
   constexpr int NV = kTC * W / 4;      // float4 per tile
@@ -129,37 +129,52 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(
     if (tid < TR) msk[buf][tid] = w;
   };
 
-  double acc[NFB][4];
+  double acc[RG][NFB][4];
 #pragma unroll
-  for (int fb = 0; fb < NFB; ++fb)
+  for (int g = 0; g < RG; ++g)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[fb][i] = 0.0;
+    for (int fb = 0; fb < NFB; ++fb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[g][fb][i] = 0.0;
 
-  // transposed-read address of this lane: group g = lane >> 4 reads rows 8g + q (+4), q = (lane & 15) >> 2,
+  // transposed-read address of this lane: group q4 = lane >> 4 reads rows 8 q4 + q (+4), q = (lane & 15) >> 2,
   // columns 4 (lane & 3) .. +3 of each 16-column block
   const int trow = 8 * (lane >> 4) + ((lane & 15) >> 2);
   const int tcolo = 4 * (lane & 3);
-  const int mrow = 16 * wave + (lane & 15);  // this lane's A row (of the block)
-  const int mshift = 8 * (lane >> 4);        // its byte of the 32-bit row mask
+  const int mrow = 16 * RG * wave + (lane & 15);  // this lane's A row of row group 0 (of the block)
+  const int mshift = 8 * (lane >> 4);              // its byte of the 32-bit row mask
   auto compute = [&](int buf) {
-    const uint32_t mw = msk[buf][mrow];
-    if (!__any(mw != 0u)) return;  // none of the wave's 16 rows has an entry in this tile (wave-uniform)
-    const uint4 av = lut[(mw >> mshift) & 0xFFu];
-    const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+    uint32_t mw[RG];
+    bool any = false;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      mw[g] = msk[buf][mrow + 16 * g];
+      any = any || mw[g] != 0u;
+    }
+    if (!__any(any)) return;  // none of the wave's rows has an entry in this tile (wave-uniform)
+    bf16x8 a[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) a[g] = __builtin_bit_cast(bf16x8, lut[(mw[g] >> mshift) & 0xFFu]);
 #pragma unroll
     for (int fb = 0; fb < NFB; ++fb) {
-      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+      f32x4 c[RG];
 #pragma unroll
-      for (int p = 2; p >= 0; --p) {  // lo, mid, hi
+      for (int g = 0; g < RG; ++g) c[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 2; p >= 0; --p) {  // lo, mid, hi: one B fragment read, RG row groups
         const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (lds_s16x4*)(&img[buf][p][trow][16 * fb + tcolo]));
         const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (lds_s16x4*)(&img[buf][p][trow + 4][16 * fb + tcolo]));
         const s16x8 bv = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bv), c, 0, 0, 0);
+        const bf16x8 b = __builtin_bit_cast(bf16x8, bv);
+#pragma unroll
+        for (int g = 0; g < RG; ++g) c[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[g], b, c[g], 0, 0, 0);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[fb][i] += (double)c[i];
+      for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[g][fb][i] += (double)c[g][i];
     }
   };
 
@@ -192,14 +207,16 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(
   }
   // D layout of 16x16x32: column = lane & 15, row = 4 (lane >> 4) + i
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rl = 16 * wave + 4 * (lane >> 4) + i;
-    const int64_t row = rb * TR + rl;
-    if (it.w < 0 && row >= t.n_plan) continue;
-    double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * TR + rl) * W;
+  for (int g = 0; g < RG; ++g)
 #pragma unroll
-    for (int fb = 0; fb < NFB; ++fb) dst[16 * fb + (lane & 15)] = acc[fb][i];
-  }
+    for (int i = 0; i < 4; ++i) {
+      const int rl = 16 * (RG * wave + g) + 4 * (lane >> 4) + i;
+      const int64_t row = rb * TR + rl;
+      if (it.w < 0 && row >= t.n_plan) continue;
+      double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * TR + rl) * W;
+#pragma unroll
+      for (int fb = 0; fb < NFB; ++fb) dst[16 * fb + (lane & 15)] = acc[g][fb][i];
+    }
 }
 
 // row blocks split over several workgroups: part = their slots summed in slot order
@@ -451,10 +468,14 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
   t.part = p->part;
   t.slots = p->slots;
   if (p->n_items > 0) {
-    const dim3 grid(p->n_items), block(4 * p->rows);
+    // 128-row blocks: 8 waves of 16 rows, or (tile_rg = 2) 4 waves of two 16-row groups sharing
+    // each B fragment (half the LDS reads)
+    const int rg = (p->rows == 128 && L->tune.tile_rg == 2) ? 2 : 1;
+    const dim3 grid(p->n_items), block(4 * p->rows / rg);
 #define WG_TILES(NFB)                                                                                  \
-  if (p->rows == 128) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 8>), grid, block, 0, stream, t);    \
-  else hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4>), grid, block, 0, stream, t);
+  if (p->rows == 64) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 1>), grid, block, 0, stream, t);   \
+  else if (rg == 2) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 2>), grid, block, 0, stream, t);   \
+  else hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 8, 1>), grid, block, 0, stream, t);
     switch (F / 16) {
       case 1: WG_TILES(1) break;
       case 2: WG_TILES(2) break;
