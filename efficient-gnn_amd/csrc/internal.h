@@ -131,9 +131,9 @@ struct Lds1Plan {
 };
 
 // Hybrid step (tiles.hip) for wide signals on large unweighted graphs: internal rows in
-// blocks of 64, columns in tiles of 32; each (row block, column tile) pair holding at
-// least tile_th entries is a dense block, summed on the matrix cores from its 64 row
-// masks of 32 bits; the rest of each row (its "tail") comes first in the row's range of
+// blocks of 64 or 128, columns in tiles of 32; each (row block, column tile) pair holding at
+// least tile_th entries is a dense block, summed on the matrix cores from its row masks of
+// 32 bits; the rest of each row (its "tail") comes first in the row's range of
 // tcol and is gathered by the step kernel (phases 4, or 1 + 6), which adds the blocks' sums.
 struct TilePlan {
   int64_t n_plan = 0;          // rows planned: [0, n_plan)
@@ -200,8 +200,8 @@ struct Tuning {
   int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple
   int32_t tiles = -1;        // hybrid step (tiles.hip): -1 = auto (unweighted, width % 16 == 0, >= 8 M nonzeros,
                              // >= 30 % of the entries in dense blocks), 0 = off, 1 = whenever it applies
-  int32_t tile_th = 64;      // entries that make a 64 x 32 (row block, column tile) pair a dense block
-  int32_t tile_max = 128;    // dense blocks per workgroup (longer row blocks split over slots)
+  int32_t tile_th = 128;     // entries that make a (row block, 32-column tile) pair a dense block
+  int32_t tile_max = 64;     // dense blocks per workgroup (longer row blocks split over slots)
   int32_t tiles_overlap = 0; // hybrid step: the tail gathers on a side stream beside the dense blocks
                              // (Reddit-size F=41: 1176 vs 1136 us per step sequential, r02_tiles: off)
   int32_t tile_rows = 128;   // hybrid step: rows per row block (64 or 128)
