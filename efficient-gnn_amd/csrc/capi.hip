@@ -253,6 +253,20 @@ int wg_cheb_step(wg_laplacian_t L, int32_t k, int64_t F, const float* t_km1, con
   return launch_step(L, k, F, t_km1, t_km2, t_k, S, H, alpha0, alpha_k, as_stream(stream_));
 }
 
+int wg_clenshaw_step(wg_laplacian_t L, int64_t F, const float* b1, const float* b2, const float* x0, float* out,
+                     double ck, double cacc, int32_t flags, void* stream_) {
+  if (!L || F < 1 || (L->n_rows && (!b1 || !x0 || !out)) || (flags & ~31) ||
+      ((flags & WG_CLEN_FINAL) && (flags & WG_CLEN_UOUT)) || ((flags & (WG_CLEN_UIN | WG_CLEN_UPREV)) && !L->unit))
+    return fail(WG_ERR_INVALID, "wg_clenshaw_step: bad arguments (F=%lld flags=%d)", (long long)F, flags);
+  const bool fin = (flags & WG_CLEN_FINAL) != 0;
+  ClenArgs cl{x0, ck, cacc, fin ? 1 : 0};
+  cl.uin = (flags & WG_CLEN_UIN) ? 1 : 0;
+  cl.uprev = (flags & WG_CLEN_UPREV) ? 1 : 0;
+  cl.uout = (flags & WG_CLEN_UOUT) ? 1 : 0;
+  return launch_step(L, 2, F, b1, b2, fin ? nullptr : out, fin ? out : nullptr, nullptr, 1.0, 0.0, as_stream(stream_),
+                     (flags & WG_CLEN_ACTIVE) != 0, nullptr, &cl);
+}
+
 int wg_cheb_u_len(wg_laplacian_t L, int64_t* len) {
   if (!L || !len) return fail(WG_ERR_INVALID, "wg_cheb_u_len: NULL argument");
   *len = 0;

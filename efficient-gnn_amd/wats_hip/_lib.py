@@ -72,6 +72,7 @@ SIGNATURES = {
     "wg_scale_dinv": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
     "wg_lds_plan_info": (ctypes.c_int, [c_vp, c_i32, ctypes.POINTER(c_i64)]),
     "wg_cheb_step_u": (ctypes.c_int, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_vp]),
+    "wg_clenshaw_step": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_i32, c_vp]),
     "wg_rownorm_create": (ctypes.c_int, [c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_vp, ctypes.POINTER(c_vp)]),
     "wg_spmm": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "wg_wats_head_forward": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32] + [c_vp] * 8 + [c_vp]),

@@ -182,6 +182,25 @@ int wg_cheb_step_u(wg_laplacian_t L, int32_t k, const float* u_km1, const float*
                    const float* t_km2, float* t_k, float* u_k, float* S, double alpha0,
                    double alpha_k, void* stream);
 
+/* One step of the heat sum by Clenshaw's recurrence (WATS.py:32-36 with the
+ * sum of :65-68), the step wg_wavelet_features (F > 1) and the row-sharded
+ * chain run, on internal rows:
+ *   out = ck * x0 + cacc * (L_hat b1) - b2        (b2 NULL = 0)
+ * flags: WG_CLEN_UIN  b1 holds u = b * dinv (unweighted handles: the gathers
+ *                     read no values; own + halo rows, like t_km1 of wg_cheb_step)
+ *        WG_CLEN_UPREV b2 holds u;  WG_CLEN_UOUT out receives u (not with FINAL)
+ *        WG_CLEN_FINAL out is the finished sum S
+ *        WG_CLEN_ACTIVE only the rows that enter wg_wavelet_features' chain.
+ * With WG_CLEN_UIN on a large unweighted graph and F a multiple of 16 (<= 64)
+ * this is the hybrid step (dense blocks on the matrix cores). */
+#define WG_CLEN_UIN 1
+#define WG_CLEN_UPREV 2
+#define WG_CLEN_UOUT 4
+#define WG_CLEN_FINAL 8
+#define WG_CLEN_ACTIVE 16
+int wg_clenshaw_step(wg_laplacian_t L, int64_t F, const float* b1, const float* b2, const float* x0,
+                     float* out, double ck, double cacc, int32_t flags, void* stream);
+
 /* Row permutation between the caller's order and the internal order:
  * direction 0: dst[i_internal] = src[perm[i]]  (caller -> internal)
  * direction 1: dst[perm[i]] = src[i_internal]  (internal -> caller). */

@@ -58,6 +58,13 @@ for part in $PARTS; do
         --connected-companion 0 > "$OUT/prof.log" 2>&1
       fatal benchprof $?
       ;;
+    tracetiles)
+      # the hybrid step (tiles.hip) on Reddit-size F=41 with its defaults: tile kernel + tail step kernel
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/trace_tiles -o run -- \
+        python3 tools/tiles_probe.py --config reddit-f41 --sets "tiles=-1" --reps 5 > "$OUT/trace_tiles.log" 2>&1
+      fatal trace_tiles $?
+      cp /tmp/trace_tiles/run_kernel_stats.csv "$OUT/trace_tiles_kernel_stats.csv"
+      ;;
     rehearse2)
       WATS_BENCH_PG=gloo WATS_BENCH_DEVICE=0 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
         --nproc-per-node=2 --master-addr=127.0.0.1 --master-port=29611 bench.py --gpus 2 --exchange ipc \

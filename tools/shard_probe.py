@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--F", type=int, default=1, help="signal width (F > 1: the gather kernel at this width)")
     ap.add_argument("--groups", type=int, default=1, help="hand the degree-ordered halo groups to the handle "
                                                           "(the F = 1 hub kernel applies to the shard)")
+    ap.add_argument("--clen", type=int, default=1, help="F > 1: the value-free Clenshaw step of the sharded chain "
+                                                       "(wg_clenshaw_step; the hybrid step where it applies); 0 = wg_cheb_step")
     ap.add_argument("--grid", default="", help="';'-separated knob sets to time, e.g. 'lds_wg=64;lds_wg=128,lds_k=2'")
     a = ap.parse_args()
     n, nnz_t, K, _ = NAMED_CONFIGS[a.config]
@@ -82,8 +84,15 @@ def probe(L, lib, n_own, n_cols, K, a, dev, kv):
         F = a.F
         X = [torch.rand(n_cols, F, device=dev), torch.rand(n_own, F, device=dev), torch.rand(n_own, F, device=dev)]
         SF = torch.zeros(n_own, F, device=dev)
-        run = lambda k: L.step(k, X[0], X[1], X[2], S=SF, alpha0=1.0, alpha_k=math.exp(-0.8 * k))
-        info = f"gather kernel F={F}"
+        if a.clen:
+            flags = 1 | 2 | 4   # WG_CLEN_UIN | UPREV | UOUT: b1 (own + halo rows of u), b2 = u, out = u over b2
+            run = lambda k: check(lib.wg_clenshaw_step(L.handle, F, ptr(X[0]), ptr(X[1]), ptr(X[2]), ptr(X[1]), 0.3,
+                                                       2.0, flags, st), "clenshaw_step")
+            info = f"value-free Clenshaw step F={F}; " + "; ".join(ln for ln in L.describe(F).splitlines()
+                                                                      if ln.startswith("tiles:"))
+        else:
+            run = lambda k: L.step(k, X[0], X[1], X[2], S=SF, alpha0=1.0, alpha_k=math.exp(-0.8 * k))
+            info = f"gather kernel F={F}"
     elif ulen.value:
         U = [torch.rand(ulen.value, device=dev) for _ in range(2)]
         run = lambda k: check(lib.wg_cheb_step_u(L.handle, k, ptr(U[0]), ptr(T[0]), ptr(T[1]), ptr(T[2]), ptr(U[1]),
@@ -96,6 +105,9 @@ def probe(L, lib, n_own, n_cols, K, a, dev, kv):
     for k in range(2, 6):
         run(k)
     torch.cuda.synchronize()
+    if a.F > 1 and a.clen:   # the plan text once the first step has built it
+        info = f"value-free Clenshaw step F={a.F}; " + "; ".join(ln for ln in L.describe(a.F).splitlines()
+                                                                  if ln.startswith("tiles:"))
     L.profile_enable(True)
     for _ in range(a.reps):
         for k in range(2, K + 1):
