@@ -197,7 +197,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.tile_rg = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_max")) {
-    if (value < 1 || value > 1 << 20) return fail(WG_ERR_INVALID, "tile_max must be in [1, 2^20]");
+    if (value < 0 || value > 1 << 20) return fail(WG_ERR_INVALID, "tile_max must be in [0 (auto), 2^20]");
     L->tune.tile_max = (int32_t)value;
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;

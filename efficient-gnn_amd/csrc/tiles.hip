@@ -266,7 +266,7 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   const int64_t n_plan = active_only ? L->n_active : n;
   const int64_t col_limit = active_only ? L->n_active : L->n_cols;  // closed-form rows are never gathered
   const int th = std::max(1, L->tune.tile_th);
-  const int tmax = std::max(1, L->tune.tile_max);
+  int tmax = L->tune.tile_max;  // <= 0: auto (below)
   const int kTR = L->tune.tile_rows == 128 ? 128 : 64;
   p->rows = kTR;
   std::vector<int32_t> rp(n + 1), col(nnz);
@@ -277,6 +277,7 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   std::vector<int32_t> bct, tcol(col), tsplit(n);
   std::vector<uint32_t> bmask;
   std::vector<int4> items, multi;
+  std::vector<int2> rbs;  // row blocks with dense blocks: {row block, first block}
   int32_t n_slots = 0;
   int64_t dense = 0;
   for (int64_t r = n_plan; r < n; ++r) tsplit[r] = rp[r + 1];  // unplanned rows: all tail
@@ -322,15 +323,24 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
       sel[ct] = -1;
     }
     const int32_t nb = (int32_t)bct.size() - first;
-    if (nb == 0) continue;  // every entry is tail: no part is added to these rows
+    if (nb > 0) rbs.push_back(make_int2((int)rb, first));  // nb == 0: every entry is tail, no part added
+  }
+  // work items: a row block's dense blocks, split over several workgroups (slots) past tmax;
+  // auto tmax: about 3072 items for the chip's 256 CUs x 3 resident workgroups x 4, within [8, 64]
+  // (the 8-way Reddit-size shard: 22 k blocks -> 8 per item; the whole graph: 187 k -> 61)
+  const int64_t nblk = (int64_t)bct.size();
+  if (tmax <= 0) tmax = (int)std::max<int64_t>(8, std::min<int64_t>(64, ceil_div(nblk, 3072)));
+  for (size_t q0 = 0; q0 < rbs.size(); ++q0) {
+    const int rb = rbs[q0].x, first = rbs[q0].y;
+    const int32_t nb = (int32_t)((q0 + 1 < rbs.size() ? rbs[q0 + 1].y : nblk) - first);
     const int32_t k = (nb + tmax - 1) / tmax;
     if (k == 1) {
-      items.push_back(make_int4((int)rb, first, first + nb, -1));
+      items.push_back(make_int4(rb, first, first + nb, -1));
     } else {
       for (int32_t q = 0; q < k; ++q)
-        items.push_back(make_int4((int)rb, first + (int32_t)((int64_t)nb * q / k), first + (int32_t)((int64_t)nb * (q + 1) / k),
+        items.push_back(make_int4(rb, first + (int32_t)((int64_t)nb * q / k), first + (int32_t)((int64_t)nb * (q + 1) / k),
                                   n_slots + q));
-      multi.push_back(make_int4((int)rb, n_slots, k, 0));
+      multi.push_back(make_int4(rb, n_slots, k, 0));
       n_slots += k;
     }
   }
