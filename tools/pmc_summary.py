@@ -25,7 +25,7 @@ def main():
                     name = r.get("Kernel_Name", "")
                     if a.match and a.match not in name:
                         continue
-                    short = name.split("(")[0].replace("void ", "").replace("wg::(anonymous namespace)::", "")
+                    short = name.replace("void ", "").replace("wg::(anonymous namespace)::", "").split("(")[0]
                     acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for k, cs in acc.items():
