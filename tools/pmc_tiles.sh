@@ -16,7 +16,7 @@ for grp in "${PASSES[@]}"; do
   timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d /tmp/pmc_tiles_$i -o run -- \
       python3 tools/tiles_probe.py --config reddit-f41 --sets "${SETS:-tiles=-1}" --reps 1 > "$OUT/pass_$i.log" 2>&1
   rc=$?
-  cp /tmp/pmc_tiles_$i/run_counter_collection.csv "$OUT/pass_${i}_counters.csv" 2>/dev/null
+  grep -E "Counter_Name|cheb_|tiles_combine" /tmp/pmc_tiles_$i/run_counter_collection.csv > "$OUT/pass_${i}_counters.csv" || true
   echo "[pass $i: $grp] rc=$rc" | tee -a "$OUT/steps.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc $rc"; exit $rc; fi
 done
