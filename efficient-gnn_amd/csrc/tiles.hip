@@ -26,8 +26,9 @@
 // Workgroup = 4 waves = one row block (or a share of a long row block's dense
 // blocks: those write float64 slots that tiles_combine_kernel sums in order).
 // Per dense block: the 256 lanes load the 32 x W tile of u (float4, L2), split it
-// into the three bf16 pieces in an LDS image [piece][32 rows][W] (double-
-// buffered: the next tile's loads are in flight while this one is multiplied),
+// into the three bf16 pieces in an LDS image per piece (bank-conflict-free rows,
+// img_row; double-buffered, and a 3-deep register ring keeps three tiles' loads
+// in flight),
 // and each wave multiplies its 16 rows: A fragments from a byte -> 8 x bf16
 // lookup table indexed by the row mask, B fragments by the transposed LDS read
 // ds_read_b64_tr_b16 (two per fragment), three MFMAs (lo, mid, hi) per 16 columns.
@@ -47,6 +48,19 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// LDS image of one bf16 piece of a 32-row tile: row r at dword r*S + X*bit3(r) + Y*bit4(r), so the
+// transposed reads (two 16-lane groups of a 32-lane half read rows 8 apart) hit 64 distinct banks
+// (searched exhaustively for each width; a plain [32][W] image is 2-way conflicted: 66 M
+// SQ_LDS_BANK_CONFLICT cycles per launch, a third of the kernel, r02 pmc_tiles)
+__host__ __device__ constexpr int img_s(int nfb) { return nfb == 1 ? 8 : nfb == 2 ? 16 : nfb == 3 ? 24 : 40; }
+__host__ __device__ constexpr int img_x(int nfb) { return nfb == 2 ? 8 : 32; }
+__host__ __device__ constexpr int img_y(int nfb) { return nfb == 2 ? 8 : nfb == 4 ? 24 : 32; }
+__host__ __device__ constexpr int img_dwords(int nfb) { return 31 * img_s(nfb) + img_x(nfb) + img_y(nfb) + 8 * nfb; }
+template <int NFB>
+__device__ __forceinline__ int img_row(int r) {  // bf16 offset of row r
+  return 2 * (r * img_s(NFB) + img_x(NFB) * ((r >> 3) & 1) + img_y(NFB) * ((r >> 4) & 1));
+}
 
 struct TileArgs {
   const float* u;        // gathered vector (rows = columns of L_hat), row stride ld
@@ -79,7 +93,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(
   constexpr int NV = kTC * W / 4;      // float4 per tile
   constexpr int PER = (NV + NT - 1) / NT;
   __shared__ uint4 lut[256];                                          // byte -> 8 bf16 (bit j ? 1.0 : 0)
-  __shared__ __attribute__((aligned(16))) uint16_t img[2][3][kTC][W];  // [buffer][piece hi/mid/lo][k][f]
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][3][2 * img_dwords(NFB)];  // [buffer][piece hi/mid/lo][k, f]
   __shared__ uint32_t msk[2][TR];                                     // [buffer][row] the block's row masks
   const int tid = threadIdx.x;
   if (tid < 256) {
@@ -121,9 +135,10 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(
         split3(x[i].y, h[1], m[1], l[1]);
         split3(x[i].z, h[2], m[2], l[2]);
         split3(x[i].w, h[3], m[3], l[3]);
-        *reinterpret_cast<uint2*>(&img[buf][0][kk][f]) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-        *reinterpret_cast<uint2*>(&img[buf][1][kk][f]) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
-        *reinterpret_cast<uint2*>(&img[buf][2][kk][f]) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+        const int o = img_row<NFB>(kk) + f;
+        *reinterpret_cast<uint2*>(&img[buf][0][o]) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        *reinterpret_cast<uint2*>(&img[buf][1][o]) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+        *reinterpret_cast<uint2*>(&img[buf][2][o]) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
       }
     }
     if (tid < TR) msk[buf][tid] = w;
@@ -141,6 +156,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(
   // columns 4 (lane & 3) .. +3 of each 16-column block
   const int trow = 8 * (lane >> 4) + ((lane & 15) >> 2);
   const int tcolo = 4 * (lane & 3);
+  const int tr_lo = img_row<NFB>(trow) + tcolo, tr_hi = img_row<NFB>(trow + 4) + tcolo;
   const int mrow = 16 * RG * wave + (lane & 15);  // this lane's A row of row group 0 (of the block)
   const int mshift = 8 * (lane >> 4);              // its byte of the 32-bit row mask
   auto compute = [&](int buf) {
@@ -162,10 +178,8 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(
       for (int g = 0; g < RG; ++g) c[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int p = 2; p >= 0; --p) {  // lo, mid, hi: one B fragment read, RG row groups
-        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)(&img[buf][p][trow][16 * fb + tcolo]));
-        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)(&img[buf][p][trow + 4][16 * fb + tcolo]));
+        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_lo + 16 * fb]));
+        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_hi + 16 * fb]));
         const s16x8 bv = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
         const bf16x8 b = __builtin_bit_cast(bf16x8, bv);
 #pragma unroll
