@@ -86,7 +86,10 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 }
 
 template <int NFB, int NWV, int RG>
-__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 6 : 4) void cheb_tiles_kernel(TileArgs t) {
+#ifndef WG_TILES_MINW
+#define WG_TILES_MINW 6
+#endif
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_tiles_kernel(TileArgs t) {
   constexpr int TR = 16 * NWV * RG;    // rows per row block (RG groups of 16 per wave)
   constexpr int NT = 64 * NWV;         // threads
   constexpr int W = 16 * NFB;          // signal width
