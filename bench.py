@@ -310,6 +310,9 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     lds_info = sw.L.lds_plan_info(active_only=False) if (F == 1 and sw.u_len() > 0) else None
     b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
     kernel = lds_kernel_name(lds_info) + " (rank 0 shard)"
+    tiles_plan = [ln for ln in sw.L.describe(F).splitlines() if ln.startswith("tiles:")]
+    if tiles_plan:   # the hybrid step: dense blocks on MFMA + the tail on the step kernel
+        kernel = "hybrid step: cheb_tiles_kernel + cheb_step_kernel over the tail (rank 0 shard)"
     avg_ms = prof["step_ms"]
     sw.close()
     del sw
@@ -350,6 +353,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                      "graph_replayed": bool(dinfo.get("captured")) if dinfo else None,
                      "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
+                     "tiles_plan": tiles_plan[0] if tiles_plan else None,
                      "nominal_8d_bytes": b_8d,
                      "nominal_8d_frac": (b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None},
         "check": chk,
