@@ -105,3 +105,41 @@ def test_tiles_not_taken_for_weighted_or_narrow():
     L = NormalizedLaplacian.from_graph(g)
     _run(L, X, 4, tiles=1)
     assert "tiles:" not in L.describe(8)
+
+
+@pytest.mark.parametrize("F,tiles", [(48, 0), (48, 1), (6, 0)])
+def test_clenshaw_step_abi(F, tiles):
+    """wg_clenshaw_step (one step of the chain through the C ABI) against the
+    per-step API: out = ck x0 + cacc (L_hat b1) - b2, valued (flags 0) on any
+    graph, and value-free on u = b dinv (UIN | UPREV | UOUT) on an unweighted one
+    -- the hybrid step when tiles = 1."""
+    from wats_hip import _lib
+    from wats_hip._lib import check, ptr
+    g = rmat_graph(4000, 120000, seed=11)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(tiles=tiles, tile_th=8)
+    dev = L.device
+    rng = np.random.default_rng(5)
+    b1, b2, x0 = (torch.from_numpy(rng.standard_normal((g.n, F)).astype(np.float32)).to(dev) for _ in range(3))
+    T1 = torch.empty_like(b1)
+    L.step(1, b1, None, T1)                      # T_1 = L_hat b1 (internal order, like every vector here)
+    ck, cacc = 0.3, 2.0
+    ref = (ck * x0.double() + cacc * T1.double() - b2.double())
+    lib = _lib.load()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    out = torch.empty_like(b1)
+    check(lib.wg_clenshaw_step(L.handle, F, ptr(b1), ptr(b2), ptr(x0), ptr(out), ck, cacc, 0, st), "clenshaw_step")
+    torch.cuda.synchronize()
+    _close(out, ref.float(), f"valued F={F}", tol=1e-6)
+    # value-free: b1, b2 given as u = b * dinv; out comes back as u
+    iperm_deg = torch.from_numpy(np.diff(g.indptr).astype(np.float64))   # column degrees: the graph is symmetric
+    deg_int = L.permute(iperm_deg.float().reshape(-1, 1).to(dev), to_internal=True).double()
+    dinv = torch.where(deg_int > 0, 1.0 / torch.sqrt(deg_int), torch.ones_like(deg_int))
+    u1, u2 = (b1.double() * dinv).float(), (b2.double() * dinv).float()
+    outu = torch.empty_like(b1)
+    check(lib.wg_clenshaw_step(L.handle, F, ptr(u1), ptr(u2), ptr(x0), ptr(outu), ck, cacc, 1 | 2 | 4, st),
+          "clenshaw_step u")
+    torch.cuda.synchronize()
+    _close((outu.double() / dinv).float(), ref.float(), f"value-free F={F} tiles={tiles}", tol=2e-6)
+    if tiles:
+        assert "tiles:" in L.describe(F)
