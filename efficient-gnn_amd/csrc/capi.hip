@@ -192,6 +192,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "tile_rows")) {
     if (value != 64 && value != 128) return fail(WG_ERR_INVALID, "tile_rows must be 64 or 128");
     L->tune.tile_rows = (int32_t)value;
+  } else if (!strcmp(key, "xcd")) {
+    L->tune.xcd = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_rg")) {
     if (value != 1 && value != 2) return fail(WG_ERR_INVALID, "tile_rg must be 1 or 2");
     L->tune.tile_rg = (int32_t)value;

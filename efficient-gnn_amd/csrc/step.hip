@@ -92,6 +92,7 @@ struct StepArgs {
   // tail into part on a side stream and phase 6 (no entries) adds part + part2 (the blocks'
   // sums, rows with dense entries) and runs the epilogue
   const double* part2;
+  int32_t xcd;  // knob xcd: XCD-contiguous unit order (cheb_step_kernel)
 };
 
 // the entry range of a row (or of a split-row chunk) this launch's phase covers
@@ -750,7 +751,14 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
 
 template <int VEC, bool BCAST, int NW>
 __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
-  unit_body<VEC, BCAST, NW, false>(a, segs, nseg, (int32_t)blockIdx.x, 0);
+  // knob xcd: workgroups are dealt to the 8 XCDs round-robin; remap so that XCD x runs the
+  // contiguous x-th eighth of the plan's units (rows of similar degree share an L2)
+  int32_t unit = (int32_t)blockIdx.x;
+  if (a.xcd) {
+    const int32_t n = (int32_t)gridDim.x, q = n >> 3, r = n & 7, x = unit & 7;
+    unit = x * q + min(x, r) + (unit >> 3);
+  }
+  unit_body<VEC, BCAST, NW, false>(a, segs, nseg, unit, 0);
 }
 
 // Persistent F == 1 variant: one workgroup per CU stages T_{k-1}[0, H) in LDS
@@ -1383,6 +1391,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         }
       }
       a.probe = L->tune.probe;
+      a.xcd = L->tune.xcd;
       if (a.probe && !a.xk) a.xk = S ? S + f0 : nullptr;  // the final step of a chain stores into S
       a.chunks = plan->chunks;
       a.partial = plan->partial;

@@ -287,7 +287,8 @@ def test_wats_dropin_on_gpu_matches_reference():
                                    dict(gbuf=1), dict(hubf=64), dict(hubf=700, waves=16, chunk_iter=2, block_iter=2),
                                    dict(hubf=5000, waves=8), dict(gbuf=1, iter=2, block_iter=1, chunk_iter=1),
                                    dict(inkernel_combine=1, iter=2, block_iter=1, chunk_iter=2, waves=8),
-                                   dict(fuse_finalize=0), dict(fuse_finalize=0, tile_f=8)])
+                                   dict(fuse_finalize=0), dict(fuse_finalize=0, tile_f=8), dict(xcd=1),
+                                   dict(xcd=1, iter=2, block_iter=1, chunk_iter=1)])
 def test_tuning_knobs_preserve_results(knobs):
     _check_knobs(knobs, F=12)
 
@@ -313,7 +314,7 @@ def _check_knobs(knobs, F):
     H1, S1 = wats_hip.graph_wavelet_features(L, k=8, X0=torch.from_numpy(X), return_S=True)
     assert_parity(_np(S1), ref["S"], what=f"{knobs} S")
     assert_parity(_np(H1), ref["H"], what=f"{knobs} H")
-    if set(knobs) <= {"bcast", "nt", "inkernel_combine"}:
+    if set(knobs) <= {"bcast", "nt", "inkernel_combine", "xcd"}:
         assert torch.equal(S0, S1), "same plan must give bitwise-identical results"
 
 
