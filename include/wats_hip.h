@@ -224,7 +224,9 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
  * shape), "chunk_iter" (chunk-mode nonzeros per sub-group),
  * "seg_mask" (bitmask of plan segments to launch -- timing attribution only;
  * results are wrong unless all bits are set), "clenshaw" (wavelet_features'
- * heat sum, default 1), and the kernel-variant keys listed in
+ * heat sum, default 1), "tiles" (the hybrid step, DESIGN.md 4.6: -1 auto,
+ * 0 off, 1 whenever it applies; with "tile_th", "tile_rows", "tile_max",
+ * "tile_rg", "tiles_overlap"), and the kernel-variant keys listed in
  * efficient-gnn_amd/csrc/internal.h (struct Tuning).  Plan-shaping keys are
  * synchronous (they drop cached plans); launch-time keys are not. */
 int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value);
