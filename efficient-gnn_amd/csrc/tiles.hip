@@ -128,6 +128,11 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
     if (tid < TR) w = t.bmask[(int64_t)b * TR + tid];
   };
   auto store = [&](const float4 (&x)[PER], uint32_t w, int buf) {
+#ifdef WG_TILES_PROBE_NO_STORE  // timing attribution only (results wrong): the tile is loaded, not staged
+    if (x[0].x == 12345.f) img[buf][0][tid] = 1;
+    if (tid < TR) msk[buf][tid] = w;
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int v = tid + i * NT;
@@ -181,12 +186,22 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
       for (int g = 0; g < RG; ++g) c[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int p = 2; p >= 0; --p) {  // lo, mid, hi: one B fragment read, RG row groups
+#ifdef WG_TILES_PROBE_NO_TR  // timing attribution only (results wrong): no B reads from LDS
+        const s16x4 lo4 = {(short)(p + fb), 0, 0, 0}, hi4 = {0, 0, 0, (short)lane};
+#else
         const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_lo + 16 * fb]));
         const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_hi + 16 * fb]));
+#endif
         const s16x8 bv = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
         const bf16x8 b = __builtin_bit_cast(bf16x8, bv);
 #pragma unroll
-        for (int g = 0; g < RG; ++g) c[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[g], b, c[g], 0, 0, 0);
+        for (int g = 0; g < RG; ++g) {
+#ifdef WG_TILES_PROBE_NO_MFMA  // timing attribution only (results wrong)
+          c[g][0] += (float)b[0] * (float)a[g][1];
+#else
+          c[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[g], b, c[g], 0, 0, 0);
+#endif
+        }
       }
 #pragma unroll
       for (int g = 0; g < RG; ++g)
