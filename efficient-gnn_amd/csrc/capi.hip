@@ -192,6 +192,8 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "tile_rows")) {
     if (value != 64 && value != 128) return fail(WG_ERR_INVALID, "tile_rows must be 64 or 128");
     L->tune.tile_rows = (int32_t)value;
+  } else if (!strcmp(key, "probe_tailwin")) {
+    L->tune.probe_tailwin = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 1024));  // plan-time, timing only
   } else if (!strcmp(key, "xcd")) {
     L->tune.xcd = value ? 1 : 0;
     return WG_OK;  // launch-time choice

@@ -206,6 +206,7 @@ struct Tuning {
   int32_t tiles_overlap = 0; // hybrid step: the tail gathers on a side stream beside the dense blocks
                              // (Reddit-size F=41: 1176 vs 1136 us per step sequential, r02_tiles: off)
   int32_t tile_rows = 128;   // hybrid step: rows per row block (64 or 128)
+  int32_t probe_tailwin = 0; // timing only (results wrong): the hybrid step's tail columns folded into 1/n of the columns
   int32_t xcd = 0;           // step kernel: XCD x runs the x-th contiguous eighth of the units
   int32_t tile_rg = 1;       // hybrid step, 128-row blocks: 16-row groups per wave (1: 8 waves, 2: 4 waves)
 };

@@ -347,6 +347,10 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
           tmp.push_back(c);
         }
       }
+      if (L->tune.probe_tailwin > 0) {  // timing probe only (results wrong): every tail column folded
+        const int64_t win = std::max<int64_t>(1, col_limit / L->tune.probe_tailwin);  // into one window
+        for (auto& c : tmp) c = (int32_t)(col_limit / 2 + c % win < col_limit ? col_limit / 2 + c % win : c % win);
+      }
       tsplit[r] = rp[r] + (int32_t)tmp.size();
       std::copy(tmp.begin(), tmp.end(), tcol.begin() + rp[r]);
     }
