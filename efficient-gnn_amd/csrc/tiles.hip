@@ -19,7 +19,7 @@
 // (truncations: hi = u with the low 16 bits cleared, mid likewise of u - hi, and
 // lo = u - hi - mid has at most 8 significant bits), so every product is exact
 // and each v_mfma_f32_16x16x32_bf16 adds 32 of them in float32; each block's
-// float32 sum (<= 96 exact terms) is added to a float64 accumulator.  Results
+// float32 sums (<= 4 blocks x 96 exact terms) are added to a float64 accumulator.  Results
 // differ from the all-float64 gather kernel only by that float32 rounding of
 // each block sum (tests/test_gpu_parity.py, test_tiles_*).
 //
@@ -86,6 +86,9 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 }
 
 template <int NFB, int NWV, int RG>
+#ifndef WG_TILES_FLUSH  // computed tiles per float32 -> float64 flush of the block sums
+#define WG_TILES_FLUSH 4  // 917 vs 928 us per step at 1 (Reddit-size F=41, r02_s70), same S to 1e-8
+#endif
 #ifndef WG_TILES_MINW
 #define WG_TILES_MINW 6
 #endif
@@ -167,6 +170,24 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
   const int tr_lo = img_row<NFB>(trow) + tcolo, tr_hi = img_row<NFB>(trow + 4) + tcolo;
   const int mrow = 16 * RG * wave + (lane & 15);  // this lane's A row of row group 0 (of the block)
   const int mshift = 8 * (lane >> 4);              // its byte of the 32-bit row mask
+  // float32 MFMA sums of the last <= WG_TILES_FLUSH computed tiles, added to the float64 acc
+  f32x4 cacc[NFB][RG];
+  int nacc = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int fb = 0; fb < NFB; ++fb)
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[g][fb][i] += (double)cacc[fb][g][i];
+        cacc[fb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    nacc = 0;
+  };
+#pragma unroll
+  for (int fb = 0; fb < NFB; ++fb)
+#pragma unroll
+    for (int g = 0; g < RG; ++g) cacc[fb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int buf) {
     uint32_t mw[RG];
     bool any = false;
@@ -181,9 +202,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
     for (int g = 0; g < RG; ++g) a[g] = __builtin_bit_cast(bf16x8, lut[(mw[g] >> mshift) & 0xFFu]);
 #pragma unroll
     for (int fb = 0; fb < NFB; ++fb) {
-      f32x4 c[RG];
-#pragma unroll
-      for (int g = 0; g < RG; ++g) c[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 (&c)[RG] = cacc[fb];
 #pragma unroll
       for (int p = 2; p >= 0; --p) {  // lo, mid, hi: one B fragment read, RG row groups
 #ifdef WG_TILES_PROBE_NO_TR  // timing attribution only (results wrong): no B reads from LDS
@@ -203,11 +222,8 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
 #endif
         }
       }
-#pragma unroll
-      for (int g = 0; g < RG; ++g)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[g][fb][i] += (double)c[g][i];
     }
+    if (++nacc == WG_TILES_FLUSH) flush();
   };
 
   const int32_t b0 = it.y, n = it.z - it.y;
@@ -237,6 +253,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
     if (j + 5 >= n) break;
     tile(std::integral_constant<int, 5>{}, j + 5);
   }
+  if (nacc > 0) flush();
   // D layout of 16x16x32: column = lane & 15, row = 4 (lane >> 4) + i
 #pragma unroll
   for (int g = 0; g < RG; ++g)
