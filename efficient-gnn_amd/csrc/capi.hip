@@ -198,7 +198,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.xcd = value ? 1 : 0;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_rg")) {
-    if (value != 1 && value != 2) return fail(WG_ERR_INVALID, "tile_rg must be 1 or 2");
+    if (value != 1 && value != 2 && value != 4) return fail(WG_ERR_INVALID, "tile_rg must be 1, 2 or 4");
     L->tune.tile_rg = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_max")) {

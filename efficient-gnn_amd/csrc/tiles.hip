@@ -85,15 +85,20 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
   l = __float_as_uint(r2) >> 16;
 }
 
-template <int NFB, int NWV, int RG>
 #ifndef WG_TILES_FLUSH  // computed tiles per float32 -> float64 flush of the block sums
 #define WG_TILES_FLUSH 4  // 917 vs 928 us per step at 1 (Reddit-size F=41, r02_s70), same S to 1e-8
 #endif
 #ifndef WG_TILES_MINW
 #define WG_TILES_MINW 6
 #endif
-__global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_tiles_kernel(TileArgs t) {
-  constexpr int TR = 16 * NWV * RG;    // rows per row block (RG groups of 16 per wave)
+// NWV waves; FW = false: every wave multiplies all NFB column blocks for its RG groups of 16
+// rows; FW = true: wave w multiplies column block w % NFB for RG row groups, so each B
+// fragment read from LDS serves RG row groups (NFB * 8 / RG waves for 128 rows)
+template <int NFB, int NWV, int RG, bool FW>
+__global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) void cheb_tiles_kernel(TileArgs t) {
+  constexpr int NRW = FW ? NWV / NFB : NWV;  // waves along the rows
+  constexpr int NFW = FW ? 1 : NFB;          // column blocks per wave
+  constexpr int TR = 16 * NRW * RG;    // rows per row block (RG groups of 16 per wave)
   constexpr int NT = 64 * NWV;         // threads
   constexpr int W = 16 * NFB;          // signal width
   constexpr int NV = kTC * W / 4;      // float4 per tile
@@ -102,12 +107,12 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
   __shared__ __attribute__((aligned(16))) uint16_t img[2][3][2 * img_dwords(NFB)];  // [buffer][piece hi/mid/lo][k, f]
   __shared__ uint32_t msk[2][TR];                                     // [buffer][row] the block's row masks
   const int tid = threadIdx.x;
-  if (tid < 256) {
+  for (int e = tid; e < 256; e += NT) {
     uint32_t d[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      d[q] = (((tid >> (2 * q)) & 1) ? 0x3F80u : 0u) | (((tid >> (2 * q + 1)) & 1) ? 0x3F800000u : 0u);
-    lut[tid] = make_uint4(d[0], d[1], d[2], d[3]);
+      d[q] = (((e >> (2 * q)) & 1) ? 0x3F80u : 0u) | (((e >> (2 * q + 1)) & 1) ? 0x3F800000u : 0u);
+    lut[e] = make_uint4(d[0], d[1], d[2], d[3]);
   }
   const int4 it = t.items[blockIdx.x];
   const int64_t rb = it.x;
@@ -155,11 +160,11 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
     if (tid < TR) msk[buf][tid] = w;
   };
 
-  double acc[RG][NFB][4];
+  double acc[RG][NFW][4];
 #pragma unroll
   for (int g = 0; g < RG; ++g)
 #pragma unroll
-    for (int fb = 0; fb < NFB; ++fb)
+    for (int fb = 0; fb < NFW; ++fb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[g][fb][i] = 0.0;
 
@@ -168,14 +173,16 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
   const int trow = 8 * (lane >> 4) + ((lane & 15) >> 2);
   const int tcolo = 4 * (lane & 3);
   const int tr_lo = img_row<NFB>(trow) + tcolo, tr_hi = img_row<NFB>(trow + 4) + tcolo;
-  const int mrow = 16 * RG * wave + (lane & 15);  // this lane's A row of row group 0 (of the block)
+  const int rwave = FW ? wave / NFB : wave;       // the wave's slot along the rows
+  const int fb0 = FW ? wave % NFB : 0;            // its first column block
+  const int mrow = 16 * RG * rwave + (lane & 15);  // this lane's A row of row group 0 (of the block)
   const int mshift = 8 * (lane >> 4);              // its byte of the 32-bit row mask
   // float32 MFMA sums of the last <= WG_TILES_FLUSH computed tiles, added to the float64 acc
-  f32x4 cacc[NFB][RG];
+  f32x4 cacc[NFW][RG];
   int nacc = 0;
   auto flush = [&]() {
 #pragma unroll
-    for (int fb = 0; fb < NFB; ++fb)
+    for (int fb = 0; fb < NFW; ++fb)
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
 #pragma unroll
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
     nacc = 0;
   };
 #pragma unroll
-  for (int fb = 0; fb < NFB; ++fb)
+  for (int fb = 0; fb < NFW; ++fb)
 #pragma unroll
     for (int g = 0; g < RG; ++g) cacc[fb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int buf) {
@@ -201,8 +208,9 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
 #pragma unroll
     for (int g = 0; g < RG; ++g) a[g] = __builtin_bit_cast(bf16x8, lut[(mw[g] >> mshift) & 0xFFu]);
 #pragma unroll
-    for (int fb = 0; fb < NFB; ++fb) {
-      f32x4 (&c)[RG] = cacc[fb];
+    for (int fw = 0; fw < NFW; ++fw) {
+      const int fb = fb0 + fw;
+      f32x4 (&c)[RG] = cacc[fw];
 #pragma unroll
       for (int p = 2; p >= 0; --p) {  // lo, mid, hi: one B fragment read, RG row groups
 #ifdef WG_TILES_PROBE_NO_TR  // timing attribution only (results wrong): no B reads from LDS
@@ -259,12 +267,12 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? WG_TILES_MINW : 4) void cheb_t
   for (int g = 0; g < RG; ++g)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int rl = 16 * (RG * wave + g) + 4 * (lane >> 4) + i;
+      const int rl = 16 * (RG * rwave + g) + 4 * (lane >> 4) + i;
       const int64_t row = rb * TR + rl;
       if (it.w < 0 && row >= t.n_plan) continue;
       double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * TR + rl) * W;
 #pragma unroll
-      for (int fb = 0; fb < NFB; ++fb) dst[16 * fb + (lane & 15)] = acc[g][fb][i];
+      for (int fw = 0; fw < NFW; ++fw) dst[16 * (fb0 + fw) + (lane & 15)] = acc[g][fw][i];
     }
 }
 
@@ -533,12 +541,14 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
   if (p->n_items > 0) {
     // 128-row blocks: 8 waves of 16 rows, or (tile_rg = 2) 4 waves of two 16-row groups sharing
     // each B fragment (half the LDS reads)
-    const int rg = (p->rows == 128 && L->tune.tile_rg == 2) ? 2 : 1;
+    const int rg = p->rows == 128 ? L->tune.tile_rg : 1;
     const dim3 grid(p->n_items), block(4 * p->rows / rg);
 #define WG_TILES(NFB)                                                                                  \
-  if (p->rows == 64) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 1>), grid, block, 0, stream, t);   \
-  else if (rg == 2) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 2>), grid, block, 0, stream, t);   \
-  else hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 8, 1>), grid, block, 0, stream, t);
+  if (p->rows == 64) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 1, false>), grid, block, 0, stream, t);             \
+  else if (rg == 4) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 2 * NFB, 4, true>), dim3(p->n_items), dim3(128 * NFB), 0, \
+                                       stream, t);                                                                  \
+  else if (rg == 2) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 2, false>), grid, block, 0, stream, t);             \
+  else hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 8, 1, false>), grid, block, 0, stream, t);
     switch (F / 16) {
       case 1: WG_TILES(1) break;
       case 2: WG_TILES(2) break;
