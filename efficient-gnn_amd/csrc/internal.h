@@ -268,8 +268,9 @@ int build_operator(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indi
 int sort_row_columns(wg_laplacian_s* L, hipStream_t stream);
 // step.hip
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
+// hybrid: the plan of the hybrid step's tail (tiles.hip; its own key and larger work units)
 int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, int block = -1, int64_t r0 = 0,
-             int64_t r1 = 0);
+             int64_t r1 = 0, bool hybrid = false);
 // S_out (finalize fused into the last step; needs S, H and F within one tile):
 // the rows' final S and H go to caller row perm[row] of S_out / H
 // Clenshaw form of the heat sum (wavelet_features): a step computes

@@ -1128,7 +1128,17 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // keep more lanes per row for latency (PubMed-size F=40: 9.3 us with iter 24, 17.2
 // with 96).  F = 1 from 1 M nonzeros: 8 entries per lane (ogbn-arxiv-size: 10.7 us per
 // step vs 11.6 with 16, s34).
-void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter) {
+void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter,
+                   bool hybrid = false) {
+  if (hybrid) {
+    // the hybrid step's tail (~22 % of each row's entries): one sub-group per row up
+    // to 6144 entries per lane, 4096-iteration block and split units (Reddit-size F=41: 784 vs 917 us
+    // per step with the gather kernel's defaults, profiles/r02/s72)
+    *iter = t.iter > 0 ? t.iter : 6144;
+    *block_iter = t.block_iter > 0 ? t.block_iter : 4096;
+    *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : 4096;
+    return;
+  }
   const bool wide = G <= 16;
   const bool big = nnz >= (int64_t)1 << 20;
   // from 8 M nonzeros: longer team runs and 256-iteration split-row chunks (Reddit-size F=41,
@@ -1149,12 +1159,14 @@ void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_it
 // Row-block plans (block >= 0): the same classification over internal rows [r0, r1) only (the
 // row-sharded chain streams each block's rows to the peers while the next block computes,
 // dist.hip); the block's split rows index rowchunks / arrivals from r0.
-int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, int block, int64_t r0, int64_t r1) {
+int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, int block, int64_t r0, int64_t r1,
+             bool hybrid) {
   active_only = active_only && L->reordered;
   const int NW = (L->tune.waves == 16 || L->tune.waves == 8) ? L->tune.waves : 4;
   const bool ranged = block >= 0;
+  hybrid = hybrid && !ranged;
   const int64_t key = (int64_t)(((LF * 8 + VEC) * 2 + (active_only ? 1 : 0)) * 32 + NW +
-                                (L->tune.hot > 0 && !ranged ? (1 << 28) : 0)) +
+                                (L->tune.hot > 0 && !ranged ? (1 << 28) : 0) + (hybrid ? (1 << 29) : 0)) +
                       (ranged ? ((int64_t)(block + 1) << 32) : 0);
   auto it = L->plans.find(key);
   if (it != L->plans.end() && (!ranged || (it->second.row0 == r0 && it->second.row1 == r1))) {
@@ -1200,7 +1212,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, i
   p.row0 = base;
   p.row1 = ranged ? r1 : n;
   int iter, block_iter, chunk_iter;
-  default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter);
+  default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter, hybrid);
   const int64_t team_max = (int64_t)G * iter;
   const int64_t block_max = (int64_t)NW * G * block_iter;
   const int64_t CH = (int64_t)NW * G * chunk_iter;
@@ -1346,7 +1358,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       Plan* plan = nullptr;
       const bool ranged = ph && ph->block >= 0;
       int rc = ranged ? get_plan(L, LF, vec, false, &plan, ph->block, ph->row_begin, ph->row_end)
-                      : get_plan(L, LF, vec, active_only, &plan);
+                      : get_plan(L, LF, vec, active_only, &plan, -1, 0, 0, /*hybrid=*/ph && ph->col);
       if (rc) return rc;
       StepArgs a{};
       a.rowptr = L->rowptr;
