@@ -1129,11 +1129,13 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // with 96).  F = 1 from 1 M nonzeros: 8 entries per lane (ogbn-arxiv-size: 10.7 us per
 // step vs 11.6 with 16, s34).
 void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter,
-                   bool hybrid = false) {
-  if (hybrid) {
-    // the hybrid step's tail (~22 % of each row's entries): one sub-group per row up
-    // to 6144 entries per lane, 4096-iteration block and split units (Reddit-size F=41: 784 vs 917 us
-    // per step with the gather kernel's defaults, profiles/r02/s72)
+                   bool hybrid = false, int64_t rows = 0) {
+  if (hybrid && rows >= (int64_t)64 * G * 256) {
+    // the hybrid step's tail (~22 % of each row's entries) on graphs with rows
+    // enough for 64 waves of one-row sub-groups per CU: one sub-group per row up to 6144 entries,
+    // 4096-iteration block and split units (Reddit-size F=41: 784 vs 917 us per step with the
+    // gather kernel's defaults, profiles/r02/s72; its 8-way shard, 29 k rows, is faster with
+    // them: 162 vs 296 us, r02_s73)
     *iter = t.iter > 0 ? t.iter : 6144;
     *block_iter = t.block_iter > 0 ? t.block_iter : 4096;
     *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : 4096;
@@ -1212,7 +1214,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, i
   p.row0 = base;
   p.row1 = ranged ? r1 : n;
   int iter, block_iter, chunk_iter;
-  default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter, hybrid);
+  default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter, hybrid, ranged ? r1 - r0 : n);
   const int64_t team_max = (int64_t)G * iter;
   const int64_t block_max = (int64_t)NW * G * block_iter;
   const int64_t CH = (int64_t)NW * G * chunk_iter;
