@@ -1130,15 +1130,17 @@ int pick_vec(int64_t F, std::initializer_list<const void*> ptrs) {
 // step vs 11.6 with 16, s34).
 void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_iter, int* chunk_iter,
                    bool hybrid = false, int64_t rows = 0) {
-  if (hybrid && rows >= (int64_t)64 * G * 256) {
-    // the hybrid step's tail (~22 % of each row's entries) on graphs with rows
-    // enough for 64 waves of one-row sub-groups per CU: one sub-group per row up to 6144 entries,
-    // 4096-iteration block and split units (Reddit-size F=41: 784 vs 917 us per step with the
-    // gather kernel's defaults, profiles/r02/s72; its 8-way shard, 29 k rows, is faster with
-    // them: 162 vs 296 us, r02_s73)
-    *iter = t.iter > 0 ? t.iter : 6144;
-    *block_iter = t.block_iter > 0 ? t.block_iter : 4096;
-    *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : 4096;
+  // the hybrid step's tail (~22 % of each row's entries) wants longer one-row
+  // sub-groups and larger block / split units the more rows there are to fill the CUs with
+  // (Reddit-size F=41, rows / (G x 256 CUs): 182 -> iter 6144: 784 vs 917 us per step with the
+  // gather kernel's defaults; its 2- and 4-way shards (92, 46) -> 1536: 415 vs 473 and 233 vs 249;
+  // the 8-way shard (23) keeps the defaults: 156 vs 172 with 1536; profiles/r02/s72-s74)
+  const int64_t per_cu = rows / ((int64_t)G * 256);
+  if (hybrid && per_cu >= 32) {
+    const bool big = per_cu >= 128;
+    *iter = t.iter > 0 ? t.iter : (big ? 6144 : 1536);
+    *block_iter = t.block_iter > 0 ? t.block_iter : (big ? 4096 : 1024);
+    *chunk_iter = t.chunk_iter > 0 ? t.chunk_iter : (big ? 4096 : 1024);
     return;
   }
   const bool wide = G <= 16;
