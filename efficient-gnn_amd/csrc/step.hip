@@ -1133,10 +1133,12 @@ void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_it
   // the hybrid step's tail (~22 % of each row's entries) wants longer one-row
   // sub-groups and larger block / split units the more rows there are to fill the CUs with
   // (Reddit-size F=41, rows / (G x 256 CUs): 182 -> iter 6144: 784 vs 917 us per step with the
-  // gather kernel's defaults; its 2- and 4-way shards (92, 46) -> 1536: 415 vs 473 and 233 vs 249;
-  // the 8-way shard (23) keeps the defaults: 156 vs 172 with 1536; profiles/r02/s72-s74)
+  // gather kernel's defaults; its 2-way shards (92) -> 1536: 415 vs 473; the 4-way shards (46)
+  // keep the defaults: 1536 gives 232-234 vs 246-249 on three ranks but 312 vs 247 on the fourth
+  // (a long-tailed row walked by one sub-group), the 8-way shards (23) 172 vs 156;
+  // profiles/r02/s72-s76)
   const int64_t per_cu = rows / ((int64_t)G * 256);
-  if (hybrid && per_cu >= 32) {
+  if (hybrid && per_cu >= 64) {
     const bool big = per_cu >= 128;
     *iter = t.iter > 0 ? t.iter : (big ? 6144 : 1536);
     *block_iter = t.block_iter > 0 ? t.block_iter : (big ? 4096 : 1024);
