@@ -1401,7 +1401,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.rsplit = ph->rsplit;
         a.rsplit2 = ph->rsplit2;
         a.part = ph->part + f0;
-        a.part2 = ph->part2;
+        a.part2 = ph->part2 ? ph->part2 + f0 : nullptr;
         if (a.phase == 1 || a.phase == 3) {  // nothing but the sums: no epilogue operands, no T / S / H stores
           a.xk = nullptr;
           a.S = nullptr;

@@ -84,6 +84,22 @@ def test_tiles_isolated_rows_and_no_closed_form():
         _close(S1, S0, "S")
 
 
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_tiles_with_signal_tiles(overlap):
+    """tile_f splits the step kernel's launch into column tiles (here 16 of the 48
+    columns each) while the dense blocks run over all columns at once: every
+    tile's tail sum meets its own columns of the blocks' sums."""
+    g = rmat_graph(4000, 120000, seed=13)
+    A = g.to_scipy()
+    X = np.random.default_rng(3).standard_normal((g.n, 48)).astype(np.float32)
+    ref = O.graph_wavelet_features(A, k=6, s=0.8, X0=X, return_all=True)
+    L = NormalizedLaplacian.from_graph(g)
+    H1, S1 = _run(L, X, 6, tiles=1, tile_th=8, tile_f=16, tiles_overlap=overlap)
+    assert "tiles:" in L.describe(48)
+    assert_parity(_np(S1), ref["S"], what=f"tile_f=16 overlap={overlap} S")
+    assert_parity(_np(H1), ref["H"], what=f"tile_f=16 overlap={overlap} H")
+
+
 def test_tiles_deterministic():
     g = rmat_graph(4000, 120000, seed=9)
     X = np.random.default_rng(1).standard_normal((g.n, 48)).astype(np.float32)
