@@ -139,7 +139,7 @@ def test_sharded_chain_cpu_gloo(world, kind, tiers):
 
 
 # ------------------------------------------------------------------ GPU, ranks share one device
-def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=1):
+def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=1, tiles=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -157,8 +157,10 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
         # lds 4 (hub teams) with a 256-column hub: the shard's hub mixes its own top columns
         # with every peer group's (halo groups in descending degree), the rest is gathered
         sw.L.tune(lds=lds, **({"lds_cb": 256} if lds == 4 else {}))
-        if exchange == "ipc":
-            sw.L.tune(overlap=1)   # the two-phase steps (off by default) on every IPC case
+        if tiles:   # the hybrid step on every shard: exchange-then-step, u_0 exchanged
+            sw.L.tune(tiles=1, tile_th=8, tile_max=3)
+        elif exchange == "ipc":
+            sw.L.tune(overlap=1)   # the two-phase steps (off by default) on every other IPC case
         q_path = "u" if (F == 1 and sw.u_len() > 0) else "t"
         rng = np.random.default_rng(0)
         X = rng.standard_normal((g.n, F)).astype(np.float32)
@@ -169,7 +171,9 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
         if exchange == "ipc":
             # the gather-kernel path overlaps each step's exchange with the step's own-column half
             ov = sw.info()["overlapped"]
-            assert ov == (q_path == "t" and sw.plan.n_halo > 0), (ov, q_path, sw.plan.n_halo)
+            assert ov == (q_path == "t" and sw.plan.n_halo > 0 and not tiles), (ov, q_path, sw.plan.n_halo)
+            if tiles:
+                assert "tiles:" in sw.L.describe(F + (-F) % 16), sw.L.describe(F)
             assert sw.info()["tiers"] == tiers
             sw.check_exchange()
             sw.close()
@@ -179,26 +183,28 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,kind,F,lds,exchange,tiers", [
-    (2, "rmat", 1, 2, "host", 1), (4, "rmat", 1, 2, "host", 1), (2, "rmat", 1, 0, "host", 1), (3, "rmat", 40, 2, "host", 1),
-    (2, "weighted", 4, 2, "host", 1), (2, "weighted", 1, 2, "host", 1),
-    (2, "rmat", 1, 2, "ipc", 1), (4, "rmat", 1, 2, "ipc", 1), (2, "rmat", 1, 0, "ipc", 1), (3, "rmat", 40, 2, "ipc", 1),
-    (2, "weighted", 4, 2, "ipc", 1), (3, "weighted", 1, 2, "ipc", 1), (2, "rmat", 1, 4, "ipc", 1), (2, "rmat", 1, 4, "host", 1),
-    (3, "rmat", 40, 2, "ipc", 2), (2, "weighted", 4, 2, "ipc", 2), (4, "rmat", 1, 2, "ipc", 2),
-    (3, "rmat", 8, 2, "host", 2), (8, "rmat", 40, 2, "ipc", 1), (8, "rmat", 1, 2, "ipc", 1),
-    (8, "weighted", 4, 2, "ipc", 2)])
-def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiers):
+@pytest.mark.parametrize("world,kind,F,lds,exchange,tiers,tiles", [
+    (2, "rmat", 1, 2, "host", 1, 0), (4, "rmat", 1, 2, "host", 1, 0), (2, "rmat", 1, 0, "host", 1, 0), (3, "rmat", 40, 2, "host", 1, 0),
+    (2, "weighted", 4, 2, "host", 1, 0), (2, "weighted", 1, 2, "host", 1, 0),
+    (2, "rmat", 1, 2, "ipc", 1, 0), (4, "rmat", 1, 2, "ipc", 1, 0), (2, "rmat", 1, 0, "ipc", 1, 0), (3, "rmat", 40, 2, "ipc", 1, 0),
+    (2, "weighted", 4, 2, "ipc", 1, 0), (3, "weighted", 1, 2, "ipc", 1, 0), (2, "rmat", 1, 4, "ipc", 1, 0), (2, "rmat", 1, 4, "host", 1, 0),
+    (3, "rmat", 40, 2, "ipc", 2, 0), (2, "weighted", 4, 2, "ipc", 2, 0), (4, "rmat", 1, 2, "ipc", 2, 0),
+    (3, "rmat", 8, 2, "host", 2, 0), (8, "rmat", 40, 2, "ipc", 1, 0), (8, "rmat", 1, 2, "ipc", 1, 0),
+    (8, "weighted", 4, 2, "ipc", 2, 0), (2, "rmat", 48, 2, "ipc", 1, 1), (3, "rmat", 41, 2, "ipc", 1, 1),
+    (4, "rmat", 48, 2, "ipc", 2, 1)])
+def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiers, tiles):
     """Several ranks on one GPU: the Python exchange over gloo host copies, or
     the native chain with the one-sided IPC exchange (ranks pull from each
     other's memory; same-device IPC stands in for xGMI peers).  tiers = 2:
-    the halo in a hot and a cold tier (three-phase steps)."""
+    the halo in a hot and a cold tier (three-phase steps).  tiles = 1: the
+    hybrid step on every shard (dense blocks over [own | halo] columns)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     K = 8
-    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, kind, K, F, q, lds, exchange, tiers))
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, kind, K, F, q, lds, exchange, tiers, tiles))
              for r in range(world)]
     for p in procs:
         p.start()
