@@ -4,34 +4,35 @@
 // On an unweighted graph the value-free Clenshaw step sums u_j = b_j * dinv_j
 // over each row's columns (step.hip, reference calibration/WATS.py:32-36).  In
 // descending-degree order the hub columns form dense blocks: on the Reddit-size
-// R-MAT graph the (64-row block, 32-column tile) pairs holding >= 64 entries
-// carry 78 % of the 114.6 M entries.  The gather kernel pays two or three L2
-// line requests per entry (a 192-B row of u each); a dense block instead reads
-// its 32 rows of u once (6 KB, coalesced), shared by the 64 rows of the block.
+// R-MAT graph the (128-row block, 32-column tile) pairs holding >= 128 entries
+// carry 78 % of the 114.6 M entries.  The gather kernel pays two L2 line
+// requests per entry (a 192-B row of u each); a dense block instead reads its
+// 32 rows of u once (6 KB, coalesced), shared by the 128 rows of the block.
 //
 //   part[row] = sum over the row's dense entries of u_j      (this file)
 //   step      = cheb_step_kernel over the tail entries (each row's tail first in
-//               tcol), + part, epilogue: phase 4 after the blocks, or (tiles_overlap)
-//               phase 1 into part2 on a side stream beside them, then phase 6
+//               tcol; its own plan, get_plan(hybrid)), + part, epilogue: phase 4
+//               after the blocks, or (tiles_overlap) phase 1 into part2 on a side
+//               stream beside them, then phase 6
 //
-// The block sum is a 64 x 32 by 32 x W product A.U with A a 0/1 matrix (exact in
+// The block sum is a 128 x 32 by 32 x W product A.U with A a 0/1 matrix (exact in
 // bf16).  U is split exactly into three bf16 pieces, u = hi + mid + lo
 // (truncations: hi = u with the low 16 bits cleared, mid likewise of u - hi, and
 // lo = u - hi - mid has at most 8 significant bits), so every product is exact
-// and each v_mfma_f32_16x16x32_bf16 adds 32 of them in float32; each block's
-// float32 sums (<= 4 blocks x 96 exact terms) are added to a float64 accumulator.  Results
-// differ from the all-float64 gather kernel only by that float32 rounding of
-// each block sum (tests/test_gpu_parity.py, test_tiles_*).
+// and each v_mfma_f32_16x16x32_bf16 adds 32 of them in float32; the float32 sums
+// of up to 4 blocks (<= 384 exact terms) are added to a float64 accumulator.
+// Results differ from the all-float64 gather kernel by that float32 rounding
+// only (6.7e-8 relative on Reddit-size F = 41; tests/test_tiles.py).
 //
-// Workgroup = 4 waves = one row block (or a share of a long row block's dense
-// blocks: those write float64 slots that tiles_combine_kernel sums in order).
-// Per dense block: the 256 lanes load the 32 x W tile of u (float4, L2), split it
-// into the three bf16 pieces in an LDS image per piece (bank-conflict-free rows,
-// img_row; double-buffered, and a 3-deep register ring keeps three tiles' loads
-// in flight),
-// and each wave multiplies its 16 rows: A fragments from a byte -> 8 x bf16
-// lookup table indexed by the row mask, B fragments by the transposed LDS read
-// ds_read_b64_tr_b16 (two per fragment), three MFMAs (lo, mid, hi) per 16 columns.
+// Workgroup = 8 waves = one 128-row block (or a share of a long row block's
+// dense blocks: those write float64 slots that tiles_combine_kernel sums in
+// order).  Per dense block: the lanes load the 32 x W tile of u (float4) three
+// tiles ahead in a register ring, split it into the three bf16 pieces in a
+// double-buffered LDS image per piece (bank-conflict-free rows, img_row), and
+// each wave multiplies its 16 rows: A fragments from a byte -> 8 x bf16 lookup
+// table indexed by the row mask, B fragments by the transposed LDS read
+// ds_read_b64_tr_b16 (two per fragment), three MFMAs (lo, mid, hi) per 16
+// columns.  DESIGN.md 4.6 has the measurements and the variants kept as knobs.
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
@@ -71,7 +72,7 @@ struct TileArgs {
   const uint32_t* bmask;
   const int4* items;
   double* part;          // [rows][ld]
-  double* slots;         // [slot][64][W]
+  double* slots;         // [slot][rows per block][W]
 };
 
 // u = hi + mid + lo exactly, each piece a bf16 (the high half of a float32)
