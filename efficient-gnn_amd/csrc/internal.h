@@ -200,9 +200,9 @@ struct Tuning {
   int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple
   int32_t tiles = -1;        // hybrid step (tiles.hip): -1 = auto (unweighted, width % 16 == 0, >= 8 M nonzeros,
                              // >= 30 % of the entries in dense blocks), 0 = off, 1 = whenever it applies
-  int32_t tile_th = 128;     // entries that make a (row block, 32-column tile) pair a dense block
-  int32_t tile_max = 64;     // dense blocks per workgroup (longer row blocks split over slots); 0 = auto
-                             // (~3072 items: slower, 8-way Reddit shard 182 vs 162 us per step, r02_s62)
+  int32_t tile_th = 96;      // entries that make a (row block, 32-column tile) pair a dense block
+  int32_t tile_max = 0;      // dense blocks per workgroup (longer row blocks split over slots);
+                             // 0 = auto: 128 from 100 k rows, else 64 (tiles.hip, r02_s80-s81)
   int32_t tiles_overlap = 0; // hybrid step: the tail gathers on a side stream beside the dense blocks
                              // (Reddit-size F=41: 1176 vs 1136 us per step sequential, r02_tiles: off)
   int32_t tile_rows = 128;   // hybrid step: rows per row block (64 or 128)

@@ -388,10 +388,11 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
     if (nb > 0) rbs.push_back(make_int2((int)rb, first));  // nb == 0: every entry is tail, no part added
   }
   // work items: a row block's dense blocks, split over several workgroups (slots) past tmax;
-  // auto tmax: about 3072 items for the chip's 256 CUs x 3 resident workgroups x 4, within [8, 64]
-  // (the 8-way Reddit-size shard: 22 k blocks -> 8 per item; the whole graph: 187 k -> 61)
+  // auto (tile_max <= 0): 128 blocks per workgroup from 100 k rows, else 64 (Reddit-size F=41,
+  // 128 vs 64: whole graph 751 vs 773 us per step, 2-way shard 383 vs 408; the 4- and 8-way
+  // shards want more workgroups: 259 vs 242 and 184 vs 153; profiles/r02/s80-s81)
   const int64_t nblk = (int64_t)bct.size();
-  if (tmax <= 0) tmax = (int)std::max<int64_t>(8, std::min<int64_t>(64, ceil_div(nblk, 3072)));
+  if (tmax <= 0) tmax = n_plan >= 100000 ? 128 : 64;
   for (size_t q0 = 0; q0 < rbs.size(); ++q0) {
     const int rb = rbs[q0].x, first = rbs[q0].y;
     const int32_t nb = (int32_t)((q0 + 1 < rbs.size() ? rbs[q0 + 1].y : nblk) - first);
