@@ -428,6 +428,9 @@ __device__ __forceinline__ void accumulate_hot1(const StepArgs& a, int32_t e, in
 // fs loads element t0+fs and the sub-group shares the LF (col, val) pairs
 // through ds_bpermute, which runs on the LDS pipe.  Same elements, same
 // order as accumulate() -> bitwise-identical sums.  U = gathers in flight.
+#ifndef WG_BCAST_U  // gathers in flight per lane on the widths whose LF is not a multiple of 5
+#define WG_BCAST_U 4
+#endif
 template <int VEC, int U>
 __device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
                                                  const float* __restrict__ xb, double (&acc)[VEC], int fs,
@@ -589,7 +592,7 @@ __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t 
     } else if (a.LF % 5 == 0) {
       accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
     } else {
-      accumulate_bcast<VEC, 4>(a, e, e1, stride, xb, acc, fs, base);
+      accumulate_bcast<VEC, WG_BCAST_U>(a, e, e1, stride, xb, acc, fs, base);
     }
   } else {
     accumulate<VEC>(a, e, e1, stride, xb, acc);
