@@ -754,8 +754,9 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
 
 template <int VEC, bool BCAST, int NW>
 __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
-  // knob xcd: workgroups are dealt to the 8 XCDs round-robin; remap so that XCD x runs the
-  // contiguous x-th eighth of the plan's units (rows of similar degree share an L2)
+  // knob xcd (off): workgroups are dealt to the 8 XCDs round-robin; remap so that XCD x runs
+  // the contiguous x-th eighth of the plan's units.  Measured 3x slower on arxiv F=40: the units
+  // are in descending row length, so one XCD gets every hub row
   int32_t unit = (int32_t)blockIdx.x;
   if (a.xcd) {
     const int32_t n = (int32_t)gridDim.x, q = n >> 3, r = n & 7, x = unit & 7;
