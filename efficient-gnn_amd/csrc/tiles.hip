@@ -366,7 +366,10 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
         if (s >= 0) {
           uint32_t& w = bmask[(size_t)s * kTR + (r - r0)];
           const uint32_t bit = 1u << (c % kTC);
-          if (w & bit) return fail(WG_ERR_INVALID, "tiles: duplicate column %d in row %lld", c, (long long)r);
+          if (w & bit) {  // a repeated entry: a row mask cannot count it twice -- keep the gather kernel
+            p->n_blocks = 0;
+            return WG_OK;
+          }
           w |= bit;
           ++dense;
         } else {

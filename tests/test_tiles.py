@@ -160,3 +160,20 @@ def test_clenshaw_step_abi(F, tiles):
     _close((outu.double() / dinv).float(), ref.float(), f"value-free F={F} tiles={tiles}", tol=2e-6)
     if tiles:
         assert "tiles:" in L.describe(F)
+
+
+def test_tiles_duplicate_entries_keep_the_gather_kernel():
+    """A CSR with a repeated entry (outside the canonical-input precondition) cannot be
+    a 0/1 row mask: the hybrid step declines and the gather kernel runs, unchanged."""
+    g = rmat_graph(3000, 90000, seed=4)
+    indptr, indices = g.indptr.copy(), g.indices.copy()
+    r = int(np.argmax(np.diff(indptr)))                 # repeat the first entry of the longest row
+    pos = indptr[r]
+    indices = np.insert(indices, pos, indices[pos])
+    indptr[r + 1:] += 1
+    X = np.random.default_rng(8).standard_normal((g.n, 48)).astype(np.float32)
+    L = NormalizedLaplacian.from_csr(indptr, indices, None, n=g.n)
+    H0, S0 = _run(L, X, 6, tiles=0)
+    H1, S1 = _run(L, X, 6, tiles=1, tile_th=4)
+    assert "tiles:" not in L.describe(48)
+    assert torch.equal(S0, S1) and torch.equal(H0, H1)
