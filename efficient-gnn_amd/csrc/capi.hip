@@ -341,8 +341,11 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   const size_t stride = ((size_t)n * Fp + 63) / 64 * 64;
   const size_t ustride = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
   // the hybrid step (tiles.hip) gathers the first step's X0 value-free too, as u_0 = X0 * dinv
-  const bool u0 = !lp && L->tune.clenshaw && K >= 1 && L->unit && L->tune.uscale && !L->tune.gbuf &&
-                  L->tune.hubf == 0 && L->tune.hot == 0 && tiles_wanted(L, Fp);
+  TilePlan* tp0 = nullptr;  // the hybrid step's plan, when it applies (built here once, synchronous)
+  if (!lp && L->tune.clenshaw && K >= 1 && L->unit && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 &&
+      L->tune.hot == 0 && !L->tune.probe && tiles_wanted(L, Fp))
+    if (int rc0 = get_tile_plan(L, /*active_only=*/true, Fp, &tp0)) return rc0;
+  const bool u0 = tp0 != nullptr;
   const size_t need = (u0 ? 4 : 3) * stride + 2 * ustride;
   if (L->ws_floats < need) {
     WG_HIP_TRY(hipStreamSynchronize(stream));

@@ -616,7 +616,9 @@ struct wg_dist_s {
                         L->tune.hot == 0) ? 1 : 0;
       // the hybrid step (tiles.hip): phase 1 exchanges and gathers u_0 = X0 * dinv (own rows scaled
       // in place; x0 keeps X0) value-free like every later phase
-      const bool u0 = useu && tiles_wanted(L, Fp);
+      TilePlan* tp0 = nullptr;
+      if (!rc && useu && K >= 1 && !L->tune.probe && tiles_wanted(L, Fp)) rc = get_tile_plan(L, false, Fp, &tp0);
+      const bool u0 = tp0 != nullptr;
       if (!rc && u0) rc = launch_scale_rows(L, n_own, Fp, x0, A[0], st);
       for (int32_t j = 1; j <= K && !rc; ++j) {
         const int32_t k = K - j;  // this phase computes b_k (k = 0: the final S)
