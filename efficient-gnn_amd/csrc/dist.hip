@@ -614,11 +614,12 @@ struct wg_dist_s {
       // DESIGN.md 4.1) and the halo rows exchanged are u rows; X0 (phase 1) stays unscaled
       const int useu = (L->unit && L->values_null && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 &&
                         L->tune.hot == 0) ? 1 : 0;
-      // the hybrid step (tiles.hip): phase 1 exchanges and gathers u_0 = X0 * dinv (own rows scaled
-      // in place; x0 keeps X0) value-free like every later phase
-      TilePlan* tp0 = nullptr;
-      if (!rc && useu && K >= 1 && !L->tune.probe && tiles_wanted(L, Fp)) rc = get_tile_plan(L, false, Fp, &tp0);
-      const bool u0 = tp0 != nullptr;
+      // phase 1 exchanges and gathers u_0 = X0 * dinv (own rows scaled in place; x0 keeps X0)
+      // value-free like every later phase.  The choice depends only on useu, which every rank
+      // shares (values == NULL on every shard), never on this rank's own hybrid-step plan: the
+      // halo rows a rank receives in phase 1 must be in the format it gathers (a
+      // shard that declined its plan must not send unscaled rows to one that took it).
+      const bool u0 = useu && K >= 1;
       if (!rc && u0) rc = launch_scale_rows(L, n_own, Fp, x0, A[0], st);
       for (int32_t j = 1; j <= K && !rc; ++j) {
         const int32_t k = K - j;  // this phase computes b_k (k = 0: the final S)

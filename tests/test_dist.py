@@ -157,8 +157,12 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
         # lds 4 (hub teams) with a 256-column hub: the shard's hub mixes its own top columns
         # with every peer group's (halo groups in descending degree), the rest is gathered
         sw.L.tune(lds=lds, **({"lds_cb": 256} if lds == 4 else {}))
-        if tiles:   # the hybrid step on every shard: exchange-then-step, u_0 exchanged
-            sw.L.tune(tiles=1, tile_th=8, tile_max=3)
+        # tiles = 1: the hybrid step on every shard, exchange-then-step, u_0
+        # exchanged; tiles = 2: the same except rank 1, whose shard keeps the gather kernel (ADVICE
+        # r2: ranks that disagree on the plan must still exchange u_0 in one format)
+        hybrid = bool(tiles) and not (tiles == 2 and rank == 1)
+        if tiles:
+            sw.L.tune(tiles=1 if hybrid else 0, tile_th=8, tile_max=3)
         elif exchange == "ipc":
             sw.L.tune(overlap=1)   # the two-phase steps (off by default) on every other IPC case
         q_path = "u" if (F == 1 and sw.u_len() > 0) else "t"
@@ -173,7 +177,7 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
             ov = sw.info()["overlapped"]
             assert ov == (q_path == "t" and sw.plan.n_halo > 0 and not tiles), (ov, q_path, sw.plan.n_halo)
             if tiles:
-                assert "tiles:" in sw.L.describe(F + (-F) % 16), sw.L.describe(F)
+                assert ("tiles:" in sw.L.describe(F + (-F) % 16)) == hybrid, sw.L.describe(F)
             assert sw.info()["tiers"] == tiers
             sw.check_exchange()
             sw.close()
@@ -191,13 +195,14 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
     (3, "rmat", 40, 2, "ipc", 2, 0), (2, "weighted", 4, 2, "ipc", 2, 0), (4, "rmat", 1, 2, "ipc", 2, 0),
     (3, "rmat", 8, 2, "host", 2, 0), (8, "rmat", 40, 2, "ipc", 1, 0), (8, "rmat", 1, 2, "ipc", 1, 0),
     (8, "weighted", 4, 2, "ipc", 2, 0), (2, "rmat", 48, 2, "ipc", 1, 1), (3, "rmat", 41, 2, "ipc", 1, 1),
-    (4, "rmat", 48, 2, "ipc", 2, 1)])
+    (4, "rmat", 48, 2, "ipc", 2, 1), (3, "rmat", 48, 2, "ipc", 1, 2), (2, "rmat", 41, 2, "ipc", 1, 2)])
 def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiers, tiles):
     """Several ranks on one GPU: the Python exchange over gloo host copies, or
     the native chain with the one-sided IPC exchange (ranks pull from each
     other's memory; same-device IPC stands in for xGMI peers).  tiers = 2:
     the halo in a hot and a cold tier (three-phase steps).  tiles = 1: the
-    hybrid step on every shard (dense blocks over [own | halo] columns)."""
+    hybrid step on every shard (dense blocks over [own | halo] columns); tiles = 2:
+    on every shard but rank 1's (the ranks disagree on the plan)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = mp.get_context("spawn")
