@@ -2,10 +2,12 @@
 
 numpy restatement of the reference's ``utils/ece.py:8-89``
 (``calculate_ece`` / ``calculate_average_ece``), used only by tests to check
-``wats_hip.metrics``.  PARITY UNPINNED against the reference module itself:
-``utils/ece.py`` imports seaborn and matplotlib (``utils/ece.py:3,6``), which
-are not installed here, so it cannot be imported to generate golden vectors;
-this restatement follows the file line by line instead.
+``wats_hip.metrics``.  PINNED to the reference: ``tools/gen_ece_golden.py``
+imports the reference module itself (a stub stands in for its unused seaborn
+import, ``utils/ece.py:6``) and writes its outputs on logits, probabilities
+and binning edge cases to ``tests/golden/ece_cases.npz``;
+``tests/test_oracle.py::test_ece_oracle_bitwise_vs_reference_fixtures``
+checks this restatement against every case bit for bit.
 """
 import numpy as np
 from scipy.special import softmax

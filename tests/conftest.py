@@ -21,7 +21,7 @@ def pytest_configure(config):
 
 def golden_names(prefix=""):
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, prefix + "*.npz"))
-                  if not os.path.basename(p).startswith("wats_forward"))
+                  if not os.path.basename(p).startswith(("wats_forward", "ece_")))
 
 
 def load_golden(name):

@@ -87,9 +87,11 @@ def _check_H(H, S):
 @pytest.mark.parametrize("F,cols", [(1, None), (41, [0, 17, 40])])
 def test_reddit_random_signal_vs_oracle(F, cols):
     """Reddit-size K=16, auto plan: the F=1 chunk-window LDS kernel
-    (csrc/lds1.hip) and the F=41 wide tiles (padded to 44; split rows with
-    128-entry chunks, in-kernel combine, non-temporal stores) -- the >= 16 M
-    nonzero plan defaults."""
+    (csrc/lds1.hip) and, at F=41, the hybrid step (width padded
+    to 48, dense blocks on the bf16 MFMA tile kernel, the rest of each row
+    gathered by the step kernel with the >= 8 M-nonzero tail plan) -- asserted,
+    so a change of the auto rule cannot move the only full-size test of the
+    MFMA kernel back onto the gather kernel."""
     indptr, indices = _graph("reddit")
     n = len(indptr) - 1
     L = NormalizedLaplacian(n, torch.from_numpy(indptr), torch.from_numpy(indices))
@@ -99,6 +101,8 @@ def test_reddit_random_signal_vs_oracle(F, cols):
     X = np.random.default_rng(11 + F).standard_normal((n, F)).astype(np.float32)
     H, S = wats_hip.graph_wavelet_features(L, k=16, X0=torch.from_numpy(X), return_S=True)
     S, H = S.cpu().numpy(), H.cpu().numpy()
+    if F == 41:
+        assert "tiles:" in L.describe(48), "the hybrid step did not run: " + L.describe(48)
     L.close()
     S_ref, H_ref = _oracle(indptr, indices, X, 16, cols)
     got = S if cols is None else S[:, cols]
@@ -186,6 +190,8 @@ def _shard_worker(rank, world, port, config, F, K, seed_x, q, graph_dir):
         H, S = outs[0]
         same = all(torch.equal(o[1], S) for o in outs)
         path = "u" if (F == 1 and sw.u_len() > 0) else "t"
+        if F > 1 and "tiles:" in sw.L.describe(F + (-F) % 16):
+            path = "tiles"   # the hybrid step ran on this shard
         sw.check_exchange()
         sw.close()
         q.put((rank, r0, r1, S.cpu().numpy(), H.cpu().numpy(), same, path))
@@ -233,6 +239,8 @@ def test_sharded_full_size_vs_oracle(world, config, F, cols, tmp_path):
         assert r[5], f"rank {r[0]}: eager / captured / replayed chains differ"
     if F == 1 and config == "reddit":
         assert all(r[6] == "u" for r in res), "Reddit F=1 shards should run the LDS kernel"
+    if F == 41:
+        assert all(r[6] == "tiles" for r in res), f"every Reddit F=41 shard should run the hybrid step: {[r[6] for r in res]}"
     S = np.concatenate([r[3] for r in res])
     H = np.concatenate([r[4] for r in res])
     indptr, indices = _graph(config)

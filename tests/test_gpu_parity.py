@@ -2,6 +2,8 @@
 golden vectors and the CPU oracle, on seeded inputs; size-independent
 properties (eigenvector KAT, determinism, relabelling invariance) at the
 named full sizes."""
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -607,8 +609,8 @@ def test_split_rows_inkernel_combine_bitwise_equals_combine_kernel():
 @pytest.mark.parametrize("logits,n,c", [(True, 5000, 7), (False, 3000, 40), (True, 169343, 40)])
 def test_device_ece_vs_restatement(logits, n, c):
     """wats_hip.metrics on GPU tensors (utils/ece.py:8-89: 10 equal-width
-    bins per class, np.digitize quirks) against oracle/ece_oracle.py (parity
-    unpinned vs the reference import, which needs seaborn)."""
+    bins per class, np.digitize quirks) against oracle/ece_oracle.py (pinned
+    bit for bit to the reference's own outputs, test_oracle.py)."""
     from oracle import ece_oracle as E
     from wats_hip import metrics as M
     rng = np.random.default_rng(n)
@@ -623,3 +625,17 @@ def test_device_ece_vs_restatement(logits, n, c):
     assert abs(got - ref) < 1e-6
     for k in (0, c // 2, c - 1):
         assert abs(M.calculate_ece(o_d, y_d, k, logits=logits) - E.calculate_ece(out, y, k, logits=logits)) < 1e-6
+
+
+def test_device_ece_vs_reference_fixtures():
+    """wats_hip.metrics on device tensors against the reference's own
+    calculate_ece / calculate_average_ece outputs (tests/golden/ece_cases.npz,
+    tools/gen_ece_golden.py): every case, every class, within 1e-7."""
+    from wats_hip import metrics as M
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "ece_cases.npz"))
+    for nm in sorted({k.split("__")[0] for k in d.files}):
+        o, y, (c, lg) = d[nm + "__outputs"], d[nm + "__labels"], d[nm + "__meta"]
+        ot, yt = torch.from_numpy(o).cuda(), torch.from_numpy(y).cuda()
+        per = np.array([M.calculate_ece(ot, yt, k, logits=bool(lg)) for k in range(c)])
+        assert np.abs(per - d[nm + "__per_class"]).max() <= 1e-7, nm
+        assert abs(M.calculate_average_ece(ot, yt, int(c), logits=bool(lg)) - d[nm + "__average"][0]) <= 1e-7, nm

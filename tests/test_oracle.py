@@ -120,3 +120,40 @@ def test_c_oracle_matches_python_oracle_random_graphs():
             S, H = C.graph_wavelet_features(g.indptr, g.indices, g.values, X0, k, 0.8, threads=th)
             np.testing.assert_array_equal(S, ref["S"])
             np.testing.assert_allclose(H, ref["H"], rtol=1e-14, atol=1e-300)
+
+
+# ----------------------------------------------------------------- ECE (utils/ece.py:8-89), pinned to the reference
+def _ece_cases():
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "ece_cases.npz"))
+    return d, sorted({k.split("__")[0] for k in d.files})
+
+
+def test_ece_oracle_bitwise_vs_reference_fixtures():
+    """oracle/ece_oracle.py against the reference's own calculate_ece /
+    calculate_average_ece outputs (tools/gen_ece_golden.py imports
+    utils/ece.py itself): logits and probabilities, probabilities exactly 0
+    and on bin edges, bins with < 4 samples, empty classes -- bit for bit."""
+    from oracle import ece_oracle as E
+    d, names = _ece_cases()
+    assert len(names) >= 10
+    for nm in names:
+        o, y, (c, lg) = d[nm + "__outputs"], d[nm + "__labels"], d[nm + "__meta"]
+        per = np.array([E.calculate_ece(o, y, k, logits=bool(lg)) for k in range(c)])
+        np.testing.assert_array_equal(per, d[nm + "__per_class"], err_msg=nm)
+        assert E.calculate_average_ece(o, y, int(c), logits=bool(lg)) == d[nm + "__average"][0], nm
+
+
+def test_ece_metrics_cpu_vs_reference_fixtures():
+    """wats_hip.metrics (torch, float64 bins) on CPU tensors against the
+    reference's outputs: within 1e-7 absolute (the reference averages float32
+    probabilities in float32; the bin assignment is identical)."""
+    import torch
+    from wats_hip import metrics as M
+    d, names = _ece_cases()
+    for nm in names:
+        o, y, (c, lg) = d[nm + "__outputs"], d[nm + "__labels"], d[nm + "__meta"]
+        ot, yt = torch.from_numpy(o), torch.from_numpy(y)
+        per = np.array([M.calculate_ece(ot, yt, k, logits=bool(lg)) for k in range(c)])
+        assert np.abs(per - d[nm + "__per_class"]).max() <= 1e-7, nm
+        assert abs(M.calculate_average_ece(ot, yt, int(c), logits=bool(lg)) - d[nm + "__average"][0]) <= 1e-7, nm
