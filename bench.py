@@ -77,7 +77,7 @@ def parse():
                          "'auto': the committed PMC summary of the default workload (profiles/r02/s12_traffic.json, "
                          "tools/r02_traffic.sh) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    ap.add_argument("--sharded-extra", default="reddit-f41,reddit,rmat-8m",
+    ap.add_argument("--sharded-extra", default="reddit-f41,reddit,rmat-8m,ogbn-arxiv",
                     help="comma-separated configs also measured row-sharded over all ranks (halo exchange), attached "
                          "as 'sharded' (first) and 'sharded_<config>' objects of the line; 'none' to skip.  At N > 1 "
                          "the --scale-config run is the headline and is not repeated here")
@@ -103,6 +103,8 @@ def parse():
                     help="also time the same graph with the F=1 log1p-degree signal (SURVEY 8(d) 'also report F=1')")
     ap.add_argument("--connected-companion", type=int, default=1,
                     help="N = 1: also time an arxiv-shaped graph without isolated rows (graphgen.connect_isolated)")
+    ap.add_argument("--pubmed-companion", type=int, default=1,
+                    help="N = 1: also time the PubMed-size K=16 F=1 chain (BASELINE configs[1], launch-bound)")
     ap.add_argument("--replicas", type=int, default=1,
                     help="N > 1: also time one independent arxiv-size graph per rank (no collective) as 'replicas'")
     ap.add_argument("--mode", default="auto", choices=["auto", "graphs", "sharded"],
@@ -137,7 +139,9 @@ def _byte_model(info) -> str:
     return "lds (16-bit ids, no values; DESIGN.md 4.4)"
 
 
-def lds_kernel_name(info) -> str:
+def lds_kernel_name(info, chain1: bool = False) -> str:
+    if chain1:
+        return "cheb_chain1_kernel (the whole chain in one launch; per-step time = launch / K)"
     if not info:
         return "cheb_step_kernel"
     return {1: "cheb_lds1_kernel", 2: "cheb_lds3_kernel + combine_lds2_kernel",
@@ -384,6 +388,56 @@ def _check_vs_unsharded(sw, indptr_d, indices_d, n, r0, r1, F, K, s_heat, world,
                     "the same GPU; max over ranks and columns of max|dS| / max|S|"}
 
 
+def one_gpu_chain(config, K, F, steps, seed, s_heat, device) -> dict:
+    """The N > 1 headline's workload unsharded on ONE GPU (every rank runs it on
+    its own device, no collective; rank 0's is reported): the same graph
+    (GPU generator, same seed), K, F and s through wg_wavelet_features, so the
+    row-sharded curve can be read against the same config's one-GPU chain
+    (VERDICT r2 item 6)."""
+    import wats_hip
+    from wats_hip import NormalizedLaplacian
+    from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
+    n_t, nnz_t, K_def, F_def = NAMED_CONFIGS[config]
+    K = K if K is not None else K_def
+    F = F if F is not None else F_def
+    ip, ix = rmat_graph_device(n_t, nnz_t, seed=seed, device=device)
+    L = NormalizedLaplacian(n_t, ip, ix, device=device)
+    del ip, ix
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1)
+    X = L.log1p_degree() if F == 1 else torch.randn(n_t, F, generator=gen, device=device)
+    S = torch.empty(n_t, F, device=device)
+    H = torch.empty(n_t, F, device=device)
+    lib = wats_hip._lib.load()
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def run():
+        wats_hip._lib.check(lib.wg_wavelet_features(L.handle, X.data_ptr(), F, K, s_heat, S.data_ptr(),
+                                                    H.data_ptr(), stream), "wavelet_features")
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize(device)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    evs[0].record()
+    for i in range(steps):
+        run()
+        evs[i + 1].record()
+    torch.cuda.synchronize(device)
+    per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    total = evs[0].elapsed_time(evs[-1])
+    plan = [ln for ln in L.describe(F).splitlines() if ln.startswith("tiles:")]
+    nnz = L.nnz
+    L.close()
+    del S, H, X
+    torch.cuda.empty_cache()
+    return {"config": config, "K": K, "F": F, "nnz": nnz, "steps": steps, "ms_per_step": total / steps,
+            "median_step_ms": per[len(per) // 2], "value": float(nnz) * K * steps / (total * 1e-3),
+            "unit": "edges*K/s", "hybrid_step": bool(plan),
+            "what": "the same graph / K / F unsharded through wg_wavelet_features on one GPU (HIP events over "
+                    "the chains; each rank on its own device, rank 0 reported): divide the headline's value by "
+                    "this value for the row-sharded speed-up on the same config"}
+
+
 # ----------------------------------------------------------------------------- single-GPU measurement
 def cold_chains(step, L, reps, device):
     """SURVEY.md 8(d) 'cold' protocol: before each timed pass, write a 512 MiB
@@ -564,6 +618,9 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
         edges_k = _allreduce(edges_k, dist.ReduceOp.SUM, device)
     avg_ms = prof["sum_ms"] / max(1, prof["launches"])
+    one_launch_chain = F == 1 and "chain1:" in L.describe(1)
+    if one_launch_chain:   # csrc/chain.hip: one launch runs all K steps: per step = / K
+        avg_ms /= K
     # the step kernel processes the rows that enter the chain; purely
     # isolated rows (closed form T_k = (-1)^k X0) are handled by finalize
     n_active = n - int(L.info["n_closed_form"])
@@ -573,6 +630,9 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
     # roofline.achieved: SURVEY 8(d)'s per-row / per-nonzero figure x the rows and nonzeros one launch
     # processes (the contract); the bytes this kernel's own algorithm needs are reported beside it.
     # (F == 1 LDS formats: their own model -- SURVEY's 8 B/nnz would read above 1.0)
+    if one_launch_chain:   # chain.hip reads neither the LDS plan's format nor values: SURVEY 8(d) / Clenshaw-u bytes
+        lds_info = None
+        b_step = clenshaw_bytes(n_active, nnz, F, unit)
     b_roof = b_step if lds_info else b_8d
     achieved = b_roof / (avg_ms * 1e-3) / 1e9
     traffic, traffic_src = None, None
@@ -615,7 +675,7 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
             "traffic_source": (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction: "
                                f"an upper bound) + WRITE_SIZE per launch of this kernel on this workload"
                                if traffic is not None else None),
-            "kernel": lds_kernel_name(lds_info),
+            "kernel": lds_kernel_name(lds_info, one_launch_chain),
             "byte_model": _byte_model(lds_info) if lds_info else
                           "SURVEY 8(d): 8 B/nnz + 4(N+1) + 20 N F over the launched rows",
             "algorithmic_bytes_per_launch": b_roof,
@@ -672,7 +732,8 @@ def _companion_summary(d: dict) -> dict:
     out = {k: d[k] for k in keep if k in d}
     r = d.get("roofline", {})
     out["roofline"] = {k: r.get(k) for k in ("achieved", "frac", "kernel_bytes_frac", "all_rows_frac",
-                                             "avg_launch_us", "rows_per_launch", "closed_form_rows")}
+                                             "avg_launch_us", "rows_per_launch", "closed_form_rows",
+                                             "algorithmic_bytes_per_launch", "kernel")}
     return out
 
 
@@ -696,6 +757,10 @@ def main():
             else:
                 dist.init_process_group(backend)
             dist.barrier()
+            # a CPU group created up front: per-rank failure flags are agreed over it before any
+            # rank changes course, so no rank starts another collective alone
+            global _CPU_GROUP
+            _CPU_GROUP = dist.new_group(backend="gloo")
     mode = args.mode if args.mode != "auto" else ("graphs" if world == 1 else "sharded")
     exchanges = [x for x in args.exchange.split(",") if x]
     from wats_hip.graphgen import NAMED_CONFIGS, connect_isolated, named_graph
@@ -720,12 +785,17 @@ def main():
         hw = threading.Timer(args.headline_timeout, _expire_headline)
         hw.daemon = True
         hw.start()
+        exc = None
         try:
             line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
                                exchanges[0], median_reps=max(20, args.steps), halo_tiers=args.halo_tiers)
-        except Exception as exc:  # noqa: BLE001 -- keep a headline: the next exchange, noted in the line
+        except Exception as e:  # noqa: BLE001 -- keep a headline: the next exchange, noted in the line
+            exc = e
+        if _any_rank(exc is not None, world):   # every rank switches together, or none does
+            if exc is None:
+                exc = RuntimeError(f"the {exchanges[0]} headline failed on another rank")
             if len(exchanges) < 2:
-                raise
+                raise exc
             _log(f"headline with exchange {exchanges[0]} failed ({type(exc).__name__}: {exc}); using {exchanges[1]}")
             torch.cuda.empty_cache()
             line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
@@ -755,6 +825,8 @@ def main():
             except Exception as exc:  # noqa: BLE001
                 alt = {"error": f"{type(exc).__name__}: {exc}", "exchange": exchanges[1]}
             pw.cancel()
+            if _any_rank("error" in alt, world) and "error" not in alt:   # failed elsewhere: same choice everywhere
+                alt = {"error": f"exchange {exchanges[1]} failed on another rank", "exchange": exchanges[1]}
 
             def _ok(r):
                 return r.get("value") is not None and bool((r.get("check") or {}).get("ok"))
@@ -775,7 +847,14 @@ def main():
         line["metric"] = (f"Chebyshev SpMM-chain edges*K/s ({cfg}-size, K={line['config']['K']}, F="
                           f"{line['config']['F']}, row-sharded over {world} GPUs)")
         line["headline_note"] = ("N > 1 headline: BASELINE.json configs[3] (Reddit-size, 1-D row-sharded, RCCL "
-                                 "halo exchange); the N = 1 line carries the same run at one rank as `sharded`")
+                                 "halo exchange); the N = 1 line carries the same run at one rank as `sharded`; "
+                                 "same_config_1gpu: the same config unsharded on one GPU")
+        try:
+            torch.cuda.empty_cache()
+            line["same_config_1gpu"] = one_gpu_chain(cfg, args.K, args.F, args.steps, args.seed, args.s, device)
+            line["same_config_1gpu"]["speedup"] = line["value"] / line["same_config_1gpu"]["value"]
+        except Exception as exc:  # noqa: BLE001
+            line["same_config_1gpu"] = {"error": f"{type(exc).__name__}: {exc}"}
     else:
         n_target, nnz_target, K_def, F_def = NAMED_CONFIGS[args.config]
         K = args.K if args.K is not None else K_def
@@ -791,6 +870,22 @@ def main():
             line["connected_companion"]["what"] = ("the same R-MAT graph with every isolated node attached to one "
                                                    "random node (graphgen.connect_isolated): no closed-form rows, "
                                                    "as the real ogbn-arxiv")
+        if world == 1 and args.pubmed_companion and args.config == "ogbn-arxiv":
+            # BASELINE.json configs[1]: the small, launch-bound chain (replayed as a hipGraph)
+            a = argparse.Namespace(**vars(args))
+            a.cold_reps = 0
+            a.settle_s = 0.1
+            pk, pf = NAMED_CONFIGS["pubmed"][2], NAMED_CONFIGS["pubmed"][3]
+            pm = _companion_summary(single_gpu_line(a, named_graph("pubmed", seed=args.seed), "pubmed", pk, pf,
+                                                    world, rank, device, full=False))
+            chain_s = pm["ms_per_step"] * 1e-3
+            b = pm["roofline"]["algorithmic_bytes_per_launch"]
+            pm["chain_us"] = chain_s * 1e6
+            pm["chain_frac"] = pk * b / chain_s / (HBM_PEAK_GBS * 1e9)
+            pm["roofline_chain_us"] = pk * b / (HBM_PEAK_GBS * 1e9) * 1e6
+            pm["what"] = ("PubMed-size R-MAT, K=16, the reference's F=1 signal: one whole chain per step (permute, 16 "
+                          "steps, finalize), replayed as a hipGraph; chain_frac = K x B_step / chain time / 8 TB/s")
+            line["pubmed_companion"] = pm
         del g
 
     extras = [c for c in (args.sharded_extra or "none").split(",") if c and c != "none"]
@@ -883,6 +978,18 @@ def _log(msg: str) -> None:
     """Progress on stderr (rank-prefixed), so long multi-rank runs show where they are."""
     print(f"[bench rank {os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr,
           flush=True)
+
+
+_CPU_GROUP = None
+
+
+def _any_rank(flag: bool, world: int) -> bool:
+    """True on every rank if `flag` is true on any rank (over the CPU group)."""
+    if world <= 1:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_CPU_GROUP)
+    return bool(t.item())
 
 
 def _allreduce(x: float, op, device) -> float:

@@ -206,6 +206,19 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.tile_max = (int32_t)value;
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;
+  } else if (!strcmp(key, "chain")) {
+    if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "chain must be -1 (auto), 0 or 1");
+    L->tune.chain = (int32_t)value;
+  } else if (!strcmp(key, "chain_wg")) {
+    if (value < 0 || value > 64) return fail(WG_ERR_INVALID, "chain_wg must be in [0 (auto), 64]");
+    L->tune.chain_wg = (int32_t)value;
+  } else if (!strcmp(key, "chain_xcd")) {
+    L->tune.chain_xcd = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "graph")) {
+    if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "graph must be -1 (auto), 0 or 1");
+    L->tune.graph = (int32_t)value;
+    return WG_OK;  // launch-time choice (tune_gen: a captured chain is re-captured)
   } else {
     return fail(WG_ERR_INVALID, "wg_laplacian_tune: unknown key '%s'", key);
   }
@@ -213,6 +226,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   for (auto& kv : L->plans) kv.second.release();
   L->plans.clear();
   release_lds1(L);
+  release_chain1(L);
   return WG_OK;
 }
 
@@ -247,6 +261,7 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
   if (F == 1) {
     Lds1Plan* lp = nullptr;
     if (!get_lds1_plan(L, true, &lp) && lp) g_text += lp->text;
+    if (L->chain1) g_text += L->chain1->text;  // once a chain has built it
   }
   return g_text.c_str();
 }
@@ -320,15 +335,31 @@ int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float*
   return launch_permute(L, direction, F, src, dst, as_stream(stream_));
 }
 
-int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s, float* S, float* H,
-                        void* stream_) {
-  if (!L || F < 1 || K < 0 || (!S && !H) || (L->n_rows && !X0))
-    return fail(WG_ERR_INVALID, "wg_wavelet_features: bad arguments (F=%lld K=%d)", (long long)F, K);
-  if (L->n_cols != L->n_rows)
-    return fail(WG_ERR_INVALID, "wg_wavelet_features: sharded handle (halo columns); use wg_cheb_step");
-  hipStream_t stream = as_stream(stream_);
+}  // extern "C"
+
+namespace wg {
+
+void ChainGraph::release() {
+  if (exec) (void)hipGraphExecDestroy(exec);
+  if (fork) (void)hipEventDestroy(fork);
+  if (join) (void)hipEventDestroy(join);
+  if (cap) (void)hipStreamDestroy(cap);
+  *this = ChainGraph{};
+}
+
+namespace {
+
+// The whole graph_wavelet_features chain (WATS.py:39-74) enqueued on `stream`: permute in, K
+// Chebyshev / Clenshaw steps, finalize.  Eager, or recorded into a hipGraph by the caller.
+int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s, float* S, float* H,
+                  hipStream_t stream) {
   const int64_t n = L->n_rows;
-  if (n == 0) return WG_OK;
+  // small unweighted graphs, F == 1: the whole chain in one launch (chain.hip)
+  if (F == 1 && K >= 1 && S && H) {
+    ChainPlan* cp = nullptr;
+    if (int rc0 = get_chain1_plan(L, F, K, &cp)) return rc0;
+    if (cp) return launch_chain1(L, cp, X0, K, s, S, H, stream);
+  }
   // F == 1 on an unweighted graph: the column-blocked LDS kernel (lds1.hip)
   Lds1Plan* lp = nullptr;
   if (F == 1 && K >= 1) {
@@ -439,6 +470,96 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   }
   if (fuse_fin) return WG_OK;
   return launch_finalize(L, F, sint, b0, coef, S, H, stream, Fp);
+}
+
+}  // namespace
+}  // namespace wg
+
+extern "C" {
+
+int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s, float* S, float* H,
+                        void* stream_) {
+  if (!L || F < 1 || K < 0 || (!S && !H) || (L->n_rows && !X0))
+    return fail(WG_ERR_INVALID, "wg_wavelet_features: bad arguments (F=%lld K=%d)", (long long)F, K);
+  if (L->n_cols != L->n_rows)
+    return fail(WG_ERR_INVALID, "wg_wavelet_features: sharded handle (halo columns); use wg_cheb_step");
+  hipStream_t stream = as_stream(stream_);
+  if (L->n_rows == 0) return WG_OK;
+  if (L->warm_gen != L->tune_gen) {  // a tune drops plans: every width builds again
+    L->warm_widths.clear();
+    L->warm_gen = L->tune_gen;
+  }
+  const bool warmed = std::find(L->warm_widths.begin(), L->warm_widths.end(), F) != L->warm_widths.end();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  WG_HIP_TRY(hipStreamIsCapturing(stream, &cs));
+  if (cs != hipStreamCaptureStatusNone) {
+    // the caller records the chain into its own graph: only widths whose plans and workspace
+    // exist (plan building copies to the host and workspace growth synchronises)
+    if (!warmed)
+      return fail(WG_ERR_UNSUPPORTED,
+                  "wg_wavelet_features: the first call with F=%lld builds its plans and workspace synchronously; "
+                  "call it once on an uncaptured stream before capturing",
+                  (long long)F);
+    return wavelet_chain(L, X0, F, K, s, S, H, stream);
+  }
+  // small chains are launch-bound (PubMed-size: 19 launches of a few us): replay them as a hipGraph
+  const int64_t work = std::max<int64_t>(L->nnz, 1) * padded_features(L, F);
+  const bool use_graph = L->tune.graph == 1 || (L->tune.graph < 0 && work <= ((int64_t)1 << 22));
+  if (!use_graph || L->prof || !warmed) {
+    const int rc = wavelet_chain(L, X0, F, K, s, S, H, stream);
+    if (!rc && !warmed) L->warm_widths.push_back(F);
+    return rc;
+  }
+  ChainGraph& g = L->chain;
+  if (g.x0 != X0 || g.S != S || g.H != H || g.ws != L->ws || g.F != F || g.K != K || g.s != s ||
+      g.gen != L->tune_gen) {
+    if (g.exec) {
+      WG_HIP_TRY(hipStreamSynchronize(g.cap));
+      (void)hipGraphExecDestroy(g.exec);
+      g.exec = nullptr;
+    }
+    g.x0 = X0; g.S = S; g.H = H; g.ws = L->ws; g.F = F; g.K = K; g.s = s; g.gen = L->tune_gen;
+    g.warm = 0;
+  }
+  if (!g.exec && g.warm < 2) {  // capture only arguments seen twice in a row (not alternating buffers)
+    const int rc = wavelet_chain(L, X0, F, K, s, S, H, stream);
+    if (!rc) ++g.warm;
+    return rc;
+  }
+  if (!g.cap) {
+    WG_HIP_TRY(hipStreamCreateWithFlags(&g.cap, hipStreamNonBlocking));
+    WG_HIP_TRY(hipEventCreateWithFlags(&g.fork, hipEventDisableTiming));
+    WG_HIP_TRY(hipEventCreateWithFlags(&g.join, hipEventDisableTiming));
+  }
+  // the chain runs on the handle's stream, joined to the caller's on both sides
+  WG_HIP_TRY(hipEventRecord(g.fork, stream));
+  WG_HIP_TRY(hipStreamWaitEvent(g.cap, g.fork, 0));
+  if (!g.exec) {
+    hipGraph_t gr = nullptr;
+    WG_HIP_TRY(hipStreamBeginCapture(g.cap, hipStreamCaptureModeRelaxed));
+    const int rc = wavelet_chain(L, X0, F, K, s, S, H, g.cap);
+    const hipError_t ec = hipStreamEndCapture(g.cap, &gr);
+    if (rc) {
+      if (gr) (void)hipGraphDestroy(gr);
+      return rc;
+    }
+    if (ec != hipSuccess) return fail(WG_ERR_HIP, "wg_wavelet_features: capture failed: %s", hipGetErrorString(ec));
+    const hipError_t ei = hipGraphInstantiate(&g.exec, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (ei != hipSuccess) {
+      g.exec = nullptr;
+      return fail(WG_ERR_HIP, "wg_wavelet_features: graph instantiate: %s", hipGetErrorString(ei));
+    }
+  }
+  WG_HIP_TRY(hipGraphLaunch(g.exec, g.cap));
+  WG_HIP_TRY(hipEventRecord(g.join, g.cap));
+  WG_HIP_TRY(hipStreamWaitEvent(stream, g.join, 0));
+  return WG_OK;
+}
+
+int wg_chain_status(wg_laplacian_t L, int32_t* timed_out) {
+  if (!L || !timed_out) return fail(WG_ERR_INVALID, "wg_chain_status: NULL argument");
+  return chain1_status(L, timed_out);
 }
 
 int wg_profile_enable(wg_laplacian_t L, int32_t enable) {

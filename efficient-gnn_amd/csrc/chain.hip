@@ -1,0 +1,480 @@
+// chain.hip -- the whole Chebyshev chain of a small graph in ONE launch
+// (reference calibration/WATS.py:29-37 recurrence, heat sum :65-68 by
+// Clenshaw's recurrence, row-L1 normalisation :71-72), F == 1 on unweighted
+// graphs: SURVEY.md 7.5's "persistent kernel with a grid barrier for small
+// graphs" (VERDICT r2 item 7).
+//
+// Why.  A PubMed-size chain (9.1 k active rows, 88.6 k nonzeros, K = 16) moves
+// 1.2 MB per step; as K + 3 launches it is bound by the launch boundaries
+// (~5 us each eagerly; a hipGraph replay of the same launches measured slower
+// on this stack, +2.7 us per node: profiles/r03/s3_graph_probe.log).  Here P
+// workgroups (one per CU, 1024 threads) run every step:
+//
+//  * each worker owns a contiguous, cost-balanced range of internal rows; its
+//    rows' 16-bit column ids, row pointers, X0, dinv (sign = isolated flag) and
+//    previous u stay in LDS for the whole chain;
+//  * the gathered vector u = b * dinv (the value-free Clenshaw form of
+//    DESIGN.md 4.1) of ALL active rows is staged in LDS; each step sums
+//    u[col] over a row with a team of TS lanes (TS ~ row length / 4), float64;
+//  * a worker publishes its rows' new u as data-tagged 8-byte granules {u,
+//    tag = launch epoch * 64 + phase}, each ONE write-through (sc1) store; the
+//    next phase re-stages u by loading every granule (sc1) until its tag is the
+//    phase's -- no separate flag, counter or drain (MI355X_MICROARCH.md,
+//    handoff-1to1).  Two granule buffers alternate by phase: a worker can only
+//    write phase j+2's granules after every worker published phase j+1, i.e.
+//    finished staging phase j.  One worker (small graphs, ids and both u
+//    buffers in LDS) exchanges nothing: u alternates between two LDS buffers.
+//    A wait gives up after ~0.5 s and raises an error flag (never a hang).
+//
+// Numbers (Clenshaw, b_K = c_K X0 implicit, as dist.hip's phase loop):
+//   phase j = 1..K computes b_k, k = K - j:
+//     b_k = ck X0 + cacc (L_hat b_{k+1}) - [j >= 3] b_{k+2},
+//     cacc = j == 1 ? (k == 0 ? c_K : 2 c_K) : (k == 0 ? 1 : 2),  ck = c_k - [j == 2] c_K,
+//   L_hat b = -dinv_i sum_j u_j (- b_i on isolated rows); k = 0 gives S.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "internal.h"
+
+namespace wg {
+namespace {
+
+constexpr int kChainThreads = 1024;
+constexpr int kChainWaves = kChainThreads / 64;
+constexpr int kChainLds = 160 * 1024 - 64;  // dynamic LDS per worker
+
+struct ChainArgs {
+  int32_t n_act;
+  int32_t K;
+  int32_t P;
+  int32_t stride;             // workgroup b is worker b / stride when b % stride == 0 (XCD placement)
+  int32_t ustride;            // floats per exchange buffer
+  const uint16_t* ids;        // [nnz_act] column ids (row order)
+  const int4* wdesc;          // [P] {row0, row1, e0, e1}
+  const int32_t* wpass;       // [P][kChainWaves + 1] pass offsets of each worker's waves (into passes)
+  const int2* passes;         // one wave pass: {first row, rows | log2 team size << 8}
+  const int32_t* rowptr;      // internal row pointers
+  const double* dinv;
+  const uint8_t* iso;
+  const int32_t* perm;
+  const float* x0;            // [n_act] X0 in internal order
+  const float* u0;            // [n_act] u_0 = X0 * dinv (prologue)
+  uint64_t* gbuf;             // [2][ustride] tagged granules {float bits, tag << 32}
+  int32_t* bar;               // [2] error flag, [3] launch epoch (bumped by the prologue)
+  float* S;                   // caller order
+  float* H;
+  double c[kChainMaxK + 1];   // heat coefficients exp(-s k)
+};
+
+// LDS layout of one worker (byte offsets, 16-B aligned sections): u [, u2], dinv (double), X0,
+// previous u, row pointers, 16-bit ids, wave passes
+struct ChainLayout {
+  int64_t u2, dv, x0o, pu, lrp, id, pas, bytes;
+  __host__ __device__ ChainLayout(int64_t n_act, int64_t nr, int64_t ne, int64_t npass, bool single) {
+    auto al = [](int64_t x) { return (x + 15) & ~(int64_t)15; };
+    const int64_t ub = al(4 * n_act);
+    u2 = ub;
+    dv = single ? 2 * ub : ub;
+    x0o = al(dv + 16 * nr);  // dinv and its reciprocal
+    pu = al(x0o + 4 * nr);
+    lrp = al(pu + 4 * nr);
+    id = al(lrp + 4 * (nr + 1));
+    pas = al(id + 2 * ne);
+    bytes = al(pas + 8 * npass);
+  }
+};
+
+__device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// u[0, n) <- the granules of one phase (n <= kChainThreads * kStageMax): every element of the
+// thread in flight at once (one memory round trip when the producers are done), re-polled with
+// a short sleep until every tag is the phase's; false after ~0.5 s (a worker never published)
+constexpr int kStageMax = 24;
+#ifndef WG_CHAIN_SLEEP  // s_sleep units (64 cycles) between polls of granules not yet published
+#define WG_CHAIN_SLEEP 1
+#endif
+__device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, int n, uint32_t tag, int tid) {
+  uint32_t pending = 0;
+#pragma unroll
+  for (int q = 0; q < kStageMax; ++q)
+    if (tid + q * kChainThreads < n) pending |= 1u << q;
+  int spins = 0;
+  while (pending) {
+    uint64_t v[kStageMax];
+#pragma unroll
+    for (int q = 0; q < kStageMax; ++q) v[q] = (pending >> q) & 1 ? ld_sc1_u64(g + tid + q * kChainThreads) : 0ull;
+#pragma unroll
+    for (int q = 0; q < kStageMax; ++q) {
+      if (((pending >> q) & 1) && (uint32_t)(v[q] >> 32) == tag) {
+        u[tid + q * kChainThreads] = __uint_as_float((uint32_t)v[q]);
+        pending &= ~(1u << q);
+      }
+    }
+    if (pending) {
+      __builtin_amdgcn_s_sleep(WG_CHAIN_SLEEP);
+      if (++spins > (1 << 22)) return false;
+    }
+  }
+  return true;
+}
+
+// internal X0 of the active rows, u_0 = X0 * dinv into exchange buffer 0, and the
+// closed-form rows' S = coef * X0, H = S / (|S| + 1e-8) straight to the caller's rows
+__global__ void chain_prologue_kernel(int64_t n, int64_t n_act, const int32_t* __restrict__ perm,
+                                      const float* __restrict__ X0, const double* __restrict__ dinv, double coef,
+                                      float* __restrict__ x0int, float* __restrict__ u0, float* __restrict__ S,
+                                      float* __restrict__ H, int32_t* __restrict__ epoch) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row == 0) *epoch = *epoch + 1;  // read by the chain kernel after this launch (stream order)
+  if (row >= n) return;
+  const int32_t r = perm[row];
+  const float x = X0[r];
+  if (row < n_act) {
+    x0int[row] = x;
+    u0[row] = (float)((double)x * dinv[row]);
+  } else {
+    const double s = coef * (double)x;
+    S[r] = (float)s;
+    H[r] = (float)(s / (fabs(s) + 1e-8));
+  }
+}
+
+__global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a) {
+  if (blockIdx.x % a.stride) return;  // placement filler
+  const int w = blockIdx.x / a.stride;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int4 d = a.wdesc[w];
+  const int row0 = d.x, nr = d.y - d.x, e0 = d.z, ne = d.w - d.z;
+  const int32_t* wp = a.wpass + w * (kChainWaves + 1);
+  const int pass0 = wp[0], npass = wp[kChainWaves] - pass0;
+  const ChainLayout lay(a.n_act, nr, ne, npass, a.P == 1);
+  float* u = reinterpret_cast<float*>(smem);                         // [n_act] the gathered u
+  float* u2 = reinterpret_cast<float*>(smem + lay.u2);               // [n_act] one worker: the next u
+  double* dv = reinterpret_cast<double*>(smem + lay.dv);             // [nr] dinv, negative = isolated row
+  double* rdv = dv + nr;                                             // [nr] 1 / dinv
+  float* x0o = reinterpret_cast<float*>(smem + lay.x0o);             // [nr]
+  float* pu = reinterpret_cast<float*>(smem + lay.pu);               // [nr] previous u of own rows
+  int32_t* lrp = reinterpret_cast<int32_t*>(smem + lay.lrp);         // [nr + 1]
+  uint16_t* id = reinterpret_cast<uint16_t*>(smem + lay.id);         // [ne]
+  int2* pas = reinterpret_cast<int2*>(smem + lay.pas);               // [npass] the worker's wave passes
+  const uint32_t ep = (uint32_t)a.bar[3] & 0x3ffffffu;             // this launch's epoch (tags ep * 64 + j)
+  // ---- stage the worker's rows, its pass table and u_0
+  for (int i = tid; i < nr; i += kChainThreads) {
+    const double di = a.dinv[row0 + i];
+    dv[i] = a.iso[row0 + i] ? -di : di;
+    rdv[i] = 1.0 / di;
+    x0o[i] = a.x0[row0 + i];
+    lrp[i] = a.rowptr[row0 + i] - e0;
+  }
+  if (tid == 0) lrp[nr] = ne;
+  for (int i = tid; i < ne; i += kChainThreads) id[i] = a.ids[e0 + i];
+  for (int i = tid; i < npass; i += kChainThreads) pas[i] = a.passes[pass0 + i];
+  for (int i = tid; i < a.n_act; i += kChainThreads) u[i] = a.u0[i];
+  __syncthreads();
+#ifdef WG_CHAIN_TRACE  // timing build: worker 0 prints its phase timeline (s_memtime cycles)
+  long long tr[2 * kChainMaxK + 4];
+  int ntr = 0;
+  tr[ntr++] = clock64();
+#endif
+  const int wave = tid >> 6, lane = tid & 63;
+  const int pb = wp[wave] - pass0, pe = wp[wave + 1] - pass0;  // this wave's passes (no workgroup sync inside a phase)
+  const int K = a.K;
+  for (int j = 1; j <= K; ++j) {
+    const int k = K - j;
+    const double cacc = (j == 1) ? (k == 0 ? a.c[K] : 2.0 * a.c[K]) : (k == 0 ? 1.0 : 2.0);
+    const double ck = a.c[k] - (j == 2 ? a.c[K] : 0.0);
+    const bool prevs = j >= 3;
+    const uint64_t tag = (uint64_t)((ep << 6) | (uint32_t)j) << 32;
+    uint64_t* gnext = a.gbuf + (size_t)(j & 1) * a.ustride;
+    for (int pi = pb; pi < pe; ++pi) {
+      const int2 P = pas[pi];
+      const int lts = P.y >> 8;
+      const int TS = 1 << lts;
+      const int team = lane >> lts;
+      const int tl = lane & (TS - 1);
+      {
+        const int row = P.x + team;
+        const bool act = team < (P.y & 0xff);
+        const int li = row - row0;
+        double s = 0.0;
+        if (act) {  // four independent LDS chains per lane (the phase is latency-bound)
+          const int b = lrp[li], e = lrp[li + 1];
+          double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+          int q = b + tl;
+          for (; q + 3 * TS < e; q += 4 * TS) {
+            const int i0 = id[q], i1 = id[q + TS], i2 = id[q + 2 * TS], i3 = id[q + 3 * TS];
+            s += (double)u[i0];
+            s1 += (double)u[i1];
+            s2 += (double)u[i2];
+            s3 += (double)u[i3];
+          }
+          for (; q < e; q += TS) s += (double)u[id[q]];
+          s = (s + s1) + (s2 + s3);
+        }
+        for (int off = TS >> 1; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (act && tl == 0) {
+          const double dsi = dv[li];
+          const double di = fabs(dsi);
+          const double rdi = rdv[li];  // 1 / dinv
+          const float ui = u[row];
+          double lb = -di * s;
+          if (dsi < 0.0) lb -= (double)ui * rdi;  // isolated row: L_hat_ii = -1 (ui / di = b_i)
+          const double t = ck * (double)x0o[li] + cacc * lb - (prevs ? (double)pu[li] * rdi : 0.0);
+          if (k > 0) {
+            pu[li] = ui;  // b_{k+1} (as u): the next phase's b_{k+2}
+            const float un = (float)(t * di);
+            if (a.P == 1) u2[row] = un;
+            else __hip_atomic_store(gnext + row, tag | __float_as_uint(un), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            const int32_t r = a.perm[row];
+            a.S[r] = (float)t;
+            a.H[r] = (float)(t / (fabs(t) + 1e-8));
+          }
+        }
+      }
+    }
+#ifdef WG_CHAIN_TRACE
+    __syncthreads();
+    tr[ntr++] = clock64();
+#endif
+    if (k == 0) break;
+    __syncthreads();  // every gather of this phase is done with u
+    if (a.P == 1) {
+      float* t = u;
+      u = u2;
+      u2 = t;
+    } else if (!stage_tagged(u, gnext, a.n_act, (uint32_t)(tag >> 32), tid)) {
+      __hip_atomic_store(a.bar + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // results invalid
+    }
+    __syncthreads();
+#ifdef WG_CHAIN_TRACE
+    tr[ntr++] = clock64();
+#endif
+  }
+#ifdef WG_CHAIN_TRACE
+  if (w == 0 && tid == 0) {
+    printf("chain1 trace P=%d n_act=%d rows=%d entries=%d passes(wave0)=%d: staged at %lld\n", a.P, a.n_act, nr, ne,
+           pe - pb, tr[0]);
+    for (int i = 1; i < ntr; ++i) printf("  +%lld", tr[i] - tr[i - 1]);
+    printf("\n");
+  }
+#endif
+}
+
+template <typename T>
+int upload(T** d, const std::vector<T>& h) {
+  if (int rc = dmalloc(d, h.size())) return rc;
+  if (!h.empty()) WG_HIP_TRY(hipMemcpy(*d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  return WG_OK;
+}
+
+// rows r0..r1 (descending length) as wave passes: runs of rows sharing a team size TS (~4
+// entries per lane, at most 64 lanes), 64 / TS rows per pass
+void make_passes(const std::vector<int32_t>& rp, int64_t r0, int64_t r1, std::vector<int2>& out,
+                 std::vector<int64_t>& cost) {
+  int64_t r = r0;
+  while (r < r1) {
+    const int64_t len = rp[r + 1] - rp[r];
+    int lts = 0;
+    while (lts < 6 && ((int64_t)4 << lts) < len) ++lts;
+    const int64_t rows = std::min<int64_t>(64 >> lts, r1 - r);
+    int64_t n = 0;
+    while (n < rows) {  // the same team size for every row of the pass (lengths only decrease)
+      const int64_t l = rp[r + n + 1] - rp[r + n];
+      int t = 0;
+      while (t < 6 && ((int64_t)4 << t) < l) ++t;
+      if (t != lts) break;
+      ++n;
+    }
+    out.push_back(int2{(int)r, (int)n | (lts << 8)});
+    cost.push_back((len + (1 << lts) - 1) / (1 << lts) + 8);  // the longest lane's entries + an epilogue
+    r += n;
+  }
+}
+
+int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
+  const int64_t na = L->n_active;
+  std::vector<int32_t> rp(na + 1);
+  WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (na + 1), hipMemcpyDeviceToHost));
+  const int64_t nnz = rp[na];
+  std::vector<int32_t> col(std::max<int64_t>(nnz, 1));
+  if (nnz) WG_HIP_TRY(hipMemcpy(col.data(), L->col, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+  std::vector<uint16_t> ids(std::max<int64_t>(nnz, 1));
+  for (int64_t e = 0; e < nnz; ++e) {
+    if (col[e] < 0 || col[e] >= na) return fail(WG_ERR_INVALID, "chain plan: column %d outside the active rows", col[e]);
+    ids[e] = (uint16_t)col[e];
+  }
+  // workers: contiguous row ranges of equal cost (entries + an epilogue weight per row); per worker,
+  // wave passes dealt to its 16 waves by longest-first greedy balance
+  const int64_t kRowCost = 4;
+  const int64_t total = nnz + kRowCost * na;
+  // one worker when its ids, passes and both u buffers fit LDS (no exchange at all), else chain_wg
+  int P = L->tune.chain_wg > 0 ? L->tune.chain_wg : 1;
+  static_assert(24576 <= kChainThreads * kStageMax, "active rows per staging thread");
+  std::vector<int4> wd;
+  std::vector<int2> passes;
+  std::vector<int32_t> wpass;
+  size_t lds = 0;
+  for (;; P = (P == 1 && L->tune.chain_wg <= 0) ? 32 : 2 * P) {
+    if (P > 64) return WG_ERR_UNSUPPORTED;
+    wd.assign(P, int4{0, 0, 0, 0});
+    passes.clear();
+    wpass.assign((size_t)P * (kChainWaves + 1), 0);
+    lds = 0;
+    int64_t r = 0;
+    bool fits = true;
+    for (int w = 0; w < P && fits; ++w) {
+      const int64_t goal = total * (w + 1) / P;
+      const int64_t r0 = r;
+      while (r < na && (w == P - 1 || rp[r] + kRowCost * r < goal)) ++r;
+      wd[w] = int4{(int)r0, (int)r, rp[r0], rp[r]};
+      std::vector<int2> wps;
+      std::vector<int64_t> cost;
+      make_passes(rp, r0, r, wps, cost);
+      std::vector<int> order(wps.size());
+      for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+      std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return cost[x] > cost[y]; });
+      std::vector<int64_t> load(kChainWaves, 0);
+      std::vector<std::vector<int2>> per(kChainWaves);
+      for (int i : order) {
+        const int v = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[v] += cost[i];
+        per[v].push_back(wps[i]);
+      }
+      for (int v = 0; v < kChainWaves; ++v) {
+        wpass[(size_t)w * (kChainWaves + 1) + v] = (int32_t)passes.size();
+        passes.insert(passes.end(), per[v].begin(), per[v].end());
+      }
+      wpass[(size_t)w * (kChainWaves + 1) + kChainWaves] = (int32_t)passes.size();
+      const ChainLayout lay(na, r - r0, rp[r] - rp[r0], (int64_t)wps.size(), P == 1);
+      lds = std::max(lds, (size_t)lay.bytes);
+      if (lay.bytes > kChainLds) fits = false;
+    }
+    if (fits) break;
+  }
+  p->P = P;
+  p->n_act = (int32_t)na;
+  p->lds_bytes = (int32_t)((lds + 15) / 16 * 16);
+  p->ustride = (int32_t)((na + 63) / 64 * 64);
+  int rc = upload(&p->ids, ids);
+  if (!rc) rc = upload(&p->wdesc, wd);
+  if (!rc) rc = upload(&p->wpass, wpass);
+  if (!rc) rc = upload(&p->passes, passes);
+  if (!rc) rc = dmalloc(&p->bar, 4);
+  if (!rc) rc = dmalloc(&p->gbuf, (size_t)2 * p->ustride);
+  if (!rc) rc = dmalloc(&p->u0, (size_t)std::max<int64_t>(na, 1));
+  if (!rc) rc = dmalloc(&p->x0, (size_t)std::max<int64_t>(na, 1));
+  if (rc) return rc;
+  WG_HIP_TRY(hipMemset(p->bar, 0, 4 * sizeof(int32_t)));
+  WG_HIP_TRY(hipMemset(p->gbuf, 0, 2 * p->ustride * sizeof(uint64_t)));  // tag 0: never a live phase's
+  char buf[192];
+  snprintf(buf, sizeof(buf), "chain1: one launch per chain, %d workers x %d threads, %lld active rows, %lld nonzeros, "
+           "%d wave passes, LDS %d B per worker\n", P, kChainThreads, (long long)na, (long long)nnz,
+           (int)passes.size(), p->lds_bytes);
+  p->text = buf;
+  return WG_OK;
+}
+
+}  // namespace
+
+void ChainPlan::release() {
+  for (void* q : {(void*)ids, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar, (void*)gbuf, (void*)u0,
+                  (void*)x0})
+    (void)hipFree(q);
+  *this = ChainPlan{};
+}
+
+void release_chain1(wg_laplacian_s* L) {
+  if (L->chain1) {
+    L->chain1->release();
+    delete L->chain1;
+    L->chain1 = nullptr;
+  }
+  L->chain1_failed = false;
+}
+
+int get_chain1_plan(wg_laplacian_s* L, int64_t F, int32_t K, ChainPlan** out) {
+  *out = nullptr;
+  const int64_t na = L->n_active;
+  // F = 1, unweighted (value-free u), relabelled (active rows first), u of every active row in
+  // LDS with 16-bit ids, launch-bound sizes (auto: <= 2^18 nonzeros), K within the argument block
+  if (F != 1 || K < 1 || K > kChainMaxK || !L->unit || !L->reordered || L->n_cols != L->n_rows || na < 1 ||
+      na > 24576 || L->tune.chain == 0 || (L->tune.chain < 0 && L->nnz > ((int64_t)1 << 18)) ||
+      L->tune.uscale == 0)
+    return WG_OK;
+  if (L->chain1_failed) return WG_OK;
+  if (!L->chain1) {
+    auto* p = new ChainPlan();
+    const int rc = build_chain_plan(L, p);
+    if (rc) {
+      p->release();
+      delete p;
+      if (rc != WG_ERR_UNSUPPORTED) return rc;
+      L->chain1_failed = true;
+      return WG_OK;
+    }
+    L->chain1 = p;
+  }
+  *out = L->chain1;
+  return WG_OK;
+}
+
+int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, double s, float* S, float* H,
+                  hipStream_t stream) {
+  const int64_t n = L->n_rows;
+  double coef = 0.0;  // closed-form rows: S = X0 * sum_k (-1)^k c_k
+  for (int32_t k = 0; k <= K; ++k) coef += ((k & 1) ? -1.0 : 1.0) * std::exp(-s * (double)k);
+  hipLaunchKernelGGL(chain_prologue_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, n,
+                     (int64_t)p->n_act, L->perm, X0, L->dinv, coef, p->x0, p->u0, S, H, p->bar + 3);
+  WG_LAUNCH_CHECK();
+  static bool attr_set = false;
+  if (!attr_set) {
+    WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_chain1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   kChainLds));
+    attr_set = true;
+  }
+  ChainArgs a{};
+  a.n_act = p->n_act;
+  a.K = K;
+  a.P = p->P;
+  a.stride = L->tune.chain_xcd ? 8 : 1;
+  a.ustride = p->ustride;
+  a.ids = p->ids;
+  a.wdesc = p->wdesc;
+  a.wpass = p->wpass;
+  a.passes = p->passes;
+  a.rowptr = L->rowptr;
+  a.dinv = L->dinv;
+  a.iso = L->iso;
+  a.perm = L->perm;
+  a.x0 = p->x0;
+  a.u0 = p->u0;
+  a.gbuf = p->gbuf;
+  a.bar = p->bar;
+  a.S = S;
+  a.H = H;
+  for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
+  if (int rc = prof_mark(L, stream, true)) return rc;
+  hipLaunchKernelGGL(cheb_chain1_kernel, dim3((unsigned)(p->P * a.stride)), dim3(kChainThreads), (size_t)p->lds_bytes,
+                     stream, a);
+  WG_LAUNCH_CHECK();
+  return prof_mark(L, stream, false);
+}
+
+int chain1_status(wg_laplacian_s* L, int32_t* timed_out) {
+  *timed_out = 0;
+  if (!L->chain1) return WG_OK;
+  int32_t h[4] = {0, 0, 0, 0};
+  WG_HIP_TRY(hipDeviceSynchronize());
+  WG_HIP_TRY(hipMemcpy(h, L->chain1->bar, sizeof(h), hipMemcpyDeviceToHost));
+  *timed_out = h[2];
+  return WG_OK;
+}
+
+}  // namespace wg

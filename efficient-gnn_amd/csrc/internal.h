@@ -209,6 +209,49 @@ struct Tuning {
   int32_t probe_tailwin = 0; // timing only (results wrong): the hybrid step's tail columns folded into 1/n of the columns
   int32_t xcd = 0;           // step kernel: XCD x runs the x-th contiguous eighth of the units
   int32_t tile_rg = 1;       // hybrid step, 128-row blocks: 16-row groups per wave (1: 8 waves, 2: 4 waves)
+  int32_t chain = -1;        // F == 1 small unweighted graphs: the whole chain in one launch (chain.hip); -1 = auto
+                             // (<= 2^18 nonzeros, <= 24576 active rows), 0 = off, 1 = whenever it applies
+  int32_t chain_wg = 0;      // chain.hip workers (workgroups of 1024 threads; doubled until a worker fits LDS);
+                             // 0 = auto: one when its ids and two u buffers fit LDS (no exchange), else 32
+  int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works)
+  int32_t graph = -1;        // wg_wavelet_features: replay the chain as a hipGraph from its 2nd call with the same
+                             // arguments; -1 = auto (small chains, launch-bound: active nnz x width <= 2^22)
+};
+
+// The whole F = 1 chain of a small unweighted graph in one launch (chain.hip): P workgroups,
+// each owning a cost-balanced range of active rows, u of every active row staged in LDS,
+// a device-counter barrier between phases
+constexpr int kChainMaxK = 64;
+struct ChainPlan {
+  int32_t P = 0, n_act = 0, lds_bytes = 0, ustride = 0;
+  uint16_t* ids = nullptr;    // device [nnz_active]: 16-bit column ids in row order
+  int4* wdesc = nullptr;      // device [P]: {row0, row1, e0, e1}
+  int32_t* wpass = nullptr;   // device [P][17]: each worker's waves' ranges of passes
+  int2* passes = nullptr;     // device: one wave pass {first row, rows | log2 team size << 8}
+  int32_t* bar = nullptr;     // device [4]: [2] error flag, [3] launch epoch
+  uint64_t* gbuf = nullptr;   // device [2][ustride]: tagged u granules {float bits, tag << 32}
+  float* u0 = nullptr;        // device [n_act]: u_0 = X0 * dinv
+  float* x0 = nullptr;        // device [n_act]: X0 in internal order
+  std::string text;
+  void release();
+};
+
+// wg_wavelet_features captured into a hipGraph (capi.hip): the launches of one chain, keyed by the
+// call's arguments, the tuning generation and the workspace they were recorded with
+struct ChainGraph {
+  const void* x0 = nullptr;
+  const void* S = nullptr;
+  const void* H = nullptr;
+  const void* ws = nullptr;
+  int64_t F = 0;
+  int32_t K = -1;
+  double s = 0.0;
+  int64_t gen = -1;
+  int warm = 0;                   // eager calls with this key (the first builds plans and the workspace)
+  hipGraphExec_t exec = nullptr;
+  hipStream_t cap = nullptr;      // the handle's own non-blocking stream (capture and replay)
+  hipEvent_t fork = nullptr, join = nullptr;
+  void release();
 };
 
 }  // namespace wg
@@ -253,6 +296,13 @@ struct wg_laplacian_s {
   // workspace for wg_wavelet_features
   float* ws = nullptr;
   size_t ws_floats = 0;
+  // widths F whose plans and workspace wg_wavelet_features has built (at tuning generation
+  // warm_gen): only those may run on a stream the caller is capturing
+  std::vector<int64_t> warm_widths;
+  int64_t warm_gen = -1;
+  wg::ChainGraph chain;  // small chains replayed as a hipGraph (tuning key "graph")
+  wg::ChainPlan* chain1 = nullptr;  // the one-launch F = 1 chain (chain.hip), lazily
+  bool chain1_failed = false;
   // live step-kernel timing (wg_profile_*)
   bool prof = false;
   std::vector<hipEvent_t> ev;  // pool of (start, stop) pairs
@@ -338,6 +388,12 @@ int side_stream(wg_laplacian_s* L);  // creates L->side and its fork / join even
 // u = x * dinv for rows [0, n) of an F-wide signal (in place allowed): the hybrid chain's first
 // step gathers u_0 = X0 * dinv value-free like every later step
 int launch_scale_rows(wg_laplacian_s* L, int64_t n, int64_t F, const float* x, float* u, hipStream_t stream);
+// chain.hip: the one-launch chain of a small graph (*out = nullptr: not applicable)
+int get_chain1_plan(wg_laplacian_s* L, int64_t F, int32_t K, ChainPlan** out);
+int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, double s, float* S, float* H,
+                  hipStream_t stream);
+void release_chain1(wg_laplacian_s* L);
+int chain1_status(wg_laplacian_s* L, int32_t* timed_out);
 // lds1.hip
 int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out);  // *out = nullptr: not applicable
 void release_lds1(wg_laplacian_s* L);

@@ -515,6 +515,8 @@ int sort_row_columns(wg_laplacian_s* L, hipStream_t stream) {
 using namespace wg;
 
 wg_laplacian_s::~wg_laplacian_s() {
+  chain.release();
+  wg::release_chain1(this);
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   for (auto& kv : plans) kv.second.release();
   wg::release_lds1(this);

@@ -251,6 +251,14 @@ class NormalizedLaplacian:
         """The step kernel's launch plan for an F-column signal."""
         return _lib.load().wg_laplacian_describe(self.handle, int(F)).decode()
 
+    def chain_status(self) -> bool:
+        """True if a one-launch chain (csrc/chain.hip) gave up a barrier wait
+        (its results are invalid); synchronous."""
+        out = ctypes.c_int32(0)
+        with torch.cuda.device(self.device):
+            check(_lib.load().wg_chain_status(self.handle, ctypes.byref(out)), "chain_status")
+        return bool(out.value)
+
     def profile_enable(self, enable: bool = True) -> None:
         """Record HIP events around each step launch of graph_wavelet_features."""
         check(_lib.load().wg_profile_enable(self.handle, 1 if enable else 0), "profile_enable")

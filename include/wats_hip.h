@@ -214,11 +214,26 @@ int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float*
  * F > 1 or weighted: the sum is evaluated by Clenshaw's recurrence (K SpMM
  * steps, no S stream; tuning key "clenshaw" 0 = forward recurrence).
  * X0, S, H in the caller's row order, row stride F.  S and H nullable (at
- * least one non-NULL).  K >= 0.  Uses the handle's workspace (grown on first
- * use for a given F -- call once untimed before capturing into a graph).
+ * least one non-NULL).  K >= 0.  Uses the handle's workspace.
+ * The FIRST call with a given F (after creation or a wg_laplacian_tune) builds
+ * the kernel plans and grows the workspace SYNCHRONOUSLY (host copies, device
+ * allocation): on a stream that is being captured it returns
+ * WG_ERR_UNSUPPORTED -- call it once uncaptured first; later calls are plain
+ * asynchronous launches and may be captured.
+ * Small (launch-bound) chains are replayed as a hipGraph of the handle's own
+ * once the same arguments (pointers, F, K, s) were seen on two calls in a row
+ * (tuning key "graph": -1 auto = active nnz x width <= 2^22, 0 off, 1 on).
  * ---------------------------------------------------------------------- */
 int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s,
                         float* S, float* H, void* stream);
+/* F == 1 on a small unweighted graph (<= 2^18 nonzeros, <= 24576 active rows;
+ * tuning key "chain": -1 auto, 0 off, 1 on, "chain_wg" workers) with S and H
+ * given, wg_wavelet_features runs the whole chain in ONE launch of P
+ * cooperating workgroups separated by a device-counter barrier per step
+ * (csrc/chain.hip).  A barrier wait gives up after ~0.5 s
+ * instead of hanging; wg_chain_status (synchronous) reports that in
+ * *timed_out_host (1 = a chain's results are invalid). */
+int wg_chain_status(wg_laplacian_t L, int32_t* timed_out_host);
 
 /* Tuning: key "iter" (team-mode nonzeros per lane sub-group; default by
  * shape), "chunk_iter" (chunk-mode nonzeros per sub-group),

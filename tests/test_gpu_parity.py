@@ -639,3 +639,114 @@ def test_device_ece_vs_reference_fixtures():
         per = np.array([M.calculate_ece(ot, yt, k, logits=bool(lg)) for k in range(c)])
         assert np.abs(per - d[nm + "__per_class"]).max() <= 1e-7, nm
         assert abs(M.calculate_average_ece(ot, yt, int(c), logits=bool(lg)) - d[nm + "__average"][0]) <= 1e-7, nm
+
+
+# ----------------------------------------------------------------- small chains as a hipGraph
+def _wf_call(L, X, S, H, K, s=0.8):
+    lib = wats_hip._lib.load()
+    wats_hip._lib.check(lib.wg_wavelet_features(L.handle, X.data_ptr(), X.shape[1], K, s, S.data_ptr(), H.data_ptr(),
+                                                torch.cuda.current_stream().cuda_stream), "wavelet_features")
+
+
+@pytest.mark.parametrize("F", [1, 8, 40])
+def test_chain_graph_replay_bitwise(F):
+    """wg_wavelet_features replayed as a hipGraph (tuning key graph = 1, the
+    auto choice for PubMed-size chains): bitwise equal to the eager chain over
+    repeated calls, picks up new signal contents behind the same pointer, and
+    matches the oracle (WATS.py:39-74)."""
+    g = rmat_graph(19717, 88648, seed=5)
+    rng = np.random.default_rng(F)
+    Xh = rng.standard_normal((g.n, F)).astype(np.float32)
+    outs = {}
+    for mode in (0, 1):
+        L = NormalizedLaplacian.from_graph(g)
+        L.tune(graph=mode)
+        X = torch.from_numpy(Xh).cuda()
+        S = torch.empty(g.n, F, device="cuda")
+        H = torch.empty(g.n, F, device="cuda")
+        res = []
+        for i in range(5):   # eager, eager, capture + replay, replay, replay
+            _wf_call(L, X, S, H, 16)
+            res.append((S.clone(), H.clone()))
+        X.mul_(-0.5)          # same pointer, new contents: a replay must read them
+        _wf_call(L, X, S, H, 16)
+        res.append((S.clone(), H.clone()))
+        torch.cuda.synchronize()
+        outs[mode] = res
+        L.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert all(torch.equal(r[0], outs[1][0][0]) for r in outs[1][:5])
+    ref = O.graph_wavelet_features(g.to_scipy(), k=16, s=0.8, X0=Xh, return_all=True)
+    assert_parity(outs[1][4][0].cpu().numpy(), ref["S"], what=f"graph replay F={F} S")
+    assert_parity(outs[1][5][0].cpu().numpy(), -0.5 * ref["S"], what=f"graph replay F={F} S (new X0)")
+
+
+def test_chain_under_torch_graph_capture():
+    """A caller may capture wg_wavelet_features into its own CUDA graph once
+    the width was run uncaptured (plans and workspace exist); the replayed
+    graph equals the eager chain."""
+    g = rmat_graph(3000, 30000, seed=2)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(graph=0)
+    X = torch.randn(g.n, 4, device="cuda")
+    S0, H0 = torch.empty(g.n, 4, device="cuda"), torch.empty(g.n, 4, device="cuda")
+    _wf_call(L, X, S0, H0, 8)     # uncaptured first call: builds plans and workspace
+    S, H = torch.empty_like(S0), torch.empty_like(H0)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    cg = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(cg, stream=side):
+            _wf_call(L, X, S, H, 8)
+    cg.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(S, S0) and torch.equal(H, H0)
+    L.close()
+
+
+# ----------------------------------------------------------------- the one-launch chain (chain.hip)
+@pytest.mark.parametrize("n,nnz,K,knobs", [(19717, 88648, 16, {}), (2708, 10556, 8, {}), (2708, 10556, 3, {"chain_wg": 1}),
+                                           (19717, 88648, 1, {}), (19717, 88648, 2, {"chain_wg": 3}),
+                                           (19717, 88648, 32, {"chain_wg": 16, "chain_xcd": 1}),
+                                           (6000, 150000, 16, {"chain_wg": 5})])
+def test_chain1_vs_oracle(n, nnz, K, knobs):
+    """F = 1 small graphs run the whole chain in one launch (P workers, a
+    device-counter barrier per step): PubMed-size K = 16 (the
+    BASELINE configs[1] workload) and Cora-size K = 8, K = 1 / 2 / 3 / 32
+    (every branch of the Clenshaw phase coefficients), 1 to 16 workers, XCD
+    placement, against the oracle with the reference signal and a random one,
+    repeated calls bitwise equal, no barrier timeout."""
+    g = rmat_graph(n, nnz, seed=K)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(**knobs)
+    rng = np.random.default_rng(n + K)
+    for X in (None, rng.standard_normal((g.n, 1)).astype(np.float32)):
+        Xt = None if X is None else torch.from_numpy(X)
+        H1, S1 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=Xt, return_S=True)
+        H2, S2 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=Xt, return_S=True)
+        torch.cuda.synchronize()
+        assert "chain1:" in L.describe(1), L.describe(1)
+        assert not L.chain_status(), "a chain barrier wait timed out"
+        assert torch.equal(S1, S2) and torch.equal(H1, H2)
+        X0 = L.log1p_degree().cpu().numpy() if X is None else X
+        ref = O.graph_wavelet_features(g.to_scipy(), k=K, s=0.8, X0=X0, return_all=True)
+        assert_parity(S1.cpu().numpy(), ref["S"], what=f"chain1 n={n} K={K} S")
+        big = np.abs(ref["S"]) > 1e-3 * np.abs(ref["S"]).max()
+        assert np.abs(H1.cpu().numpy()[big] - ref["H"][big]).max() <= 1e-5
+    L.tune(chain=0)   # the multi-launch path gives the same result to rounding
+    _, S0 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=Xt, return_S=True)
+    assert_parity(S1.cpu().numpy(), S0.cpu().numpy().astype(np.float64), what="chain1 vs multi-launch")
+    L.close()
+
+
+def test_chain1_golden_pubmed():
+    """The reference's own PubMed-size K=16 vectors (tests/golden), through the one-launch chain."""
+    d = load_golden("pubmed_rmat_k16")
+    A = golden_csr(d)
+    L = NormalizedLaplacian.from_scipy(A)
+    H, S = wats_hip.graph_wavelet_features(L, k=16, s=0.8, return_S=True)
+    torch.cuda.synchronize()
+    assert "chain1:" in L.describe(1)
+    assert_parity(S.cpu().numpy(), d["S"], what="chain1 golden pubmed S")
+    L.close()
