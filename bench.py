@@ -550,6 +550,8 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
     st = g.stats()
     unit = g.values is None or bool(np.all(g.values == 1))   # the value-free Clenshaw chain applies
     L = wats_hip.NormalizedLaplacian.from_graph(g, device=device)
+    if getattr(args, "tune", None):
+        L.tune(**args.tune)
     pro = prologue_timing(g, L, device) if (full and world == 1) else None
     rng = np.random.default_rng(1 + rank)
     if F == 1:
@@ -883,8 +885,16 @@ def main():
             pm["chain_us"] = chain_s * 1e6
             pm["chain_frac"] = pk * b / chain_s / (HBM_PEAK_GBS * 1e9)
             pm["roofline_chain_us"] = pk * b / (HBM_PEAK_GBS * 1e9) * 1e6
-            pm["what"] = ("PubMed-size R-MAT, K=16, the reference's F=1 signal: one whole chain per step (permute, 16 "
-                          "steps, finalize), replayed as a hipGraph; chain_frac = K x B_step / chain time / 8 TB/s")
+            pm["what"] = ("PubMed-size R-MAT, K=16, the reference's F=1 signal: one whole chain per step, the auto "
+                          "path (csrc/chain.hip: the chain in one launch of cooperating workgroups, DESIGN.md 4.7); "
+                          "chain_frac = K x B_step / chain time / 8 TB/s; multi_launch: the same chain as K + 3 "
+                          "launches (tuning key chain = 0)")
+            a.tune = {"chain": 0}
+            ml = _companion_summary(single_gpu_line(a, named_graph("pubmed", seed=args.seed), "pubmed", pk, pf,
+                                                    world, rank, device, full=False))
+            pm["multi_launch"] = {"chain_us": ml["ms_per_step"] * 1e3,
+                                  "chain_frac": pk * b / (ml["ms_per_step"] * 1e-3) / (HBM_PEAK_GBS * 1e9),
+                                  "avg_launch_us": ml["roofline"]["avg_launch_us"], "kernel": ml["roofline"]["kernel"]}
             line["pubmed_companion"] = pm
         del g
 

@@ -321,7 +321,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   std::vector<int2> passes;
   std::vector<int32_t> wpass;
   size_t lds = 0;
-  for (;; P = (P == 1 && L->tune.chain_wg <= 0) ? 32 : 2 * P) {
+  for (;; P = (P == 1 && L->tune.chain_wg <= 0) ? 64 : 2 * P) {
     if (P > 64) return WG_ERR_UNSUPPORTED;
     wd.assign(P, int4{0, 0, 0, 0});
     passes.clear();

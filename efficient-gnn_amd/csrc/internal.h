@@ -212,10 +212,14 @@ struct Tuning {
   int32_t chain = -1;        // F == 1 small unweighted graphs: the whole chain in one launch (chain.hip); -1 = auto
                              // (<= 2^18 nonzeros, <= 24576 active rows), 0 = off, 1 = whenever it applies
   int32_t chain_wg = 0;      // chain.hip workers (workgroups of 1024 threads; doubled until a worker fits LDS);
-                             // 0 = auto: one when its ids and two u buffers fit LDS (no exchange), else 32
+                             // 0 = auto: one when its ids and two u buffers fit LDS (no exchange), else 64
+                             // (PubMed-size K=16: 8 / 16 / 32 / 64 workers 187 / 139 / 119 / 113 us per chain,
+                             // profiles/r03/s13_chain1_worker_sweep.log)
   int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works)
-  int32_t graph = -1;        // wg_wavelet_features: replay the chain as a hipGraph from its 2nd call with the same
-                             // arguments; -1 = auto (small chains, launch-bound: active nnz x width <= 2^22)
+  int32_t graph = 0;         // wg_wavelet_features: replay the chain as a hipGraph from its 3rd call with the same
+                             // arguments (1 = on; -1 = small chains only, active nnz x width <= 2^22).  Off: the
+                             // replay measured SLOWER than eager launches on this stack, +2.7 us per kernel node
+                             // (PubMed K=16 145 vs 95 us, arxiv F=1 220 vs 170 us; profiles/r03/s3_graph_probe.log)
 };
 
 // The whole F = 1 chain of a small unweighted graph in one launch (chain.hip): P workgroups,

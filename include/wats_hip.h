@@ -220,9 +220,10 @@ int wg_permute_rows(wg_laplacian_t L, int32_t direction, int64_t F, const float*
  * allocation): on a stream that is being captured it returns
  * WG_ERR_UNSUPPORTED -- call it once uncaptured first; later calls are plain
  * asynchronous launches and may be captured.
- * Small (launch-bound) chains are replayed as a hipGraph of the handle's own
- * once the same arguments (pointers, F, K, s) were seen on two calls in a row
- * (tuning key "graph": -1 auto = active nnz x width <= 2^22, 0 off, 1 on).
+ * A chain can be replayed as a hipGraph of the handle's own once the same
+ * arguments (pointers, F, K, s) were seen on two calls in a row
+ * (tuning key "graph": 0 off = default, the replay measured slower than eager
+ * launches on ROCm 7.2; 1 on; -1 only when active nnz x width <= 2^22).
  * ---------------------------------------------------------------------- */
 int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s,
                         float* S, float* H, void* stream);
