@@ -1,0 +1,571 @@
+// step_dev.h -- device-side pieces of the Chebyshev step kernels shared by step.hip
+// (cheb_step_kernel and its plan) and hub.hip (the LDS-hub wave kernel): the launch
+// arguments, the per-row epilogue (reference calibration/WATS.py:32-36 recurrence, :65-68
+// heat sum, :71-72 normalisation) and the gather loops.
+#pragma once
+
+#include "internal.h"
+
+namespace wg {
+
+struct StepArgs {
+  const int32_t* rowptr;
+  const int32_t* col;
+  const float* val;
+  const uint8_t* iso;
+  const float* xm1;   // T_{k-1}: n_cols rows (owned + halo)
+  const float* xm2;   // T_{k-2}: n_rows rows (k >= 2)
+  float* xk;          // T_k (nullable)
+  float* S;           // heat-kernel sum (nullable)
+  float* H;           // normalised output (nullable; only when the tile covers all F)
+  const int32_t* out_perm;  // last step, finalize fused: S / H rows go to caller row out_perm[row] ...
+  float* S_out;             // ... of S_out / H (internal S is only read)
+  int64_t ld;         // row stride (floats) of every vector
+  int32_t LF;         // lanes across the tile's columns (tile width = LF * VEC)
+  int32_t k;          // step index (1 or >= 2)
+  double alpha0;
+  double alpha_k;
+  const ChunkDesc* chunks;
+  double* partial;
+  const int2* rowchunks;  // split rows: {first chunk, chunk count}
+  int32_t* arrivals;      // split rows: in-kernel combine counters (nullable = combine_kernel)
+  int64_t seg_mask;
+  int32_t nt;
+  int32_t bcast;
+  int32_t vidx;
+  int32_t gbuf;        // F > 1 bcast gathers as raw buffer loads (accumulate_bcast_buf)
+  int32_t hubf;        // F > 1, hub kernel: rows [0, hubf) of the tile from LDS
+  int64_t xm1_bytes;   // extent of T_{k-1} from xm1 (gbuf: < 2^31)
+  int32_t clen;        // 0 = forward recurrence + heat sum; 1 / 2 = Clenshaw step / final (ClenArgs)
+  const float* x0;     // Clenshaw: X0 rows (internal order, stride ld)
+  double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc - xm2
+  // Clenshaw on unweighted graphs (L_hat_ij = -dinv_i dinv_j): the chain carries u = b * dinv, so the
+  // gathers need no values (val == nullptr: every value 1).  uin: xm1 holds u; uprev: xm2 holds u;
+  // uout: xk gets u.
+  const double* dinv;
+  int32_t uin, uprev, uout;
+  // two-phase step (row-sharded chain, exchange overlapped): phase 1 sums each row's entries
+  // [e0, rsplit[row]) (the own columns) into part[row] (float64, row stride ld); phase 2 sums
+  // [rsplit[row], e1) (the halo columns), adds part[row] and runs the epilogue.  0 = whole row.
+  // Two halo tiers: phase 3 adds [rsplit[row], rsplit2[row]) (tier 0) into part between them,
+  // and phase 2 sums [rsplit2[row], e1).
+  int32_t phase;
+  const int32_t* rsplit;
+  const int32_t* rsplit2;
+  double* part;
+  int32_t probe;  // timing probe (knob "probe"): gathers only -- no epilogue operands, acc stored to xk
+  // hybrid step (tiles.hip; col = the tail-first column array, rsplit = each row's tail end):
+  // phase 4 sums the tail [e0, rsplit[row]), adds part (the dense blocks' sums) to rows with
+  // dense entries and runs the epilogue; with the dense blocks overlapped, phase 1 sums the
+  // tail into part on a side stream and phase 6 (no entries) adds part + part2 (the blocks'
+  // sums, rows with dense entries) and runs the epilogue
+  const double* part2;
+  int32_t xcd;  // knob xcd: XCD-contiguous unit order (cheb_step_kernel)
+};
+
+// the entry range of a row (or of a split-row chunk) this launch's phase covers
+__device__ __forceinline__ void phase_range(const StepArgs& a, int64_t row, int32_t& e0, int32_t& e1) {
+  if (a.phase == 0) return;
+  const int32_t sp = a.rsplit[row];
+  if (a.phase == 1 || a.phase == 4) {
+    e1 = min(e1, sp);
+  } else if (a.phase == 6) {
+    e1 = e0;
+  } else if (a.phase == 3) {
+    e0 = max(e0, sp);
+    e1 = min(e1, a.rsplit2[row]);
+  } else {
+    e0 = max(e0, a.rsplit2 ? a.rsplit2[row] : sp);
+  }
+  if (e1 < e0) e1 = e0;
+}
+
+// phases 1 and 3 end in part (no epilogue)
+__device__ __forceinline__ bool to_part(const StepArgs& a) { return a.phase == 1 || a.phase == 3; }
+
+// phase 1: the row's own-column sum goes to part; phase 3 adds its tier-0 sum; phase 2 adds
+// part before the epilogue (a fixed order: own, tier 0, tier 1)
+template <int VEC>
+__device__ __forceinline__ void part_store(const StepArgs& a, int64_t row, int fs, const double (&acc)[VEC]) {
+  double* p = a.part + row * a.ld + (int64_t)fs * VEC;
+  if (a.phase == 3) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) p[j] = p[j] + acc[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) p[j] = acc[j];
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void part_add(const StepArgs& a, int64_t row, int fs, double (&acc)[VEC]) {
+  const int64_t off = row * a.ld + (int64_t)fs * VEC;
+  if (a.phase >= 4) {  // hybrid step: the blocks' sums only for rows with dense entries
+    const bool dense = a.rsplit[row] != a.rowptr[row + 1];
+    if (a.phase == 6) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += a.part[off + j];
+    }
+    const double* p2 = a.phase == 6 ? a.part2 : a.part;
+    if (dense) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += p2[off + j];
+    }
+    return;
+  }
+  const double* p = a.part + off;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] += p[j];
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float* p, float (&x)[VEC]) {
+  if constexpr (VEC == 1) {
+    x[0] = *p;
+  } else if constexpr (VEC == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    x[0] = v.x; x[1] = v.y;
+  } else {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  }
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int VEC>
+__device__ __forceinline__ void store_vec_nt(float* p, const double (&x)[VEC]) {
+  if constexpr (VEC == 1) {
+    __builtin_nontemporal_store((float)x[0], p);
+  } else if constexpr (VEC == 2) {
+    f32x2 v = {(float)x[0], (float)x[1]};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x2*>(p));
+  } else {
+    f32x4 v = {(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(float* p, const double (&x)[VEC]) {
+  if constexpr (VEC == 1) {
+    *p = (float)x[0];
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2((float)x[0], (float)x[1]);
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]);
+  }
+}
+
+// Per-row epilogue operands, loaded BEFORE the row's gathers so their latency
+// overlaps the accumulation (they do not depend on it).
+template <int VEC>
+struct EpiIn {
+  float prev[VEC];  // k == 1: T_0 own row (for S); k >= 2: T_{k-2} own row
+  float sold[VEC];  // S own row (k >= 2); Clenshaw: X0 own row
+  int iso;
+  int32_t orow;     // out_perm[row] (finalize fused into the last step)
+  double dinv;      // Clenshaw on u = b * dinv: dinv of the row
+};
+
+template <int VEC>
+__device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int fs, EpiIn<VEC>& in) {
+  if (a.probe) return;
+  const int64_t off = row * a.ld + (int64_t)fs * VEC;
+  in.iso = a.iso[row];
+  in.orow = a.out_perm ? a.out_perm[row] : (int32_t)row;
+  if (a.clen) {
+    in.dinv = (a.uin | a.uprev | a.uout) ? a.dinv[row] : 1.0;
+    if (a.xm2) {
+      load_vec<VEC>(a.xm2 + off, in.prev);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) in.prev[j] = 0.0f;
+    }
+    load_vec<VEC>(a.x0 + off, in.sold);
+    return;
+  }
+  load_vec<VEC>((a.k == 1 ? a.xm1 : a.xm2) + off, in.prev);
+  if (a.S && a.k >= 2) load_vec<VEC>(a.S + off, in.sold);
+}
+
+// Per-row epilogue, run by the LF lanes holding the row's sums (`lane0` = wave
+// lane of the row's first column slice, for the H shuffle): diagonal of
+// isolated rows, recurrence, T_k store, heat sum, optional normalisation.
+template <int VEC>
+__device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, int fs, double (&acc)[VEC],
+                                              const EpiIn<VEC>& in, int lane0) {
+  const int64_t off = row * a.ld + (int64_t)fs * VEC;
+  const bool nt_st = (a.nt & 4) != 0;
+  if (a.probe) {  // timing probe: the row sums only (results are not the chain's)
+    if (a.xk) store_vec<VEC>(a.xk + off, acc);
+    return;
+  }
+  if (a.clen && a.uin) {  // sum of u_j over the row: L_hat b = -dinv_i * sum (off-diagonal part)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] *= -in.dinv;
+  }
+  if (in.iso) {  // L_hat_ii = -1 (scipy setdiag(1 - iso), then "- identity")
+    float x[VEC];
+    if (a.k == 1) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) x[j] = in.prev[j];
+    } else {
+      load_vec<VEC>(a.xm1 + off, x);
+    }
+    const double xs = (a.clen && a.uin) ? 1.0 / in.dinv : 1.0;  // own row of u -> b
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] -= (double)x[j] * xs;
+  }
+  double t[VEC];
+  if (a.clen) {  // Clenshaw: b = ck * X0 + cacc * (L_hat b') - b''
+    const double ps = a.uprev ? 1.0 / in.dinv : 1.0;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j)
+      t[j] = a.ck * (double)in.sold[j] + a.cacc * acc[j] - (double)in.prev[j] * ps;
+    if (a.uout && a.xk) {
+      double u[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) u[j] = t[j] * in.dinv;
+      if (nt_st) store_vec_nt<VEC>(a.xk + off, u);
+      else store_vec<VEC>(a.xk + off, u);
+      return;  // never the final step (S is written only there)
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) t[j] = (a.k == 1) ? acc[j] : 2.0 * acc[j] - (double)in.prev[j];
+  }
+  if (a.xk) {
+    if (nt_st) store_vec_nt<VEC>(a.xk + off, t);
+    else store_vec<VEC>(a.xk + off, t);
+  }
+  if (a.S) {
+    double s[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j)  // k == 1: S = alpha0*T_0 + alpha1*T_1; Clenshaw final: S = t
+      s[j] = a.clen ? t[j]
+                    : (a.k == 1) ? a.alpha0 * (double)in.prev[j] + a.alpha_k * t[j]
+                                 : (double)in.sold[j] + a.alpha_k * t[j];
+    // finalize fused (last step): the rows go straight to the caller's order
+    const int64_t oo = a.out_perm ? (int64_t)in.orow * a.ld + (int64_t)fs * VEC : off;
+    float* Sd = a.out_perm ? a.S_out : a.S;
+    if (nt_st) store_vec_nt<VEC>(Sd + oo, s);
+    else store_vec<VEC>(Sd + oo, s);
+    if (a.H) {
+      double part = 0.0;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) part += fabs(s[j]);
+      double tot = 0.0;
+      for (int q = 0; q < a.LF; ++q) tot += __shfl(part, lane0 + q, 64);
+      const double den = tot + 1e-8;
+      double h[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) h[j] = s[j] / den;
+      store_vec<VEC>(a.H + oo, h);
+    }
+  }
+}
+
+// acc += sum over e = e, e+stride, ... < e1 of val[e] * x[col[e]].
+// Default: float64 FMAs (a float32 x float32 product is exact in float64).
+// -DWG_LANE_F32 (experimental build): each lane's short sequence (<= a few
+// dozen terms) in float32, added to the float64 accumulator at the end.
+template <int VEC>
+__device__ __forceinline__ void accumulate(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                           const float* __restrict__ xb, double (&acc)[VEC]) {
+  const int32_t* __restrict__ col = a.col;
+  const float* __restrict__ val = a.val;
+  const int64_t ld = a.ld;
+#ifdef WG_LANE_F32
+  float part[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) part[j] = 0.0f;
+#define WG_FMA(j, vv, xx) part[j] = fmaf((vv), (xx), part[j])
+#else
+#define WG_FMA(j, vv, xx) acc[j] = fma((double)(vv), (double)(xx), acc[j])
+#endif
+  for (; e + 3 * stride < e1; e += 4 * stride) {
+    int32_t c[4];
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = col[e + u * stride];
+      v[u] = val ? val[e + u * stride] : 1.0f;
+    }
+    float x[4][VEC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load_vec<VEC>(xb + (int64_t)c[u] * ld, x[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) WG_FMA(j, v[u], x[u][j]);
+  }
+  for (; e < e1; e += stride) {
+    const int32_t c = col[e];
+    const float v = val ? val[e] : 1.0f;
+    float x[VEC];
+    load_vec<VEC>(xb + (int64_t)c * ld, x);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) WG_FMA(j, v, x[j]);
+  }
+#undef WG_FMA
+#ifdef WG_LANE_F32
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] += (double)part[j];
+#endif
+}
+
+// Sum the partial sums of n lane sub-groups (lanes base + q*LF + fs, q < n)
+// into sub-group 0, in a fixed order (tree for power-of-two n).  Must be
+// called by every lane of the wave (uniform control flow).
+template <int VEC>
+__device__ __forceinline__ void reduce_subgroups(double (&acc)[VEC], int n, int LF, int base, int fs) {
+  if (n <= 1) return;
+  if ((n & (n - 1)) == 0) {
+    for (int off = n >> 1; off >= 1; off >>= 1) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += __shfl_down(acc[j], off * LF, 64);
+    }
+  } else {
+    double tot[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) tot[j] = acc[j];
+    for (int q = 1; q < n; ++q) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) tot[j] += __shfl(acc[j], base + q * LF + fs, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = tot[j];
+  }
+}
+
+// Dynamic LDS of cheb_step_hot_kernel: the hot-column cache.
+extern __shared__ float g_hot_lds[];
+
+// Two separate loads (LDS / global) behind a branch.  Written as a ternary,
+// clang merges them into one flat load of a selected generic pointer, which
+// both loses the LDS fast path and (ROCm 7.2) miscompiles the LDS-to-flat
+// cast ("V_CMP_NE_U32 src_shared_base" illegal instruction).
+__device__ __forceinline__ float hot_or_global(const float* hot, const float* __restrict__ xb, int32_t c, int32_t H,
+                                               int64_t ld) {
+  float x;
+  if (c < H) {
+    x = hot[c];
+    asm volatile("" ::: "memory");
+  } else {
+    x = xb[(int64_t)c * ld];
+    asm volatile("" ::: "memory");
+  }
+  return x;
+}
+
+// F == 1 with an LDS hot-column cache: columns [0, H) of T_{k-1} (the
+// highest-degree rows after relabelling, which receive most gathers) are read
+// from LDS, the rest from global memory.
+__device__ __forceinline__ void accumulate_hot1(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                                const float* __restrict__ xb, int32_t H, double (&acc)[1]) {
+  const float* hot = g_hot_lds;
+  const int32_t* __restrict__ col = a.col;
+  const float* __restrict__ val = a.val;
+  const int64_t ld = a.ld;
+  for (; e + 3 * stride < e1; e += 4 * stride) {
+    int32_t c[4];
+    float v[4], x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = col[e + u * stride];
+      v[u] = val ? val[e + u * stride] : 1.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = hot_or_global(hot, xb, c[u], H, ld);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[0] = fma((double)v[u], (double)x[u], acc[0]);
+  }
+  for (; e < e1; e += stride) {
+    const int32_t c = col[e];
+    const float x = hot_or_global(hot, xb, c, H, ld);
+    acc[0] = fma((double)val[e], (double)x, acc[0]);
+  }
+}
+
+// Sub-group cooperative index loads (LF > 1).  The LF lanes of a sub-group
+// walk the same nonzero sequence e, e+stride, ...; instead of every lane
+// issuing a dword load of the same col/val entry (10 identical addresses per
+// sub-group at F=40: the texture-address unit was ~70 % busy, PMC s11), lane
+// fs loads element t0+fs and the sub-group shares the LF (col, val) pairs
+// through ds_bpermute, which runs on the LDS pipe.  Same elements, same
+// order as accumulate() -> bitwise-identical sums.  U = gathers in flight.
+#ifndef WG_BCAST_U  // gathers in flight per lane on the widths whose LF is not a multiple of 5
+#define WG_BCAST_U 4
+#endif
+template <int VEC, int U>
+__device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                                 const float* __restrict__ xb, double (&acc)[VEC], int fs,
+                                                 int base) {
+  const int LF = a.LF;
+  const int64_t ld = a.ld;
+  if (e >= e1) return;
+  const int32_t n = (e1 - e + stride - 1) / stride;
+  for (int32_t t0 = 0; t0 < n; t0 += LF) {
+    const int32_t tt = t0 + fs;
+    int32_t myc = 0;
+    float myv = 0.0f;
+    if (tt < n) {
+      const int32_t idx = e + tt * stride;
+      myc = a.col[idx];
+      myv = a.val ? a.val[idx] : 1.0f;
+    }
+    const int cnt = min(LF, n - t0);
+    for (int j = 0; j < cnt; j += U) {
+      int32_t c[U];
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int src = base + min(j + u, LF - 1);  // stays inside the sub-group
+        c[u] = __shfl(myc, src, 64);
+        v[u] = __shfl(myv, src, 64);
+      }
+      float x[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (j + u < cnt) load_vec<VEC>(xb + (int64_t)c[u] * ld, x[u]);  // no dummy gathers
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (j + u < cnt) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) acc[q] = fma((double)v[u], (double)x[u][q], acc[q]);
+        }
+      }
+    }
+  }
+}
+
+// Branch-free form of accumulate_bcast (same elements, same order, so the same
+// sums bit for bit).  The gathers are raw buffer loads of T_{k-1}: a masked
+// slot gets an out-of-range offset, which the hardware answers with zeros and
+// no memory request.  The inner loop has a fixed trip count, and the next LF
+// (col, val) pairs are loaded from a clamped index while the current ones are
+// gathered.  With the loads behind branches (accumulate_bcast), the waitcnt
+// pass drains every in-flight gather (vmcnt(0)) at each batch of U.
+// xoff_f: this lane's column offset in floats (fs * VEC); rs spans T_{k-1}.
+// HUB: rows [0, a.hubf) of the gathered tile come from the LDS copy at
+// g_hub_lds ([hubf][W] floats, then W zeros): their global load gets the
+// dropped offset, every other column reads the LDS zero row; x = global + LDS.
+extern __shared__ float g_hub_lds[];
+
+template <int VEC, int U, bool HUB>
+__device__ __forceinline__ void accumulate_bcast_buf(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                                     __amdgpu_buffer_rsrc_t rs, uint32_t xoff_b,
+                                                     double (&acc)[VEC], int fs, int base) {
+  constexpr uint32_t kDrop = 0x80000000u;
+  const int LF = a.LF;
+  const uint32_t ldb = (uint32_t)a.ld * 4u;
+  if (e >= e1) return;
+  const int32_t n = (e1 - e + stride - 1) / stride;
+  int32_t idx = e + min(fs, n - 1) * stride;
+  int32_t myc = a.col[idx];
+  float myv = a.val[idx];
+  for (int32_t t0 = 0; t0 < n; t0 += LF) {
+    const int32_t cc = myc;
+    const float cv = myv;
+    idx = e + min(t0 + LF + fs, n - 1) * stride;  // next LF pairs (clamped: always a valid entry)
+    myc = a.col[idx];
+    myv = a.val[idx];
+    const int cnt = min(LF, n - t0);
+    for (int j = 0; j < LF; j += U) {
+      int32_t c[U];
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int src = base + min(j + u, LF - 1);  // stays inside the sub-group
+        c[u] = __shfl(cc, src, 64);
+        v[u] = __shfl(cv, src, 64);
+      }
+      float x[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool hub = HUB && c[u] < a.hubf;
+        const uint32_t off = (j + u < cnt && !hub) ? (uint32_t)c[u] * ldb + xoff_b : kDrop;
+        // the builtins return integer data: reinterpret the bits
+        if constexpr (VEC == 4) {
+          const f32x4 g = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+          x[u][0] = g[0]; x[u][1] = g[1]; x[u][2] = g[2]; x[u][3] = g[3];
+        } else if constexpr (VEC == 2) {
+          const f32x2 g = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+          x[u][0] = g[0]; x[u][1] = g[1];
+        } else {
+          x[u][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+        if constexpr (HUB) {
+          const int W = LF * VEC;
+          const int hrow = (j + u < cnt && hub) ? c[u] : a.hubf;  // row hubf = zeros
+          const float* hp = g_hub_lds + hrow * W + fs * VEC;
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) x[u][q] += hp[q];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double vv = (j + u < cnt) ? (double)v[u] : 0.0;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[q] = fma(vv, (double)x[u][q], acc[q]);
+      }
+    }
+  }
+}
+
+// F == 1: each lane takes 4 consecutive nonzeros with one 16-B int4 / float4
+// load of col / val (4x fewer index instructions through the texture-address
+// unit).  Chunks are 4-aligned in the CSR (arrays padded by 4 entries), lane
+// ns of the row's team takes chunks ns, ns+stride, ...; elements outside
+// [e0, e1) are masked.  Different summation split than accumulate().
+__device__ __forceinline__ void accumulate_vidx1(const StepArgs& a, int32_t e0, int32_t e1, int32_t ns,
+                                                 int32_t stride, const float* __restrict__ xb, double (&acc)[1]) {
+  const int64_t ld = a.ld;
+  const int32_t eb = e0 & ~3;
+  for (int32_t q = eb + 4 * ns; q < e1; q += 4 * stride) {
+    const int4 c = *reinterpret_cast<const int4*>(a.col + q);
+    const float4 v = a.val ? *reinterpret_cast<const float4*>(a.val + q) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const int32_t cc[4] = {c.x, c.y, c.z, c.w};
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = (q + u >= e0) && (q + u < e1);
+      x[u] = ok ? xb[(int64_t)cc[u] * ld] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = (q + u >= e0) && (q + u < e1);
+      if (ok) acc[0] = fma((double)vv[u], (double)x[u], acc[0]);
+    }
+  }
+}
+
+template <int VEC, bool BCAST, bool HOT, bool HUB = false>
+__device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
+                                          const float* __restrict__ xb, double (&acc)[VEC], int32_t H, int fs,
+                                          int base) {
+  if constexpr (HOT && VEC == 1) {
+    accumulate_hot1(a, e, e1, stride, xb, H, acc);
+  } else if constexpr (BCAST) {
+    if (HUB || a.gbuf) {  // T_{k-1} as a raw buffer: [xm1, xm1 + xm1_bytes), this lane's column offset from xb
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0, (int)a.xm1_bytes, 0x00020000);
+      const uint32_t xoff = (uint32_t)((xb - a.xm1) * 4);
+      if (a.LF % 5 == 0) accumulate_bcast_buf<VEC, 5, HUB>(a, e, e1, stride, rs, xoff, acc, fs, base);
+      else accumulate_bcast_buf<VEC, 4, HUB>(a, e, e1, stride, rs, xoff, acc, fs, base);
+    } else if (a.LF % 5 == 0) {
+      accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
+    } else {
+      accumulate_bcast<VEC, WG_BCAST_U>(a, e, e1, stride, xb, acc, fs, base);
+    }
+  } else {
+    accumulate<VEC>(a, e, e1, stride, xb, acc);
+  }
+}
+
+
+}  // namespace wg
