@@ -160,7 +160,7 @@ struct Tuning {
   int32_t iter = 0;          // team mode: target nonzeros per lane sub-group
   int32_t block_iter = 0;    // block mode: rows up to NW*G*block_iter nonzeros get one workgroup
   int32_t chunk_iter = 0;    // split mode: NW*G*chunk_iter nonzeros per workgroup chunk
-  int32_t nt = -1;           // non-temporal hints: 4 = T_k / S stores; -1 = auto (4 when a step's T_k + S
+  int32_t nt = -1;           // store hints: 4 = nt T_k / S stores, 8 = write-through (sc1) T_k stores; -1 = auto (4 when a step's T_k + S
                              // streams exceed 64 MB, else 0: the next steps re-read them)
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
   int32_t bcast = 1;         // F > 1: sub-group cooperative index loads (ds_bpermute broadcast)

@@ -583,9 +583,11 @@ void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_it
   // gather kernel's defaults; its 2-way shards (92) -> 1536: 415 vs 473; the 4-way shards (46)
   // keep the defaults: 1536 gives 232-234 vs 246-249 on three ranks but 312 vs 247 on the fourth
   // (a long-tailed row walked by one sub-group), the 8-way shards (23) 172 vs 156;
-  // profiles/r02/s72-s76)
+  // profiles/r02/s72-s76).  Only from 8 M nonzeros: on the arxiv-size graph (2.3 M, hub rows of
+  // thousands of tail entries walked by one sub-group) the 1536 tier took 67.8 vs 38.6 us
+  // (profiles/r03/s20-s21)
   const int64_t per_cu = rows / ((int64_t)G * 256);
-  if (hybrid && per_cu >= 64) {
+  if (hybrid && per_cu >= 64 && nnz >= ((int64_t)8 << 20)) {
     const bool big = per_cu >= 128;
     *iter = t.iter > 0 ? t.iter : (big ? 6144 : 1536);
     *block_iter = t.block_iter > 0 ? t.block_iter : (big ? 4096 : 1024);

@@ -147,6 +147,19 @@ __device__ __forceinline__ void store_vec_nt(float* p, const double (&x)[VEC]) {
   }
 }
 
+// 16-B write-through (sc1) store: the line leaves the XCD's L2 instead of staying there
+// (MI355X_MICROARCH.md, inter-workgroup visibility table), so a step's T_k stream does not evict
+// the gathered rows of the same step from L2; other widths store plainly
+template <int VEC>
+__device__ __forceinline__ void store_vec_sc1(float* p, const double (&x)[VEC]) {
+  if constexpr (VEC == 4) {
+    f32x4 v = {(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    for (int j = 0; j < VEC; ++j) p[j] = (float)x[j];
+  }
+}
+
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* p, const double (&x)[VEC]) {
   if constexpr (VEC == 1) {
@@ -229,6 +242,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
 #pragma unroll
       for (int j = 0; j < VEC; ++j) u[j] = t[j] * in.dinv;
       if (nt_st) store_vec_nt<VEC>(a.xk + off, u);
+      else if (a.nt & 8) store_vec_sc1<VEC>(a.xk + off, u);
       else store_vec<VEC>(a.xk + off, u);
       return;  // never the final step (S is written only there)
     }
@@ -238,6 +252,7 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
   }
   if (a.xk) {
     if (nt_st) store_vec_nt<VEC>(a.xk + off, t);
+    else if (a.nt & 8) store_vec_sc1<VEC>(a.xk + off, t);
     else store_vec<VEC>(a.xk + off, t);
   }
   if (a.S) {
