@@ -94,9 +94,6 @@ def parse():
     ap.add_argument("--pick-exchange", type=int, default=1,
                     help="N > 1: time the headline with the first two --exchange kinds and report the faster "
                          "(both attached)")
-    ap.add_argument("--halo-tiers", type=int, default=None,
-                    help="sharded runs: halo tiers (1, or 2: the hot halo rows exchanged first and their entries "
-                         "summed while the rest is in flight, with two-phase steps); default 1")
     ap.add_argument("--cold-reps", type=int, default=5,
                     help="chains timed after writing a 512 MiB scratch buffer (cold Infinity Cache / L2); 0 = skip")
     ap.add_argument("--f1-companion", type=int, default=1,
@@ -217,7 +214,7 @@ def _rel_err(got, ref) -> float:
 
 # ----------------------------------------------------------------------------- row-sharded runs
 def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl",
-                median_reps: int = 0, check: bool = True, halo_tiers=None, min_time: float = 0.0):
+                median_reps: int = 0, check: bool = True, min_time: float = 0.0):
     """One graph (generated identically on every rank, on the GPU) split into
     nnz-balanced row blocks; per Chebyshev step one halo exchange (`exchange`:
     RCCL send/recv or IPC pull in the native chain, or torch
@@ -244,7 +241,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     torch.cuda.empty_cache()
     with _stdout_to_stderr():   # RCCL prints its version banner at communicator init: keep stdout one JSON line
         sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device,
-                            max_features=F, halo_tiers=halo_tiers)
+                            max_features=F)
     if F == 1:
         X = sw.L.log1p_degree()
     else:
@@ -345,15 +342,13 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                                + f"; K={K} F={F}",
                    "exchange": exchange,
                    "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
-                   "rank0_rows": p.n_own, "rank0_halo_rows": p.n_halo, "halo_tiers": p.tiers,
-                   "rank0_hot_halo_rows": p.n_hot, "parallelism": f"rows x{world}"},
+                   "rank0_rows": p.n_own, "rank0_halo_rows": p.n_halo, "parallelism": f"rows x{world}"},
         "roofline": {"bound": "hbm", "achieved": b_step / (avg_ms * 1e-3) / 1e9 if avg_ms else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None,
                      "traffic": None, "kernel": kernel,
                      "algorithmic_bytes_per_launch": b_step, "avg_launch_us": avg_ms * 1e3,
                      "avg_exchange_us": prof["exchange_ms"] * 1e3,
-                     "exchange_overlapped": prof.get("overlapped", False),
                      "graph_replayed": bool(dinfo.get("captured")) if dinfo else None,
                      "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
@@ -790,7 +785,7 @@ def main():
         exc = None
         try:
             line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
-                               exchanges[0], median_reps=max(20, args.steps), halo_tiers=args.halo_tiers)
+                               exchanges[0], median_reps=max(20, args.steps))
         except Exception as e:  # noqa: BLE001 -- keep a headline: the next exchange, noted in the line
             exc = e
         if _any_rank(exc is not None, world):   # every rank switches together, or none does
@@ -801,7 +796,7 @@ def main():
             _log(f"headline with exchange {exchanges[0]} failed ({type(exc).__name__}: {exc}); using {exchanges[1]}")
             torch.cuda.empty_cache()
             line = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank, device,
-                               exchanges[1], median_reps=max(20, args.steps), halo_tiers=args.halo_tiers)
+                               exchanges[1], median_reps=max(20, args.steps))
             line["headline_fallback"] = f"exchange {exchanges[0]} failed: {type(exc).__name__}: {exc}"
             exchanges = exchanges[1:] + exchanges[:1]
         hw.cancel()
@@ -823,7 +818,7 @@ def main():
             try:
                 torch.cuda.empty_cache()
                 alt = run_sharded(cfg, args.K, args.F, args.steps, args.warmup, args.seed, args.s, world, rank,
-                                  device, exchanges[1], median_reps=max(20, args.steps), halo_tiers=args.halo_tiers)
+                                  device, exchanges[1], median_reps=max(20, args.steps))
             except Exception as exc:  # noqa: BLE001
                 alt = {"error": f"{type(exc).__name__}: {exc}", "exchange": exchanges[1]}
             pw.cancel()
@@ -940,7 +935,7 @@ def main():
             try:
                 torch.cuda.empty_cache()
                 results[key] = run_sharded(c, None, None, args.sharded_steps, 1, args.seed, args.s, world, rank,
-                                           device, x, halo_tiers=args.halo_tiers, min_time=0.2)
+                                           device, x, min_time=0.2)
             except Exception as exc:  # noqa: BLE001
                 results[key] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
     if mode == "sharded" and len(exchanges) > 1:
@@ -954,7 +949,7 @@ def main():
             try:
                 torch.cuda.empty_cache()
                 results[f"{cfg}_{x}"] = run_sharded(cfg, args.K, args.F, args.sharded_steps, 1, args.seed, args.s,
-                                                    world, rank, device, x, halo_tiers=args.halo_tiers, min_time=0.2)
+                                                    world, rank, device, x, min_time=0.2)
             except Exception as exc:  # noqa: BLE001
                 results[f"{cfg}_{x}"] = {"error": f"{type(exc).__name__}: {exc}", "exchange": x}
     if watchdog is not None:

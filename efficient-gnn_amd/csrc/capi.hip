@@ -99,9 +99,6 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;
   } else if (!strcmp(key, "tile_f")) {
     L->tune.tile_f = (int32_t)std::max<int64_t>(0, value);
-  } else if (!strcmp(key, "seg_mask")) {
-    L->tune.seg_mask = value;
-    return WG_OK;  // no replan
   } else if (!strcmp(key, "lds")) {
     if (value < 0 || value > 4) return fail(WG_ERR_INVALID, "lds must be 0, 1, 2, 3 (auto) or 4");
     L->tune.lds = (int32_t)value;
@@ -124,12 +121,6 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "uscale")) {
     L->tune.uscale = value ? 1 : 0;
     return WG_OK;  // launch-time choice
-  } else if (!strcmp(key, "hubf")) {
-    L->tune.hubf = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 4096));
-    return WG_OK;  // launch-time choice
-  } else if (!strcmp(key, "gbuf")) {
-    L->tune.gbuf = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "inkernel_combine")) {
     L->tune.inkernel_combine = value ? 1 : 0;
     return WG_OK;  // launch-time choice
@@ -145,58 +136,23 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "fuse_finalize")) {
     L->tune.fuse_finalize = value ? 1 : 0;
     return WG_OK;  // launch-time choice
-  } else if (!strcmp(key, "hub_vidx")) {
-    L->tune.hub_vidx = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hub_iter")) {
     L->tune.hub_iter = (int32_t)std::max<int64_t>(1, std::min<int64_t>(value, 4096));
-  } else if (!strcmp(key, "probe")) {
-    L->tune.probe = value ? 1 : 0;
-    return WG_OK;  // launch-time, timing only
   } else if (!strcmp(key, "fpad")) {
     if (value != 0 && value != 4 && value != 8 && value != 16) return fail(WG_ERR_INVALID, "fpad must be 0, 4, 8 or 16");
     L->tune.fpad = (int32_t)value;
     return WG_OK;  // launch-time choice (workspace regrows on the next call)
-  } else if (!strcmp(key, "cu_reserve")) {
-    L->tune.cu_reserve = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 128));
-    return WG_OK;  // sharded chain: CUs kept free of the step kernels (the exchange stream's)
-  } else if (!strcmp(key, "hub_pipe")) {
-    L->tune.hub_pipe = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hub_sell")) {
     L->tune.hub_sell = value ? 1 : 0;  // plan-time choice (the LDS plans are rebuilt)
-  } else if (!strcmp(key, "hub_split")) {
-    L->tune.hub_split = value ? 1 : 0;  // plan-time choice (the LDS plans are rebuilt)
-  } else if (!strcmp(key, "probe_colmask")) {
-    if (value < 0 || value > 30) return fail(WG_ERR_INVALID, "probe_colmask must be in [0, 30]");
-    L->tune.probe_colmask = (int32_t)value;
-    return WG_OK;  // launch-time, timing only
-  } else if (!strcmp(key, "xskip")) {
-    L->tune.xskip = value ? 1 : 0;
-    return WG_OK;  // timing probe only: streamed blocks skip pack / RCCL / unpack (results wrong)
-  } else if (!strcmp(key, "xdelay")) {
-    L->tune.xdelay = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 100000));
-    return WG_OK;  // timing probe of the sharded chain (a captured chain re-captures: tune_gen)
-  } else if (!strcmp(key, "overlap")) {
-    L->tune.overlap = value ? 1 : 0;
-    return WG_OK;  // launch-time choice (a captured chain re-captures: tune_gen)
   } else if (!strcmp(key, "tiles")) {
     if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "tiles must be -1 (auto), 0 or 1");
     L->tune.tiles = (int32_t)value;
   } else if (!strcmp(key, "tile_th")) {
     if (value < 1 || value > 2048) return fail(WG_ERR_INVALID, "tile_th must be in [1, 2048]");
     L->tune.tile_th = (int32_t)value;
-  } else if (!strcmp(key, "tiles_overlap")) {
-    L->tune.tiles_overlap = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_rows")) {
     if (value != 64 && value != 128) return fail(WG_ERR_INVALID, "tile_rows must be 64 or 128");
     L->tune.tile_rows = (int32_t)value;
-  } else if (!strcmp(key, "probe_tailwin")) {
-    L->tune.probe_tailwin = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 1024));  // plan-time, timing only
-  } else if (!strcmp(key, "xcd")) {
-    L->tune.xcd = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_rg")) {
     if (value != 1 && value != 2 && value != 4) return fail(WG_ERR_INVALID, "tile_rg must be 1, 2 or 4");
     L->tune.tile_rg = (int32_t)value;
@@ -219,6 +175,21 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "graph must be -1 (auto), 0 or 1");
     L->tune.graph = (int32_t)value;
     return WG_OK;  // launch-time choice (tune_gen: a captured chain is re-captured)
+#ifdef WG_TIMING_PROBES
+    // timing probes (results wrong or time inflated on purpose): only in a probe build
+    // (make -C efficient-gnn_amd/csrc VARIANT=probes EXTRA_FLAGS=-DWG_TIMING_PROBES)
+  } else if (!strcmp(key, "seg_mask")) {
+    L->tune.seg_mask = value;  // plan segments launched (timing attribution)
+    return WG_OK;
+  } else if (!strcmp(key, "probe")) {
+    L->tune.probe = value ? 1 : 0;  // the gathers alone: no epilogue operands
+    return WG_OK;
+  } else if (!strcmp(key, "probe_tailwin")) {
+    L->tune.probe_tailwin = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 1024));  // plan-time
+  } else if (!strcmp(key, "xdelay")) {
+    L->tune.xdelay = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 100000));  // simulated link us
+    return WG_OK;
+#endif
   } else {
     return fail(WG_ERR_INVALID, "wg_laplacian_tune: unknown key '%s'", key);
   }
@@ -373,7 +344,7 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
   const size_t ustride = lp ? ((size_t)lp->u_floats() + 63) / 64 * 64 : 0;
   // the hybrid step (tiles.hip) gathers the first step's X0 value-free too, as u_0 = X0 * dinv
   TilePlan* tp0 = nullptr;  // the hybrid step's plan, when it applies (built here once, synchronous)
-  if (!lp && L->tune.clenshaw && K >= 1 && L->unit && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 &&
+  if (!lp && L->tune.clenshaw && K >= 1 && L->unit && L->tune.uscale &&
       L->tune.hot == 0 && !L->tune.probe && tiles_wanted(L, Fp))
     if (int rc0 = get_tile_plan(L, /*active_only=*/true, Fp, &tp0)) return rc0;
   const bool u0 = tp0 != nullptr;
@@ -431,7 +402,7 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     int nb = 0;
     // unweighted graphs: every stored b_k as u_k = b_k * dinv, so the gathers read no CSR values
     // (L_hat b = -dinv_i sum_j u_j); X0 itself stays unscaled (the first step reads the values)
-    const int useu = (L->unit && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 && L->tune.hot == 0) ? 1 : 0;
+    const int useu = (L->unit && L->tune.uscale && L->tune.hot == 0) ? 1 : 0;
     float* ub = u0 ? L->ws + 3 * stride : nullptr;  // u_0 = X0 * dinv (active rows)
     if (u0 && (rc = launch_scale_rows(L, L->n_active, Fp, b0, ub, stream))) return rc;
     for (int32_t k = K - 1; k >= 1; --k) {

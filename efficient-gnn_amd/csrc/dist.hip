@@ -53,13 +53,6 @@ void launch_pack(int64_t n, int64_t F, const int32_t* rows, const float* src, fl
 }
 
 // received rows i (row-block streaming: received contiguously per (block, peer)) -> halo row pos[i]
-__global__ void unpack_rows_kernel(int64_t n, int64_t F, const int32_t* __restrict__ pos, const float* __restrict__ src,
-                                   float* __restrict__ ext_halo) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n * F) return;
-  const int64_t i = idx / F;
-  ext_halo[(int64_t)pos[i] * F + (idx - i * F)] = src[idx];
-}
 
 // ---- one-sided exchange over IPC-mapped peer memory (exchange mode "ipc") ----
 // Each rank exposes one allocation: two slots of its extended vector ([own |
@@ -164,12 +157,14 @@ __global__ __launch_bounds__(256) void ipc_pull4_kernel(IpcPull p, int slot, int
   }
 }
 
+#ifdef WG_TIMING_PROBES
 // timing probe (knob "xdelay"): hold the stream for `ticks` of the 100 MHz constant clock,
 // standing in for link time the one-GPU runs do not have
 __global__ void spin_kernel(uint64_t ticks) {
   const uint64_t t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
+#endif
 
 // (signal the previous phase and) wait for the peers; one workgroup
 __global__ void ipc_wait_kernel(IpcPull p, int signal) { ipc_wait(p, signal != 0); }
@@ -183,11 +178,6 @@ __global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, i
   for (int q = 0; q < world; ++q)
     if (q != rank) __hip_atomic_store(peer_flags[q] + rank, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-
-// The exchange stream, at normal priority: a highest-priority stream made every later
-// handle's step kernels in the process about 2x slower (Reddit F=1 sharded chain 2.2 vs
-// 1.02 ms, F=41 23.5 vs 22.4 ms; profiles/r02/s53_stream_priority.log) and bought nothing.
-hipError_t create_exchange_stream(hipStream_t* out) { return hipStreamCreateWithFlags(out, hipStreamNonBlocking); }
 
 int nccl_try(ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return WG_OK;
@@ -217,32 +207,13 @@ struct wg_dist_s {
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
   int64_t n_own = 0, n_cols = 0, n_send = 0, n_halo = 0;
-  // tiers (1 or 2): the halo is [tier 0 | tier 1], each grouped by owner; tier 0 holds every
-  // peer's highest-degree rows (most of the gathers), exchanged first so the step's hot-halo
-  // entries run while tier 1 is in flight.  Counts and offsets are tier-major: [t * world + q].
-  int tiers = 1;
-  int32_t* send_rows = nullptr;  // internal ids of own rows, grouped by (tier, peer)
-  std::vector<int64_t> send_cnt, recv_cnt, send_off, recv_off;
+  int32_t* send_rows = nullptr;  // internal ids of own rows, grouped by peer
+  std::vector<int64_t> send_cnt, recv_cnt, send_off, recv_off;  // [world], [world + 1]
   float* ws = nullptr;
   size_t ws_floats = 0;
   bool use_graph = true;
   hipStream_t cap = nullptr;  // capture / replay stream (the caller's may be the null stream)
-  int cap_reserve = 0;        // CUs masked off cap (tuning key "cu_reserve")
   hipEvent_t fork = nullptr, join = nullptr;
-  // exchange overlapped with the own-column half of each step (two-phase steps, step.hip)
-  hipStream_t xs = nullptr;   // exchange stream
-  hipEvent_t xfork = nullptr, xjoin = nullptr, xtier = nullptr;
-  bool overlapped = false;    // the last chain ran two-phase steps
-  // row-block streaming (wg_dist_stream_blocks, RCCL): each step runs as nblk launches over
-  // nnz-balanced blocks of internal rows; block b's rows go to the peers (pack, grouped
-  // send / receive, unpack into the halo) on xs while block b+1 computes on st
-  int nblk = 0;
-  bool streamed = false;                        // the last chain streamed its blocks
-  std::vector<int64_t> blk_rows;                // [nblk + 1] internal row bounds
-  int32_t* bsend_rows = nullptr;                // [n_send] internal ids, grouped by (block, peer)
-  int32_t* brecv_pos = nullptr;                 // [n_halo] halo positions, grouped by (block, sender)
-  std::vector<int64_t> bsend_off, brecv_off;    // [nblk * world + 1]
-  std::vector<hipEvent_t> bev;                  // [nblk] block b's rows final (on st)
   hipGraphExec_t exec = nullptr;
   GraphKey key{};
   int warm = 0;  // eager calls made with the current key (the first builds plans / workspace)
@@ -271,14 +242,7 @@ struct wg_dist_s {
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
-    if (xfork) (void)hipEventDestroy(xfork);
-    if (xjoin) (void)hipEventDestroy(xjoin);
-    if (xtier) (void)hipEventDestroy(xtier);
-    for (hipEvent_t e : bev) (void)hipEventDestroy(e);
-    (void)hipFree(bsend_rows);
-    (void)hipFree(brecv_pos);
     if (cap) (void)hipStreamDestroy(cap);
-    if (xs) (void)hipStreamDestroy(xs);
     (void)hipFree(send_rows);
     (void)hipFree(ws);
   }
@@ -311,207 +275,67 @@ struct wg_dist_s {
     return WG_OK;
   }
 
-  // refresh halo tier `tier` (-1: every tier) of ext[n_own ...] (F floats per row) from the
-  // owners.  ipc: `slot` is the region slot ext lives in (the owners' rows are read from the
-  // same slot of their regions); the previous phase's completion is signalled by the same
-  // one-workgroup kernel that then waits for the peers -- once per phase, with the first tier.
-  // rccl: every send row is packed with the first tier; one grouped send/receive per call.
-  // The profiling events span the first tier's start to the last tier's end.
-  int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot = 0, int tier = -1) {
-    const int t0 = tier < 0 ? 0 : tier, t1 = tier < 0 ? tiers - 1 : tier;
-    if (int rc = transfer(ext, sendbuf, F, st, slot, t0, t1)) return rc;
-    if (L->tune.xdelay > 0 && n_halo > 0) {  // timing probe: the tiers' share of the simulated link time
-      const int64_t rows = recv_off[(size_t)(t1 + 1) * world] - recv_off[(size_t)t0 * world];
-      hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, (uint64_t)(100.0 * L->tune.xdelay * rows / n_halo));
+  // refresh the halo ext[n_own ...] (F floats per row) from the owners, then the step kernels
+  // that gather it run on the same stream.  ipc: `slot` is the region slot ext lives in (the
+  // owners' rows are read from the same slot of their regions); the previous phase's completion
+  // is signalled by the one-workgroup kernel that then waits for the peers.  rccl: pack the rows
+  // the peers asked for, one grouped send / receive straight into the halo rows.
+  int exchange(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot = 0) {
+    if (int rc = transfer(ext, sendbuf, F, st, slot)) return rc;
+#ifdef WG_TIMING_PROBES
+    if (L->tune.xdelay > 0 && n_halo > 0) {  // timing probe: simulated link time, one spinning wave
+      hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, (uint64_t)(100.0 * L->tune.xdelay));
       WG_LAUNCH_CHECK();
     }
+#endif
     return WG_OK;
   }
 
-  int transfer(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot, int t0, int t1) {
-    const bool first = t0 == 0, last = t1 == tiers - 1;
+  int transfer(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot) {
     if (ipc && world == 1) return WG_OK;  // no peers: nothing to wait for or pull
     if (ipc) {
-      if (first) {
-        if (int rc = mark(st, true)) return rc;
-        // one spinning workgroup signals and waits (ranks sharing a GPU in tests must not
-        // starve each other's kernels), then full grids pull the halo rows
-        if (int rc = ipc_wait_only(st, /*signal_first=*/true)) return rc;
-      }
-      const int64_t h0 = recv_off[(size_t)t0 * world], h1 = recv_off[(size_t)(t1 + 1) * world];
-      const int64_t total = (h1 - h0) * F;
+      if (int rc = mark(st, true)) return rc;
+      // one spinning workgroup signals and waits (ranks sharing a GPU in tests must not
+      // starve each other's kernels), then full grids pull the halo rows
+      if (int rc = ipc_wait_only(st, /*signal_first=*/true)) return rc;
+      const int64_t total = n_halo * F;
       const bool v4 = (F % 4 == 0) && slot_floats * 4 < ((int64_t)1 << 31);
       if (total > 0) {
         const int blocks = (int)std::min<int64_t>(65535, ceil_div(v4 ? total / 4 : total, 256));
         if (v4)
-          hipLaunchKernelGGL(ipc_pull4_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, h0, h1 - h0, F,
+          hipLaunchKernelGGL(ipc_pull4_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, (int64_t)0, n_halo, F,
                              halo_owner, halo_src, ext);
         else
-          hipLaunchKernelGGL(ipc_pull_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, h0, h1 - h0, F,
+          hipLaunchKernelGGL(ipc_pull_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, (int64_t)0, n_halo, F,
                              halo_owner, halo_src, ext);
         WG_LAUNCH_CHECK();
       }
-      return last ? mark(st, false) : WG_OK;
+      return mark(st, false);
     }
     if (world == 1 && n_send == 0) return WG_OK;
-    if (first) {
-      if (int rc = mark(st, true)) return rc;
-      if (n_send > 0) {
-        launch_pack(n_send, F, send_rows, ext, sendbuf, st);
-        WG_LAUNCH_CHECK();
-      }
-    }
-    // one grouped send / receive for the tiers asked for (all of them: one group)
-    if (int rc = nccl_try(ncclGroupStart(), "ncclGroupStart")) return rc;
-    for (int t = t0; t <= t1; ++t) {
-      for (int q = 0; q < world; ++q) {
-        const size_t i = (size_t)t * world + q;
-        if (send_cnt[i] > 0)
-          if (int rc = nccl_try(ncclSend(sendbuf + send_off[i] * F, (size_t)(send_cnt[i] * F), ncclFloat32, q, comm, st),
-                                "ncclSend")) {
-            (void)ncclGroupEnd();
-            return rc;
-          }
-        if (recv_cnt[i] > 0)
-          if (int rc = nccl_try(ncclRecv(ext + (n_own + recv_off[i]) * F, (size_t)(recv_cnt[i] * F), ncclFloat32, q,
-                                         comm, st),
-                                "ncclRecv")) {
-            (void)ncclGroupEnd();
-            return rc;
-          }
-      }
-    }
-    if (int rc = nccl_try(ncclGroupEnd(), "ncclGroupEnd")) return rc;
-    return last ? mark(st, false) : WG_OK;
-  }
-
-  // block b of the vector ext (own rows of block b final) to the peers, and the peers' block b
-  // rows into ext's halo, on stream xs: pack, one grouped send / receive, unpack
-  int exchange_block(int b, float* ext, float* sendbuf, float* recvbuf, int64_t F, hipStream_t xst) {
-    const size_t g0 = (size_t)b * world, g1 = (size_t)(b + 1) * world;
-    const int64_t s0 = bsend_off[g0], s1 = bsend_off[g1], h0 = brecv_off[g0], h1 = brecv_off[g1];
-    if (b == nblk - 1)  // blocks go last first
-      if (int rc = mark(xst, true)) return rc;
-    if (L->tune.xskip) {  // timing probe: the simulated link time alone
-      if (L->tune.xdelay > 0 && n_halo > 0) {
-        hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, xst,
-                           (uint64_t)(100.0 * L->tune.xdelay * (double)(h1 - h0) / (double)n_halo));
-        WG_LAUNCH_CHECK();
-      }
-      return b == 0 ? mark(xst, false) : WG_OK;
-    }
-    if (s1 > s0) {
-      launch_pack(s1 - s0, F, bsend_rows + s0, ext, sendbuf + s0 * F, xst);
+    if (int rc = mark(st, true)) return rc;
+    if (n_send > 0) {
+      launch_pack(n_send, F, send_rows, ext, sendbuf, st);
       WG_LAUNCH_CHECK();
     }
     if (int rc = nccl_try(ncclGroupStart(), "ncclGroupStart")) return rc;
     for (int q = 0; q < world; ++q) {
-      const size_t i = g0 + q;
-      const int64_t ns = bsend_off[i + 1] - bsend_off[i], nr = brecv_off[i + 1] - brecv_off[i];
-      if (ns > 0)
-        if (int rc = nccl_try(ncclSend(sendbuf + bsend_off[i] * F, (size_t)(ns * F), ncclFloat32, q, comm, xst),
+      if (send_cnt[q] > 0)
+        if (int rc = nccl_try(ncclSend(sendbuf + send_off[q] * F, (size_t)(send_cnt[q] * F), ncclFloat32, q, comm, st),
                               "ncclSend")) {
           (void)ncclGroupEnd();
           return rc;
         }
-      if (nr > 0)
-        if (int rc = nccl_try(ncclRecv(recvbuf + brecv_off[i] * F, (size_t)(nr * F), ncclFloat32, q, comm, xst),
+      if (recv_cnt[q] > 0)
+        if (int rc = nccl_try(ncclRecv(ext + (n_own + recv_off[q]) * F, (size_t)(recv_cnt[q] * F), ncclFloat32, q, comm,
+                                       st),
                               "ncclRecv")) {
           (void)ncclGroupEnd();
           return rc;
         }
     }
     if (int rc = nccl_try(ncclGroupEnd(), "ncclGroupEnd")) return rc;
-    if (h1 > h0) {
-      hipLaunchKernelGGL(unpack_rows_kernel, dim3((unsigned)ceil_div((h1 - h0) * F, 256)), dim3(256), 0, xst, h1 - h0,
-                         F, brecv_pos + h0, recvbuf + h0 * F, ext + n_own * F);
-      WG_LAUNCH_CHECK();
-    }
-    if (L->tune.xdelay > 0 && n_halo > 0) {  // timing probe: the block's share of the simulated link time
-      hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, xst,
-                         (uint64_t)(100.0 * L->tune.xdelay * (double)(h1 - h0) / (double)n_halo));
-      WG_LAUNCH_CHECK();
-    }
-    return b == 0 ? mark(xst, false) : WG_OK;
-  }
-
-  // A streamed step: launch(st, &ph) per row block; when `out` is exchanged next (not the
-  // chain's last step) block b's rows leave on xs as soon as block b's kernel is done, and st
-  // waits for every block's exchange before the next step.  Hazards: the exchange of block b
-  // reads own rows of `out` block b (final) and writes out's halo rows, which this step does
-  // not touch (it reads `cur` and out's own rows of later blocks); xs issues the blocks in
-  // order after the previous step's kernels (bev[0] follows them on st).
-  template <typename StepFn>
-  int streamed_step(float* out, bool send, float* sendbuf, float* recvbuf, int64_t Fp, hipStream_t st,
-                    StepFn&& launch) {
-    if (!send) return launch(st, nullptr);
-    // last block first: internal rows are in descending length, so the last nnz-balanced block
-    // holds most of the rows (most of the rows sent) and the first the fewest -- computed last,
-    // its small exchange is the one left exposed (r02_s23 kernel trace)
-    for (int b = nblk - 1; b >= 0; --b) {
-      if (blk_rows[b + 1] > blk_rows[b]) {
-        PhaseArgs pb;
-        pb.block = b;
-        pb.row_begin = blk_rows[b];
-        pb.row_end = blk_rows[b + 1];
-        if (int rc = launch(st, &pb)) return rc;
-      }
-      WG_HIP_TRY(hipEventRecord(bev[b], st));
-      WG_HIP_TRY(hipStreamWaitEvent(xs, bev[b], 0));
-      if (int rc = exchange_block(b, out, sendbuf, recvbuf, Fp, xs)) return rc;
-    }
-    WG_HIP_TRY(hipEventRecord(xjoin, xs));
-    WG_HIP_TRY(hipStreamWaitEvent(st, xjoin, 0));
-    return WG_OK;
-  }
-
-  // One Chebyshev step that gathers from `cur` (own rows final, halo rows to be
-  // refreshed): without overlap, exchange then the step; with overlap, phase 1
-  // (own-column entries, into `part`) forks onto xs while the exchange runs on
-  // st; st joins phase 1, then phase 2 (halo entries + part, epilogue).  With
-  // two halo tiers, phase 3 (tier-0 halo entries, added into part) runs on xs
-  // between the tier-0 and the tier-1 exchange, and phase 2 takes the tier-1
-  // entries only.  The
-  // exchange stays on st, the stream a captured chain is recorded on (RCCL
-  // under a capture joined by a side stream crashed in the one-GPU loopback).
-  // Hazards: the exchange writes only cur's halo rows and reads its own rows;
-  // phase 1 reads only own rows; it forks after every earlier kernel on st (the
-  // previous step wrote cur's own rows and last read the other buffer's halo).
-  template <typename StepFn>
-  int step_with_exchange(float* cur, float* sendbuf, int64_t Fp, hipStream_t st, int slot, const int32_t* rsplit,
-                         const int32_t* rsplit2, double* part, StepFn&& launch) {
-    if (!rsplit) {
-      if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
-      return launch(st, nullptr);
-    }
-    PhaseArgs p1;
-    p1.phase = 1;
-    p1.rsplit = rsplit;
-    p1.part = part;
-    WG_HIP_TRY(hipEventRecord(xfork, st));
-    WG_HIP_TRY(hipStreamWaitEvent(xs, xfork, 0));
-    if (int rc = launch(xs, &p1)) return rc;
-    PhaseArgs p2 = p1;
-    p2.phase = 2;
-    if (rsplit2) {
-      // tier 0 (every peer's hottest rows) first; its entries (phase 3, added into part) run
-      // on xs after phase 1 while tier 1 is exchanged on st
-      if (int rc = exchange(cur, sendbuf, Fp, st, slot, 0)) return rc;
-      WG_HIP_TRY(hipEventRecord(xtier, st));
-      WG_HIP_TRY(hipStreamWaitEvent(xs, xtier, 0));
-      PhaseArgs p3 = p1;
-      p3.phase = 3;
-      p3.rsplit2 = rsplit2;
-      if (int rc = launch(xs, &p3)) return rc;
-      WG_HIP_TRY(hipEventRecord(xjoin, xs));
-      if (int rc = exchange(cur, sendbuf, Fp, st, slot, 1)) return rc;
-      p2.rsplit2 = rsplit2;
-    } else {
-      WG_HIP_TRY(hipEventRecord(xjoin, xs));
-      if (int rc = exchange(cur, sendbuf, Fp, st, slot)) return rc;
-    }
-    WG_HIP_TRY(hipStreamWaitEvent(st, xjoin, 0));
-    return launch(st, &p2);
+    return mark(st, false);
   }
 
   // the whole chain on stream st (eager, or being captured)
@@ -527,25 +351,7 @@ struct wg_dist_s {
     // lds: T ping-pong (own rows) + u ping-pong (padded column space); else T ping-pong over [own | halo]
     // F > 1 / weighted: heat sum by Clenshaw's recurrence (as wg_wavelet_features), X0 kept in its own buffer
     const bool clen = !lp && L->tune.clenshaw && K >= 1;
-    // two-phase steps overlapping the exchange (gather-kernel path, rows column-sorted, peers present)
-    const int32_t* rsplit = nullptr;
-    const int32_t* rsplit2 = nullptr;  // first tier-1 halo entry of each row (two tiers)
-    // (any halo: at world 1 too -- the one-GPU loopback test exercises the overlapped RCCL path)
-    if (!lp && L->tune.overlap && n_halo > 0 && (comm || ipc) && n_own > 0 && K >= 1) {
-      if (int rc = get_row_split(L, n_own, &rsplit)) return rc;
-      const int64_t n_hot = recv_off[world];
-      if (rsplit && tiers == 2 && n_hot > 0 && n_hot < n_halo)
-        if (int rc = get_row_split(L, n_own + n_hot, &rsplit2)) return rc;
-    }
-    overlapped = rsplit != nullptr;
-    // row-block streaming: the gather-kernel path over RCCL with peers, in-kernel split-row combine
-    const bool strm = !lp && !rsplit && nblk > 0 && comm && !ipc && K >= 2 && L->tune.inkernel_combine &&
-                      L->reordered;
-    streamed = strm;
-    const size_t rcv = strm ? ((size_t)std::max<int64_t>(n_halo, 1) * Fp + 63) / 64 * 64 : 0;
-    const size_t partf = rsplit ? 2 * own : 0;  // float64 row partials (n_own x Fp doubles)
-    const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd + (clen ? own : 0) +
-                        partf + rcv;
+    const size_t need = (lp ? 2 * own + (ipc ? 0 : 2 * ulen) : (ipc ? 0 : 2 * ext)) + own + snd + (clen ? own : 0);
     if (ws_floats < need) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       WG_HIP_TRY(hipStreamIsCapturing(st, &cs));
@@ -591,8 +397,6 @@ struct wg_dist_s {
     float* A[2] = {ipc ? region : take(ext), ipc ? region + slot_floats : take(ext)};
     float* sint = take(own);
     float* sendbuf = take(snd);
-    double* part = rsplit ? reinterpret_cast<double*>(take(partf)) : nullptr;  // 256-B aligned (take rounds)
-    float* recvbuf = strm ? take(rcv) : nullptr;
     int rc = WG_OK;
     if (sig) rc = ipc_wait_only(st);
     if (!rc) rc = launch_permute_pad(L, F, Fp, X0, A[0], st);
@@ -612,7 +416,7 @@ struct wg_dist_s {
       // unweighted graph (every rank created its shard with values == NULL): the stored b_k
       // are u_k = b_k * dinv, so the gathers read no CSR values (as wg_wavelet_features,
       // DESIGN.md 4.1) and the halo rows exchanged are u rows; X0 (phase 1) stays unscaled
-      const int useu = (L->unit && L->values_null && L->tune.uscale && !L->tune.gbuf && L->tune.hubf == 0 &&
+      const int useu = (L->unit && L->values_null && L->tune.uscale &&
                         L->tune.hot == 0) ? 1 : 0;
       // phase 1 exchanges and gathers u_0 = X0 * dinv (own rows scaled in place; x0 keeps X0)
       // value-free like every later phase.  The choice depends only on useu, which every rank
@@ -631,30 +435,18 @@ struct wg_dist_s {
         cl.uin = useu && (j >= 2 || u0);  // j == 1 gathers X0 itself, or u_0
         cl.uprev = useu && prev_stored;
         cl.uout = useu;                   // ignored on the final step (k == 0 writes S)
-        auto launch = [&](hipStream_t s2, const PhaseArgs* ph) {
-          return launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr, k == 0 ? nullptr : A[j & 1],
-                             k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, s2, false, nullptr, &cl, ph);
-        };
-        if (strm) {  // phase 1's exchange (X0) whole; each later one streamed by the step before it
-          if (j == 1) rc = exchange(cur, sendbuf, Fp, st, 0);
-          if (!rc) rc = streamed_step(A[j & 1], k > 0, sendbuf, recvbuf, Fp, st, launch);
-        } else {
-          rc = step_with_exchange(cur, sendbuf, Fp, st, (j - 1) & 1, rsplit, rsplit2, part, launch);
-        }
+        rc = exchange(cur, sendbuf, Fp, st, (j - 1) & 1);
+        if (!rc)
+          rc = launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr, k == 0 ? nullptr : A[j & 1],
+                           k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, st, false, nullptr, &cl);
       }
     } else {
       for (int32_t k = 1; k <= K && !rc; ++k) {
         float* cur = A[(k - 1) & 1];
-        auto launch = [&](hipStream_t s2, const PhaseArgs* ph) {
-          return launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr,
-                             1.0, std::exp(-s * (double)k), s2, false, nullptr, nullptr, ph);
-        };
-        if (strm) {  // step 1's exchange (T_0) whole; each later one streamed by the step before it
-          if (k == 1) rc = exchange(cur, sendbuf, Fp, st, 0);
-          if (!rc) rc = streamed_step(A[k & 1], k < K, sendbuf, recvbuf, Fp, st, launch);
-        } else {
-          rc = step_with_exchange(cur, sendbuf, Fp, st, (k - 1) & 1, rsplit, rsplit2, part, launch);
-        }
+        rc = exchange(cur, sendbuf, Fp, st, (k - 1) & 1);
+        if (!rc)
+          rc = launch_step(L, k, Fp, cur, k >= 2 ? A[k & 1] : nullptr, k == K ? nullptr : A[k & 1], sint, nullptr,
+                           1.0, std::exp(-s * (double)k), st);
       }
     }
     if (!rc && sig) rc = ipc_signal(st);  // phase K
@@ -675,24 +467,17 @@ int wg_dist_unique_id(void* out) {
 
 int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world, const int32_t* send_rows,
                    const int64_t* send_counts, const int64_t* recv_counts, wg_dist_t* out) {
-  return wg_dist_create_tiered(L, unique_id, rank, world, 1, send_rows, send_counts, recv_counts, out);
-}
-
-int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world, int32_t tiers,
-                          const int32_t* send_rows, const int64_t* send_counts, const int64_t* recv_counts,
-                          wg_dist_t* out) {
   if (!out) return fail(WG_ERR_INVALID, "wg_dist_create: out is NULL");
   *out = nullptr;
-  if (!L || world < 1 || rank < 0 || rank >= world || !send_counts || !recv_counts || tiers < 1 || tiers > 2)
-    return fail(WG_ERR_INVALID, "wg_dist_create: bad arguments (rank=%d world=%d tiers=%d)", rank, world, tiers);
+  if (!L || world < 1 || rank < 0 || rank >= world || !send_counts || !recv_counts)
+    return fail(WG_ERR_INVALID, "wg_dist_create: bad arguments (rank=%d world=%d)", rank, world);
   auto* D = new wg_dist_s();
   D->L = L;
   D->rank = rank;
   D->world = world;
-  D->tiers = tiers;
   D->n_own = L->n_rows;
   D->n_cols = L->n_cols;
-  const int64_t nc = (int64_t)tiers * world;
+  const int64_t nc = world;
   D->send_cnt.assign(send_counts, send_counts + nc);
   D->recv_cnt.assign(recv_counts, recv_counts + nc);
   D->send_off.assign(nc + 1, 0);
@@ -700,8 +485,7 @@ int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank,
   for (int64_t i = 0; i < nc; ++i) {
     if (D->send_cnt[i] < 0 || D->recv_cnt[i] < 0) {
       delete D;
-      return fail(WG_ERR_INVALID, "wg_dist_create: negative count for (tier %d, peer %d)", (int)(i / world),
-                  (int)(i % world));
+      return fail(WG_ERR_INVALID, "wg_dist_create: negative count for peer %d", (int)i);
     }
     D->send_off[i + 1] = D->send_off[i] + D->send_cnt[i];
     D->recv_off[i + 1] = D->recv_off[i] + D->recv_cnt[i];
@@ -709,7 +493,7 @@ int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank,
   D->n_send = D->send_off[nc];
   D->n_halo = D->recv_off[nc];
   if (D->n_halo > 0 && D->n_own + D->n_halo == L->n_cols) {
-    // the halo groups (one per (tier, peer), each in descending degree: wats_hip/dist.py) for
+    // the halo groups (one per peer, each in descending degree: wats_hip/dist.py) for
     // the F = 1 hub plan of a shard; plans built before this point are dropped
     L->halo_off.assign(D->recv_off.begin(), D->recv_off.end());
     release_lds1(L);
@@ -726,12 +510,8 @@ int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank,
       rc = fail(WG_ERR_HIP, "wg_dist_create: send_rows copy");
   }
   if (!rc && (hipStreamCreateWithFlags(&D->cap, hipStreamNonBlocking) != hipSuccess ||
-              create_exchange_stream(&D->xs) != hipSuccess ||
               hipEventCreateWithFlags(&D->fork, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&D->xfork, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&D->xjoin, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&D->xtier, hipEventDisableTiming) != hipSuccess))
+              hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess))
     rc = fail(WG_ERR_HIP, "wg_dist_create: stream/event");
   if (!rc && unique_id) {  // NULL: no RCCL communicator (one-sided IPC exchange, wg_dist_ipc_*)
     ncclUniqueId id;
@@ -773,31 +553,6 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   if (!D->comm && !D->ipc && (D->n_send > 0 || D->n_halo > 0 || D->world > 1))
     return fail(WG_ERR_INVALID, "wg_dist_wavelet_features: no exchange (no RCCL id given and IPC not connected)");
   hipStream_t st = as_stream(stream_);
-  if (D->cap_reserve != D->L->tune.cu_reserve) {
-    // the compute stream with `cu_reserve` CUs (spread over the chip) masked off, so the exchange
-    // stream's kernels find free CUs while a step kernel's backlog is dispatched
-    WG_HIP_TRY(hipDeviceSynchronize());
-    if (D->exec) {
-      (void)hipGraphExecDestroy(D->exec);
-      D->exec = nullptr;
-    }
-    (void)hipStreamDestroy(D->cap);
-    D->cap = nullptr;
-    const int r = D->L->tune.cu_reserve;
-    int dev = 0, n_cu = 0;
-    WG_HIP_TRY(hipGetDevice(&dev));
-    WG_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    if (r > 0 && r < n_cu) {
-      std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
-      for (int c = 0; c < n_cu; ++c)
-        if ((int64_t)(c + 1) * r / n_cu == (int64_t)c * r / n_cu) mask[c / 32] |= 1u << (c % 32);
-      WG_HIP_TRY(hipExtStreamCreateWithCUMask(&D->cap, (uint32_t)mask.size(), mask.data()));
-    } else {
-      WG_HIP_TRY(hipStreamCreateWithFlags(&D->cap, hipStreamNonBlocking));
-    }
-    D->cap_reserve = r;
-    D->warm = 0;
-  }
   const GraphKey key{X0, S, H, F, K, s, D->L->tune_gen};
   if (!(key == D->key)) {
     if (D->exec) {
@@ -809,14 +564,12 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
     D->warm = 0;
   }
   // eager: profiling (per-step events), graphs disabled, or the first call with
-  // these arguments (it builds the kernel plans and the workspace)
-  // streamed chains run eagerly (RCCL on the side stream under capture is not used)
-  // Either way the chain runs on the handle's own non-blocking stream (cap), joined to the
-  // caller's: on the legacy null stream the step kernels would wait for every blocking
-  // stream's work, RCCL's included, and never overlap the exchange stream.
+  // these arguments (it builds the kernel plans and the workspace).  Either way the chain
+  // runs on the handle's own non-blocking stream (cap), joined to the caller's: on the legacy
+  // null stream the step kernels would wait for every blocking stream's work.
   WG_HIP_TRY(hipEventRecord(D->fork, st));
   WG_HIP_TRY(hipStreamWaitEvent(D->cap, D->fork, 0));
-  if (!D->use_graph || D->L->prof || D->warm == 0 || (D->nblk > 0 && D->comm && !D->ipc)) {
+  if (!D->use_graph || D->L->prof || D->warm == 0) {
     const int rc = D->chain(X0, F, K, s, S, H, D->cap);
     if (!rc) ++D->warm;
     WG_HIP_TRY(hipEventRecord(D->join, D->cap));
@@ -901,8 +654,8 @@ int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src)
   if (int rc = dmalloc(&D->peer_flags, (size_t)D->world)) return rc;
   WG_HIP_TRY(hipMemcpy(D->peer_flags, pf.data(), sizeof(int64_t*) * D->world, hipMemcpyHostToDevice));
   std::vector<int32_t> owner(D->n_halo);
-  for (int64_t g = 0; g < (int64_t)D->tiers * D->world; ++g)
-    for (int64_t i = D->recv_off[g]; i < D->recv_off[g + 1]; ++i) owner[i] = (int32_t)(g % D->world);
+  for (int q = 0; q < D->world; ++q)
+    for (int64_t i = D->recv_off[q]; i < D->recv_off[q + 1]; ++i) owner[i] = (int32_t)q;
   if (D->n_halo > 0) {
     if (int rc = dmalloc(&D->halo_owner, (size_t)D->n_halo)) return rc;
     if (int rc = dmalloc(&D->halo_src, (size_t)D->n_halo)) return rc;
@@ -929,125 +682,16 @@ int wg_dist_status(wg_dist_t D, int32_t* timed_out) {
   return WG_OK;
 }
 
-int wg_dist_stream_blocks(wg_dist_t D, int32_t n_blocks) {
-  if (!D || n_blocks < 0 || n_blocks > 64) return fail(WG_ERR_INVALID, "wg_dist_stream_blocks: bad arguments");
-  wg_laplacian_s* L = D->L;
-  if (n_blocks > 0 && (!D->comm || D->ipc || D->tiers != 1))
-    return fail(WG_ERR_UNSUPPORTED, "wg_dist_stream_blocks: needs the RCCL exchange with one halo tier");
-  if (n_blocks > 0 && !L->reordered)
-    return fail(WG_ERR_UNSUPPORTED, "wg_dist_stream_blocks: the operator's rows are not length-ordered");
-  WG_HIP_TRY(hipDeviceSynchronize());
-  if (D->exec) {
-    (void)hipGraphExecDestroy(D->exec);
-    D->exec = nullptr;
-  }
-  D->warm = 0;
-  for (hipEvent_t e : D->bev) (void)hipEventDestroy(e);
-  D->bev.clear();
-  (void)hipFree(D->bsend_rows);
-  (void)hipFree(D->brecv_pos);
-  D->bsend_rows = nullptr;
-  D->brecv_pos = nullptr;
-  D->nblk = 0;
-  if (n_blocks == 0) return WG_OK;
-  const int world = D->world;
-  const int64_t n = D->n_own;
-  // nnz-balanced blocks of internal rows
-  std::vector<int32_t> rp(n + 1);
-  WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
-  std::vector<int64_t> bounds(n_blocks + 1, n);
-  bounds[0] = 0;
-  for (int b = 1; b < n_blocks; ++b) {
-    const int64_t target = (int64_t)rp[n] * b / n_blocks;
-    bounds[b] = std::max<int64_t>(bounds[b - 1], std::lower_bound(rp.begin(), rp.end(), (int32_t)target) - rp.begin());
-    bounds[b] = std::min<int64_t>(bounds[b], n);
-  }
-  auto block_of = [&](int32_t row) {
-    return (int)(std::upper_bound(bounds.begin(), bounds.end(), (int64_t)row) - bounds.begin()) - 1;
-  };
-  // my send rows by (block, peer), stable within each peer's list; their block ids to the peers
-  std::vector<int32_t> srows(D->n_send);
-  if (D->n_send)
-    WG_HIP_TRY(hipMemcpy(srows.data(), D->send_rows, sizeof(int32_t) * D->n_send, hipMemcpyDeviceToHost));
-  std::vector<int32_t> sblk(D->n_send);
-  for (int64_t i = 0; i < D->n_send; ++i) sblk[i] = block_of(srows[i]);
-  const size_t ng = (size_t)n_blocks * world;
-  std::vector<int64_t> scnt(ng, 0), rcnt(ng, 0);
-  std::vector<int32_t> bsend;
-  bsend.reserve(D->n_send);
-  for (int b = 0; b < n_blocks; ++b)
-    for (int q = 0; q < world; ++q) {
-      const int64_t before = (int64_t)bsend.size();
-      for (int64_t i = D->send_off[q]; i < D->send_off[q + 1]; ++i)
-        if (sblk[i] == b) bsend.push_back(srows[i]);
-      scnt[(size_t)b * world + q] = (int64_t)bsend.size() - before;
-    }
-  // the block id of every halo row, from its owner (same order as the owner's send list to me)
-  int32_t* d_sblk = nullptr;
-  int32_t* d_rblk = nullptr;
-  int rc = dmalloc(&d_sblk, (size_t)std::max<int64_t>(1, D->n_send));
-  if (!rc) rc = dmalloc(&d_rblk, (size_t)std::max<int64_t>(1, D->n_halo));
-  if (!rc && D->n_send &&
-      hipMemcpy(d_sblk, sblk.data(), sizeof(int32_t) * D->n_send, hipMemcpyHostToDevice) != hipSuccess)
-    rc = fail(WG_ERR_HIP, "wg_dist_stream_blocks: copy");
-  if (!rc) rc = nccl_try(ncclGroupStart(), "ncclGroupStart");
-  for (int q = 0; q < world && !rc; ++q) {
-    if (D->send_cnt[q] > 0)
-      rc = nccl_try(ncclSend(d_sblk + D->send_off[q], (size_t)D->send_cnt[q], ncclInt32, q, D->comm, D->xs), "ncclSend");
-    if (!rc && D->recv_cnt[q] > 0)
-      rc = nccl_try(ncclRecv(d_rblk + D->recv_off[q], (size_t)D->recv_cnt[q], ncclInt32, q, D->comm, D->xs), "ncclRecv");
-  }
-  if (!rc) rc = nccl_try(ncclGroupEnd(), "ncclGroupEnd");
-  std::vector<int32_t> rblk(D->n_halo);
-  if (!rc && hipStreamSynchronize(D->xs) != hipSuccess) rc = fail(WG_ERR_HIP, "wg_dist_stream_blocks: sync");
-  if (!rc && D->n_halo &&
-      hipMemcpy(rblk.data(), d_rblk, sizeof(int32_t) * D->n_halo, hipMemcpyDeviceToHost) != hipSuccess)
-    rc = fail(WG_ERR_HIP, "wg_dist_stream_blocks: copy");
-  (void)hipFree(d_sblk);
-  (void)hipFree(d_rblk);
-  if (rc) return rc;
-  // receive positions by (block, sender), stable within each sender's group (the sender's order)
-  std::vector<int32_t> rpos;
-  rpos.reserve(D->n_halo);
-  for (int b = 0; b < n_blocks; ++b)
-    for (int q = 0; q < world; ++q) {
-      const int64_t before = (int64_t)rpos.size();
-      for (int64_t i = D->recv_off[q]; i < D->recv_off[q + 1]; ++i) {
-        if (rblk[i] < 0 || rblk[i] >= n_blocks)
-          return fail(WG_ERR_INVALID, "wg_dist_stream_blocks: peer %d sent block %d (of %d)", q, rblk[i], n_blocks);
-        if (rblk[i] == b) rpos.push_back((int32_t)i);
-      }
-      rcnt[(size_t)b * world + q] = (int64_t)rpos.size() - before;
-    }
-  D->bsend_off.assign(ng + 1, 0);
-  D->brecv_off.assign(ng + 1, 0);
-  for (size_t i = 0; i < ng; ++i) {
-    D->bsend_off[i + 1] = D->bsend_off[i] + scnt[i];
-    D->brecv_off[i + 1] = D->brecv_off[i] + rcnt[i];
-  }
-  if (D->bsend_off[ng] != D->n_send || D->brecv_off[ng] != D->n_halo)
-    return fail(WG_ERR_INVALID, "wg_dist_stream_blocks: block lists do not cover the exchange");
-  if (int rc2 = dmalloc(&D->bsend_rows, (size_t)std::max<int64_t>(1, D->n_send))) return rc2;
-  if (int rc2 = dmalloc(&D->brecv_pos, (size_t)std::max<int64_t>(1, D->n_halo))) return rc2;
-  if (D->n_send) WG_HIP_TRY(hipMemcpy(D->bsend_rows, bsend.data(), sizeof(int32_t) * D->n_send, hipMemcpyHostToDevice));
-  if (D->n_halo) WG_HIP_TRY(hipMemcpy(D->brecv_pos, rpos.data(), sizeof(int32_t) * D->n_halo, hipMemcpyHostToDevice));
-  D->bev.resize(n_blocks);
-  for (auto& e : D->bev) WG_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  D->blk_rows = bounds;
-  D->nblk = n_blocks;
-  return WG_OK;
-}
-
 int wg_dist_info(wg_dist_t D, int64_t* out) {
   if (!D || !out) return fail(WG_ERR_INVALID, "wg_dist_info: NULL argument");
-  out[0] = D->overlapped ? 1 : (D->streamed ? 2 : 0);
+  out[0] = 0;  // exchange, then the step (the overlap variants of round 2 are removed)
   out[1] = D->n_own;
   out[2] = D->n_halo;
   out[3] = D->n_send;
   out[4] = D->world;
   out[5] = D->ipc ? 1 : (D->comm ? 2 : 0);
   out[6] = D->exec ? 1 : 0;
-  out[7] = D->tiers;
+  out[7] = 1;  // halo tiers
   return WG_OK;
 }
 

@@ -65,13 +65,12 @@ struct ChunkDesc {  // one workgroup's share of a split row
 
 struct Plan {
   SegTable tab{};
-  int64_t row0 = 0, row1 = 0;   // the rows planned (row-block plans: a block of internal rows)
+  int64_t row0 = 0, row1 = 0;   // the rows planned
   Seg* d_segs = nullptr;        // device copy of tab.s (read with scalar loads)
   int32_t n_chunks = 0;
   int32_t width = 0;            // LF * VEC doubles per partial
   int32_t nw = 4;               // waves per workgroup of the step kernel
   int32_t hot = 0;              // F == 1: columns [0, hot) of T_{k-1} staged in LDS (0 = off)
-  int32_t hubf = 0;             // F > 1: rows [0, hubf) of the gathered tile staged in LDS (0 = off)
   int32_t n_split = 0;          // split rows = internal rows [0, n_split)
   ChunkDesc* chunks = nullptr;  // device [n_chunks]
   double* partial = nullptr;    // device [n_chunks][width]
@@ -120,8 +119,6 @@ struct Lds1Plan {
   // ranges; the kernel reads remapped columns hcol (hub column -> its LDS slot, any
   // other column c -> c + hub, gathered from u[c])
   int32_t* hcol = nullptr;    // device [nnz + 4]
-  int32_t* hsplit = nullptr;  // device [n]: first entry of each row with column >= hub (plain hub: the
-                              // hub columns are each row's prefix, rows column-sorted)
   int4* hranges = nullptr;    // device [n_hranges]: {u begin, LDS slot begin, length, 0}
   int32_t n_hranges = 0;
   std::string text;
@@ -134,7 +131,7 @@ struct Lds1Plan {
 // blocks of 64 or 128, columns in tiles of 32; each (row block, column tile) pair holding at
 // least tile_th entries is a dense block, summed on the matrix cores from its row masks of
 // 32 bits; the rest of each row (its "tail") comes first in the row's range of
-// tcol and is gathered by the step kernel (phases 4, or 1 + 6), which adds the blocks' sums.
+// tcol and is gathered by the step kernel (phase 4), which adds the blocks' sums.
 struct TilePlan {
   int64_t n_plan = 0;          // rows planned: [0, n_plan)
   int32_t rows = 64;           // rows per row block (64 or 128: 4 or 8 waves of 16 rows)
@@ -147,9 +144,8 @@ struct TilePlan {
   int4* multi = nullptr;       // device [n_multi]: {row block, first slot, slots, 0}
   int32_t* tcol = nullptr;     // device [nnz]: each row's tail entries first (the rest of its range unused)
   int32_t* tsplit = nullptr;   // device [n_rows]: end of each row's tail (== row end: no dense entries)
-  int32_t width = 0;           // doubles per row of part / part2 / slots
+  int32_t width = 0;           // doubles per row of part / slots
   double* part = nullptr;      // device [n_rows][width]: the dense blocks' sums
-  double* part2 = nullptr;     // device [n_rows][width]: the tail sums (tiles_overlap)
   double* slots = nullptr;     // device [n_slots][rows][width]
   std::string text;
   void release();
@@ -160,16 +156,14 @@ struct Tuning {
   int32_t iter = 0;          // team mode: target nonzeros per lane sub-group
   int32_t block_iter = 0;    // block mode: rows up to NW*G*block_iter nonzeros get one workgroup
   int32_t chunk_iter = 0;    // split mode: NW*G*chunk_iter nonzeros per workgroup chunk
-  int32_t nt = -1;           // store hints: 4 = nt T_k / S stores, 8 = write-through (sc1) T_k stores; -1 = auto (4 when a step's T_k + S
-                             // streams exceed 64 MB, else 0: the next steps re-read them)
+  int32_t nt = -1;           // store hints: 4 = nt T_k / S stores, 8 = write-through (sc1) T_k stores;
+                             // -1 = auto (8; step.hip)
   int32_t tile_f = 0;        // max signal columns per launch (0 = 64*VEC)
   int32_t bcast = 1;         // F > 1: sub-group cooperative index loads (ds_bpermute broadcast)
   int32_t vidx = -1;         // F == 1: 16-B aligned int4/float4 index loads; -1 = auto (on for nnz >= 16 M)
   int32_t waves = 4;         // waves per step-kernel workgroup: 4, 8 or 16
   int32_t hot = 0;           // F == 1: LDS hot-column cache size (columns), 0 = off
-  int64_t seg_mask = -1;     // timing attribution only: launch only these segments
-  int32_t gbuf = 0;          // F > 1: branch-free raw-buffer gathers (accumulate_bcast_buf); no gain measured
-  int32_t hubf = 0;          // F > 1: rows [0, hubf) of T_{k-1} staged in LDS by a persistent kernel (0 = off)
+  int64_t seg_mask = -1;     // timing attribution only (-DWG_TIMING_PROBES): launch only these segments
   int32_t inkernel_combine = 1;  // split rows: last-arriving chunk combines (sc1 hand-off) vs combine_kernel
   int32_t lds = 3;           // F == 1, unit weights: LDS kernel (0 = off, 1 = row teams, 2 = chunk windows, 3 = auto)
   int32_t lds_cb = 32768;    // LDS floats per column block (multiple of 32, <= 40960)
@@ -181,33 +175,20 @@ struct Tuning {
   int32_t fuse_finalize = 1;  // wavelet_features: closed rows in the permute-in, S / H from the last step
   int32_t clenshaw = 1;      // wavelet_features (F > 1 / weighted): heat sum by Clenshaw's recurrence (no S stream)
   int32_t uscale = 1;        // Clenshaw on unweighted graphs: carry u = b * dinv, gathers read no CSR values
-  int32_t hub_vidx = 0;      // hub teams: 1 = 16-B column loads, 4 consecutive entries per lane (s26, 8M R-MAT: 1725 vs 1299 us, off)
   int32_t hub_iter = 16;     // hub teams (lds mode 4): target entries per lane of a row team
   int32_t lds_perm = 1;      // windows: 1 = deal a segment's entries column-major over its chunks
-  int32_t overlap = 0;       // row-sharded chain: two-phase steps overlapping the halo exchange (dist.hip);
-                             // off by default: the split costs more than it hides
-  int32_t probe = 0;         // timing only: gathers + one output stream, no epilogue (results wrong)
-  int32_t cu_reserve = 0;    // sharded chain: CUs masked off the compute stream (left to the exchange)
-  int32_t xskip = 0;
-  int32_t hub_split = 0;     // hub teams on column-sorted rows: hub prefix and tail in separate loops
-                             // (8M R-MAT K=32: 1388 vs 1184 us per step interleaved, r02_s29: off)
-  int32_t hub_pipe = 0;      // hub teams: software-pipelined column ids and epilogue prefetch
-                             // (8M R-MAT K=32: 1224 vs 1197 us per step, r02_s31: off)
+  int32_t probe = 0;         // timing only (-DWG_TIMING_PROBES): gathers + one output stream, no epilogue
   int32_t hub_sell = 1;      // hub teams on plain hubs: column ids in SELL-64 order (coalesced id loads)
-  int32_t probe_colmask = 0; // timing only: hub teams fold tail columns into a 2^k-column window (results wrong)         // timing only: streamed row blocks skip their pack / RCCL / unpack
-  int32_t xdelay = 0;        // timing only: microseconds of simulated link time added to each sharded-chain
-                             // exchange (split over the halo tiers by rows; one spinning wave on the stream)
+  int32_t xdelay = 0;        // timing only (-DWG_TIMING_PROBES): microseconds of simulated link time per
+                             // sharded-chain exchange (one spinning wave on the stream)
   int32_t fpad = 0;          // internal signal width of F >= 3: 0 = auto (fewest cache lines per row), 4 / 8 / 16 = that multiple
   int32_t tiles = -1;        // hybrid step (tiles.hip): -1 = auto (unweighted, width % 16 == 0, >= 8 M nonzeros,
                              // >= 30 % of the entries in dense blocks), 0 = off, 1 = whenever it applies
   int32_t tile_th = 96;      // entries that make a (row block, 32-column tile) pair a dense block
   int32_t tile_max = 0;      // dense blocks per workgroup (longer row blocks split over slots);
                              // 0 = auto: 128 from 100 k rows, else 64 (tiles.hip, r02_s80-s81)
-  int32_t tiles_overlap = 0; // hybrid step: the tail gathers on a side stream beside the dense blocks
-                             // (Reddit-size F=41: 1176 vs 1136 us per step sequential, r02_tiles: off)
   int32_t tile_rows = 128;   // hybrid step: rows per row block (64 or 128)
-  int32_t probe_tailwin = 0; // timing only (results wrong): the hybrid step's tail columns folded into 1/n of the columns
-  int32_t xcd = 0;           // step kernel: XCD x runs the x-th contiguous eighth of the units
+  int32_t probe_tailwin = 0; // timing only (-DWG_TIMING_PROBES): the hybrid tail's columns folded into 1/n of them
   int32_t tile_rg = 1;       // hybrid step, 128-row blocks: 16-row groups per wave (1: 8 waves, 2: 4 waves)
   int32_t chain = -1;        // F == 1 small unweighted graphs: the whole chain in one launch (chain.hip); -1 = auto
                              // (<= 2^18 nonzeros, <= 24576 active rows), 0 = off, 1 = whenever it applies
@@ -277,8 +258,7 @@ struct wg_laplacian_s {
   int64_t n_closed = 0;       // purely isolated rows at the end: T_k = (-1)^k X0 (closed form)
   wg::Tuning tune;
   int64_t tune_gen = 0;       // bumped by every wg_laplacian_tune: captured chains (dist.hip) re-capture
-  std::map<int64_t, wg::Plan> plans;  // key: (LF * 8 + VEC) * 2 + active_only (...); row-block plans: + (block + 1) << 32
-  std::vector<int32_t> h_rowptr;      // host copy of the internal row pointers (row-block plans), lazily
+  std::map<int64_t, wg::Plan> plans;  // key: (LF * 8 + VEC) * 2 + active_only (...)
   // unweighted graph (every off-diagonal a_ij == 1): L_hat_ij = -dinv_i dinv_j
   // up to scipy's float32 rounding, so the F == 1 LDS kernel reads no values
   bool unit = false;
@@ -286,17 +266,12 @@ struct wg_laplacian_s {
   bool values_null = false;   // created with values == NULL (unweighted by construction: every shard of the
                               // graph agrees, so a row-sharded chain may exchange u = b * dinv)
   double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
-  int32_t* rsplit = nullptr;  // [n_rows] first halo entry of each row (two-phase steps), lazily built
-  int32_t* rsplit2 = nullptr;  // [n_rows] first entry with column >= rsplit2_at (two halo tiers)
-  int64_t rsplit2_at = -1;
   std::vector<int64_t> halo_off;  // row shard: halo columns [n_rows + halo_off[q], n_rows + halo_off[q+1])
                                   // come from peer q, each group in descending degree (wg_dist_create)
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
   bool lds1_failed[2] = {false, false};        // not applicable (too many blocks): use the gather kernel
   wg::TilePlan* tiles[2] = {nullptr, nullptr};  // [active_only] hybrid step plans (released with lds1)
   bool tiles_failed[2] = {false, false};
-  hipStream_t side = nullptr;                   // hybrid step: the tail gathers' stream (tiles_overlap)
-  hipEvent_t side_fork = nullptr, side_join = nullptr;
   // workspace for wg_wavelet_features
   float* ws = nullptr;
   size_t ws_floats = 0;
@@ -323,8 +298,7 @@ int sort_row_columns(wg_laplacian_s* L, hipStream_t stream);
 // step.hip
 int pick_vec(int64_t F, std::initializer_list<const void*> ptrs);
 // hybrid: the plan of the hybrid step's tail (tiles.hip; its own key and larger work units)
-int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, int block = -1, int64_t r0 = 0,
-             int64_t r1 = 0, bool hybrid = false);
+int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, bool hybrid = false);
 // S_out (finalize fused into the last step; needs S, H and F within one tile):
 // the rows' final S and H go to caller row perm[row] of S_out / H
 // Clenshaw form of the heat sum (wavelet_features): a step computes
@@ -339,33 +313,9 @@ struct ClenArgs {
   // uin: xm1 is u, uprev: xm2 is u, uout: write u (not on the final step)
   int uin = 0, uprev = 0, uout = 0;
 };
-// Two-phase step (the row-sharded chain overlaps the halo exchange with phase 1): phase 1
-// sums each row's own-column entries [row start, rsplit[row]) into part (float64, row
-// stride F, no epilogue); phase 2 sums the halo entries [rsplit[row], row end), adds part
-// and runs the step's epilogue.  phase 0 = the whole row in one launch.  Two halo tiers:
-// phase 3 adds the tier-0 entries [rsplit[row], rsplit2[row]) into part (between 1 and 2),
-// and phase 2 sums [rsplit2[row], row end).
-struct PhaseArgs {
-  // row block (phase 0 only): the step on internal rows [row_begin, row_end) alone, with its own
-  // plan (block id `block` >= 0); block < 0 = every row
-  int block = -1;
-  int64_t row_begin = 0, row_end = 0;
-  int phase = 0;
-  const int32_t* rsplit = nullptr;   // [n_rows] first entry with column >= n_rows (rows column-sorted)
-  const int32_t* rsplit2 = nullptr;  // [n_rows] first tier-1 halo entry (two tiers), else nullptr
-  double* part = nullptr;            // [n_rows][F]
-  // hybrid step (internal to launch_step, tiles.hip): phases 1 / 4 / 6 over the tail-first
-  // column array `col` (rsplit = each row's tail end); part2 = the dense blocks' sums (phase 6)
-  const int32_t* col = nullptr;
-  const double* part2 = nullptr;
-};
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
-                float* S_out = nullptr, const ClenArgs* cl = nullptr, const PhaseArgs* ph = nullptr);
-// per internal row, the first entry whose column is >= split (n_rows: the first halo entry;
-// n_rows + the tier-0 halo rows: the first tier-1 entry); built once per split (synchronous),
-// nullptr when rows are not column-sorted
-int get_row_split(wg_laplacian_s* L, int64_t split, const int32_t** out);
+                float* S_out = nullptr, const ClenArgs* cl = nullptr);
 int launch_finalize(wg_laplacian_s* L, int64_t F, const float* Sint, const float* X0int, double closed_coef,
                     float* S, float* H, hipStream_t stream, int64_t ldi = 0);  // ldi: internal row stride (0 = F)
 // the internal signal width of an F-column chain: odd / 4-unaligned F >= 3 is
@@ -388,7 +338,6 @@ bool tiles_wanted(const wg_laplacian_s* L, int64_t F);
 int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out);
 int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream);
 void release_tiles(wg_laplacian_s* L);
-int side_stream(wg_laplacian_s* L);  // creates L->side and its fork / join events once
 // u = x * dinv for rows [0, n) of an F-wide signal (in place allowed): the hybrid chain's first
 // step gathers u_0 = X0 * dinv value-free like every later step
 int launch_scale_rows(wg_laplacian_s* L, int64_t n, int64_t F, const float* x, float* u, hipStream_t stream);

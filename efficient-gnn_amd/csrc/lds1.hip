@@ -53,11 +53,8 @@ struct Lds1Args {
   int32_t gshift;       // mode 4: a tail column c (>= hub) is gathered from u[c - gshift] (0, or hub on a shard)
   int32_t n_hranges;    // mode 4 on a shard: LDS slots filled from these ranges of u (0: slots = u[0, hub))
   const int4* hranges;
-  const int32_t* hsplit;  // mode 4, plain hub: first tail entry of each row (nullable)
   const int2* gsell;    // mode 4, SELL-64 ids: per group {first 64-slot line, turns} (nullable)
   const int32_t* csell;
-  int32_t pipe;         // mode 4: software-pipelined column ids + epilogue prefetch (tuning key "hub_pipe")
-  int32_t colmask;      // timing probe (knob "probe_colmask"): tail columns folded into [hub, hub + colmask]
   const int2* groups;
   const int4* wgs;
   const float* u_in;   // u_{k-1}, n_cols (padded to a multiple of 32)
@@ -76,34 +73,6 @@ struct Lds1Args {
   double alpha0;
   double alpha_k;
 };
-
-// the epilogue's row operands, loaded before the row's gathers so their latency overlaps them
-struct Lds1Pre {
-  double di;
-  float xo, x2, s;
-  bool iso;
-};
-__device__ __forceinline__ Lds1Pre lds1_pre(const Lds1Args& a, int32_t row) {
-  Lds1Pre p;
-  p.di = a.dinv[row];
-  p.xo = a.xm1[row];
-  p.iso = a.iso[row] != 0;
-  p.x2 = a.k == 1 ? 0.0f : a.xm2[row];
-  p.s = (a.S && a.k != 1) ? a.S[row] : 0.0f;
-  return p;
-}
-// lds1_epilogue with the operands already loaded (same arithmetic, same order)
-__device__ __forceinline__ void lds1_finish(const Lds1Args& a, int32_t row, double acc, const Lds1Pre& p) {
-  double off = -p.di * acc;
-  if (p.iso) off -= (double)p.xo;  // L_hat_ii = -1
-  const double t = (a.k == 1) ? off : 2.0 * off - (double)p.x2;
-  if (a.xk) __builtin_nontemporal_store((float)t, a.xk + row);
-  if (a.u_out) a.u_out[row] = (float)(t * p.di);
-  if (a.S) {
-    const double s = (a.k == 1) ? a.alpha0 * (double)p.xo + a.alpha_k * t : (double)p.s + a.alpha_k * t;
-    __builtin_nontemporal_store((float)s, a.S + row);
-  }
-}
 
 // T_k,i = 2 (L_hat T_{k-1})_i - T_{k-2,i}  (k == 1: T_1 = L_hat T_0), S, u_k.
 __device__ __forceinline__ void lds1_epilogue(const Lds1Args& a, int32_t row, double acc) {
@@ -198,9 +167,6 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_lds1_kernel(Lds1Args a) {
 // columns, and the two are added (one of them is 0, so the sum is exact).
 // Row teams, row groups and the LDS counter as cheb_lds1_kernel; one column
 // block, so the epilogue runs in place.
-// VIDX: each lane takes 4 consecutive entries with one 16-B column load
-// (groups aligned to 4 entries in the padded CSR, masked to the row).
-template <bool VIDX>
 __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   __shared__ int s_next;
   constexpr uint32_t kDrop = 0x80000000u;
@@ -227,9 +193,7 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   const int32_t* __restrict__ col = a.gcol;
   const int32_t* __restrict__ rp = a.brp;
   const int32_t gs = a.gshift;
-  const int32_t cm = a.colmask;
   auto x_of = [&](int32_t c) {
-    if (cm) c = c >= H ? H + ((c - H) & cm) : c;  // timing probe only (results wrong)
     const float xl = u[min(c, H)];
     const uint32_t off = c >= H ? (uint32_t)(c - gs) * 4u : kDrop;
     const float xg = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
@@ -249,27 +213,7 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
     const int32_t row = gd.x + team;
     const bool act = team < nrows;
     double acc = 0.0;
-    if (act && VIDX) {
-      const int32_t e0 = rp[row], e1 = rp[row + 1];
-      for (int32_t qq = (e0 & ~3) + 4 * q; qq < e1; qq += 4 * ln) {
-        const int4 c4 = *reinterpret_cast<const int4*>(col + qq);
-        int32_t cc[4] = {c4.x, c4.y, c4.z, c4.w};
-        if (cm) {  // timing probe only (results wrong)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) cc[j] = cc[j] >= H ? H + ((cc[j] - H) & cm) : cc[j];
-        }
-        float x[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool ok = qq + j >= e0 && qq + j < e1;
-          const float xl = u[ok ? min(cc[j], H) : H];
-          const uint32_t off = (ok && cc[j] >= H) ? (uint32_t)(cc[j] - gs) * 4u : kDrop;
-          x[j] = xl + __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc += (double)x[j];
-      }
-    } else if (act && a.csell) {
+    if (act && a.csell) {
       // SELL-64 ids: turn i of this lane is slot (line + i) * 64 + lane -- the same entries in
       // the same order as the CSR walk below (pads: kPadCol, adding 0.0)
       const int2 gs = a.gsell[g];
@@ -285,60 +229,6 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
         acc += (double)x3;
       }
       for (; i < gs.y; ++i) acc += (double)x_of(cs[(int64_t)i * 64]);
-    } else if (act && a.hsplit) {
-      // hub columns are each row's prefix [e0, es): LDS reads only, then the tail with global
-      // loads only -- no dropped-offset loads through the address path for hub entries and
-      // no LDS reads for tail ones; each lane adds its entries in the same order as x_of's loop
-      const int32_t e1 = rp[row + 1];
-      const int32_t es = a.hsplit[row];
-      int32_t e = rp[row] + q;
-      for (; e + 3 * ln < es; e += 4 * ln) {
-        const int32_t c0 = col[e], c1 = col[e + ln], c2 = col[e + 2 * ln], c3 = col[e + 3 * ln];
-        const float x0 = u[c0], x1 = u[c1], x2 = u[c2], x3 = u[c3];
-        acc += (double)x0;
-        acc += (double)x1;
-        acc += (double)x2;
-        acc += (double)x3;
-      }
-      for (; e < es; e += ln) acc += (double)u[col[e]];
-      auto xg = [&](int32_t c) {
-        if (cm) c = H + ((c - H) & cm);  // timing probe only (results wrong)
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(c - gs) * 4u, 0, 0));
-      };
-      for (; e + 3 * ln < e1; e += 4 * ln) {
-        const int32_t c0 = col[e], c1 = col[e + ln], c2 = col[e + 2 * ln], c3 = col[e + 3 * ln];
-        const float x0 = xg(c0), x1 = xg(c1), x2 = xg(c2), x3 = xg(c3);
-        acc += (double)x0;
-        acc += (double)x1;
-        acc += (double)x2;
-        acc += (double)x3;
-      }
-      for (; e < e1; e += ln) acc += (double)xg(col[e]);
-    } else if (act && a.pipe) {
-      // software-pipelined: the next batch's 4 column ids load while this batch's gathers are
-      // in flight (one dependent round trip per batch, not two), and the epilogue's operands
-      // load first; a lane adds its entries in the same order (masked slots add 0.0)
-      const int32_t e0 = rp[row], e1 = rp[row + 1];
-      const int32_t last = max(e1 - 1, e0);
-      const Lds1Pre pre = lds1_pre(a, row);  // every lane of the team (no load behind a branch)
-      int32_t e = e0 + q;
-      int32_t c[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) c[j] = col[min(e + j * ln, last)];
-      while (e < e1) {
-        float x[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) x[j] = x_of(e + j * ln < e1 ? c[j] : kPadCol);
-        const int32_t en = e + 4 * ln;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = col[min(en + j * ln, last)];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc += (double)x[j];
-        e = en;
-      }
-      for (int o = ln >> 1; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
-      if (q == 0) lds1_finish(a, row, acc, pre);
-      continue;
     } else if (act) {
       const int32_t e1 = rp[row + 1];
       int32_t e = rp[row] + q;
@@ -376,20 +266,6 @@ __global__ void sell_fill_kernel(int32_t n_groups, const int2* __restrict__ grou
     const int32_t e = e0 + i * ln;
     dst[(int64_t)i * 64] = e < e1 ? col[e] : kPadCol;
   }
-}
-
-// first entry of each row whose column is >= hub (rows sorted by column)
-__global__ void hub_split_kernel(int32_t n, int32_t hub, const int32_t* __restrict__ rowptr,
-                                 const int32_t* __restrict__ col, int32_t* __restrict__ out) {
-  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int32_t lo = rowptr[i], hi = rowptr[i + 1];
-  while (lo < hi) {
-    const int32_t mid = lo + ((hi - lo) >> 1);
-    if (col[mid] < hub) lo = mid + 1;
-    else hi = mid;
-  }
-  out[i] = lo;
 }
 
 // a row shard's hub plan: column c -> its LDS slot when it is a hub column, else c + hub.
@@ -1041,11 +917,10 @@ int build_windows(wg_laplacian_s* L, Lds1Plan* p, const std::vector<int32_t>& cn
 
 void Lds1Plan::release() {
   for (void* p : {(void*)brp, (void*)bcol, (void*)groups, (void*)wgs, (void*)part, (void*)chunk, (void*)pos,
-                  (void*)wdesc, (void*)wblock, (void*)hcol, (void*)hranges, (void*)hsplit, (void*)gsell,
+                  (void*)wdesc, (void*)wblock, (void*)hcol, (void*)hranges, (void*)gsell,
                   (void*)csell})
     (void)hipFree(p);
   hcol = nullptr;
-  hsplit = nullptr;
   gsell = nullptr;
   csell = nullptr;
   hranges = nullptr;
@@ -1230,16 +1105,6 @@ int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out) {
       snprintf(p->sell_note, sizeof(p->sell_note), " sell_lines=%lld (ids %.2fx nnz)", (long long)lines,
                (double)lines * 64 / std::max<int64_t>(1, nnz_rows));
     }
-    if (!rc && !p->hcol && L->cols_sorted && L->tune.hub_split) {
-      // plain hub on column-sorted rows: each row's hub entries are a prefix
-      rc = dmalloc(&p->hsplit, (size_t)n);
-      if (!rc) {
-        hipLaunchKernelGGL(hub_split_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, nullptr, (int32_t)n,
-                           p->hub, L->rowptr, L->col, p->hsplit);
-        const hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) rc = fail(WG_ERR_HIP, "hub_split: %s", hipGetErrorString(e));
-      }
-    }
     if (rc) {
       p->release();
       delete p;
@@ -1354,12 +1219,11 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
   a.alpha0 = alpha0;
   a.alpha_k = alpha_k;
   if (p->mode == 4) {
-    static bool attr4[2] = {false, false};
-    const bool vx = L->tune.hub_vidx != 0;
-    if (!attr4[vx]) {
-      WG_HIP_TRY(hipFuncSetAttribute(vx ? (const void*)cheb_hub1_kernel<true> : (const void*)cheb_hub1_kernel<false>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
-      attr4[vx] = true;
+    static bool attr4 = false;
+    if (!attr4) {
+      WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_hub1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - 64));
+      attr4 = true;
     }
     a.brp = L->rowptr;
     a.gcol = p->hcol ? p->hcol : L->col;
@@ -1367,14 +1231,10 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
     a.u_bytes = (int32_t)(p->ulen * 4);
     a.gshift = p->hcol ? p->hub : 0;
     a.n_hranges = p->n_hranges;
-    a.hsplit = L->tune.hub_vidx ? nullptr : p->hsplit;
-    a.pipe = L->tune.hub_pipe;
-    a.gsell = L->tune.hub_vidx ? nullptr : p->gsell;
-    a.csell = L->tune.hub_vidx ? nullptr : p->csell;
-    a.colmask = L->tune.probe_colmask > 0 ? (int32_t)((1u << L->tune.probe_colmask) - 1u) : 0;
+    a.gsell = p->gsell;
+    a.csell = p->csell;
     a.hranges = p->hranges;
-    if (vx) hipLaunchKernelGGL(cheb_hub1_kernel<true>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
-    else hipLaunchKernelGGL(cheb_hub1_kernel<false>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
+    hipLaunchKernelGGL(cheb_hub1_kernel, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
     WG_LAUNCH_CHECK();
     return prof_mark(L, stream, false);
   }

@@ -520,11 +520,8 @@ wg_laplacian_s::~wg_laplacian_s() {
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   for (auto& kv : plans) kv.second.release();
   wg::release_lds1(this);
-  if (side_fork) (void)hipEventDestroy(side_fork);
-  if (side_join) (void)hipEventDestroy(side_join);
-  if (side) (void)hipStreamDestroy(side);
   for (void* p : {(void*)rowptr, (void*)col, (void*)val, (void*)iso, (void*)perm, (void*)iperm, (void*)rowsum,
-                  (void*)ws, (void*)dinv, (void*)rsplit, (void*)rsplit2})
+                  (void*)ws, (void*)dinv})
     (void)hipFree(p);
 }
 

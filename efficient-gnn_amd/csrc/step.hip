@@ -27,9 +27,8 @@
 //    need an agent-scope release per chunk (buffer_wbl2 of an XCD L2 full of
 //    the step's dirty lines: 1.3-2.2x slower for the whole step, DESIGN.md
 //    4.1).  inkernel_combine = 0 runs a separate combine_kernel instead.
-//  * Two-phase steps (row-sharded chain, dist.hip): phase 1 sums each row's
-//    own-column entries into a float64 row partial while the halo exchange
-//    runs; phase 2 sums the halo entries, adds the partial, runs the epilogue.
+//  * The hybrid step (tiles.hip) runs this kernel over each row's tail
+//    entries only (phase 4) and adds the dense blocks' float64 sums.
 // Row sums accumulate in float64 (products of two float32 are exact).
 #include <algorithm>
 #include <cmath>
@@ -44,7 +43,7 @@ namespace {
 
 // One work unit of the plan (a group of team rows, a block row or a split
 // chunk) processed by one workgroup of NW waves.
-template <int VEC, bool BCAST, int NW, bool HOT, bool HUB = false>
+template <int VEC, bool BCAST, int NW, bool HOT>
 __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restrict__ segs, int nseg, int32_t unit,
                                           int32_t H) {
   __shared__ double red[NW * 64 * VEC];
@@ -73,24 +72,20 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     const bool active = team < tpw && row < seg.end;
     EpiIn<VEC> in;
     if (active) {
-      if (ns == 0 && !to_part(a)) epi_prefetch<VEC>(a, row, fs, in);
+      if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
       int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
       phase_range(a, row, e0, e1);
       if constexpr (VEC == 1 && !HOT) {
         if (a.vidx && LF == 1) accumulate_vidx1(a, e0, e1, ns, LN, a.xm1, acc);
-        else acc_range<VEC, BCAST, HOT, HUB>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+        else acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
       } else {
-        acc_range<VEC, BCAST, HOT, HUB>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+        acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
       }
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
     if (active && ns == 0) {
-      if (to_part(a)) {
-        part_store<VEC>(a, row, fs, acc);
-      } else {
-        if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, fs, acc);
-        step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
-      }
+      part_add<VEC>(a, row, fs, acc);
+      step_epilogue<VEC>(a, row, fs, acc, in, team * TS);
     }
     return;
   }
@@ -116,17 +111,17 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
   const int sg = lane / LF;
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
-  if (seg.mode == 1 && threadIdx.x < LF && !to_part(a)) epi_prefetch<VEC>(a, row, threadIdx.x, in);
+  if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
   if constexpr (VEC == 1 && !HOT) {
     if (a.vidx && LF == 1) {
       // chunk-aligned ranges: for split chunks e0 is a multiple of CH (>= 4) from the row start, so
       // neighbouring chunks never both take an aligned 4-group (masking keeps the bounds exact anyway)
       accumulate_vidx1(a, e0, e1, wave * G + sg, NW * G, a.xm1, acc);
     } else if (sg < G) {
-      acc_range<VEC, BCAST, HOT, HUB>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+      acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
     }
   } else if (sg < G) {
-    acc_range<VEC, BCAST, HOT, HUB>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+    acc_range<VEC, BCAST, HOT>(a, e0 + wave * G + sg, e1, NW * G, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
   }
   reduce_subgroups<VEC>(acc, G, LF, 0, fs);
   if (lane < LF) {
@@ -144,12 +139,8 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       for (int j = 0; j < VEC; ++j) acc[j] += red[(w * LF + t) * VEC + j];
     }
     if (seg.mode == 1) {
-      if (to_part(a)) {
-        part_store<VEC>(a, row, t, acc);
-      } else {
-        if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, t, acc);
-        step_epilogue<VEC>(a, row, t, acc, in, 0);
-      }
+      part_add<VEC>(a, row, t, acc);
+      step_epilogue<VEC>(a, row, t, acc, in, 0);
     } else {
       double* p = a.partial + (int64_t)cid * (LF * VEC) + t * VEC;
 #pragma unroll
@@ -176,7 +167,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     if (s_last && threadIdx.x < LF) {
       const int t = threadIdx.x;
       EpiIn<VEC> in2;
-      if (!to_part(a)) epi_prefetch<VEC>(a, row, t, in2);
+      epi_prefetch<VEC>(a, row, t, in2);
       double sum[VEC];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) sum[j] = 0.0;
@@ -185,27 +176,17 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
 #pragma unroll
         for (int j = 0; j < VEC; ++j) sum[j] += __hip_atomic_load(pp + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (to_part(a)) {
-        part_store<VEC>(a, row, t, sum);
-      } else {
-        if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, t, sum);
-        step_epilogue<VEC>(a, row, t, sum, in2, 0);
-      }
+      part_add<VEC>(a, row, t, sum);
+      step_epilogue<VEC>(a, row, t, sum, in2, 0);
     }
   }
 }
 
 template <int VEC, bool BCAST, int NW>
 __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
-  // knob xcd (off): workgroups are dealt to the 8 XCDs round-robin; remap so that XCD x runs
-  // the contiguous x-th eighth of the plan's units.  Measured 3x slower on arxiv F=40: the units
-  // are in descending row length, so one XCD gets every hub row
-  int32_t unit = (int32_t)blockIdx.x;
-  if (a.xcd) {
-    const int32_t n = (int32_t)gridDim.x, q = n >> 3, r = n & 7, x = unit & 7;
-    unit = x * q + min(x, r) + (unit >> 3);
-  }
-  unit_body<VEC, BCAST, NW, false>(a, segs, nseg, unit, 0);
+  // units are dealt to the 8 XCDs round-robin (blockIdx order): the units are in descending row
+  // length, so an XCD-contiguous order gave one XCD every hub row (3x slower, r02_s65)
+  unit_body<VEC, BCAST, NW, false>(a, segs, nseg, (int32_t)blockIdx.x, 0);
 }
 
 // Persistent F == 1 variant: one workgroup per CU stages T_{k-1}[0, H) in LDS
@@ -217,24 +198,6 @@ __global__ __launch_bounds__(NW * 64) void cheb_step_hot_kernel(StepArgs a, cons
   __syncthreads();
   for (int32_t unit = blockIdx.x; unit < total_units; unit += gridDim.x) {
     unit_body<1, false, NW, true>(a, segs, nseg, unit, H);
-    __syncthreads();  // the block-mode LDS partials are reused by the next unit
-  }
-}
-
-// F > 1 persistent variant with the LDS hub: each workgroup stages rows
-// [0, hubf) of the gathered tile of T_{k-1} (plus a zero row) once, then walks
-// the plan's work units round-robin.
-template <int VEC, int NW>
-__global__ __launch_bounds__(NW * 64) void cheb_step_hub_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg,
-                                                                int32_t total_units) {
-  const int W = a.LF * VEC;
-  for (int32_t i = threadIdx.x; i < (a.hubf + 1) * W; i += NW * 64) {
-    const int32_t r = i / W, c = i - r * W;
-    g_hub_lds[i] = (r < a.hubf) ? a.xm1[(int64_t)r * a.ld + c] : 0.0f;
-  }
-  __syncthreads();
-  for (int32_t unit = blockIdx.x; unit < total_units; unit += gridDim.x) {
-    unit_body<VEC, true, NW, false, true>(a, segs, nseg, unit, 0);
     __syncthreads();  // the block-mode LDS partials are reused by the next unit
   }
 }
@@ -255,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
   const int64_t row = row0 + lr;
   const int width = LF * VEC;
   EpiIn<VEC> in;
-  if (!to_part(a)) epi_prefetch<VEC>(a, row, fs, in);
+  epi_prefetch<VEC>(a, row, fs, in);
   double acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
@@ -264,11 +227,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(StepArgs a, int32_t n_s
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] += p[j];
   }
-  if (to_part(a)) {
-    part_store<VEC>(a, row, fs, acc);
-    return;
-  }
-  if (a.phase == 2 || a.phase >= 4) part_add<VEC>(a, row, fs, acc);
+  part_add<VEC>(a, row, fs, acc);
   step_epilogue<VEC>(a, row, fs, acc, in, sg * LF);
 }
 
@@ -476,40 +435,10 @@ int launch_hot(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   return WG_OK;
 }
 
-template <int VEC, int NW>
-int launch_hub(const Plan& plan, const StepArgs& a, hipStream_t stream) {
-  static int n_cu = 0;
-  static bool attr_set = false;
-  if (!n_cu) {
-    int dev = 0;
-    WG_HIP_TRY(hipGetDevice(&dev));
-    WG_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  if (!attr_set) {
-    WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_step_hub_kernel<VEC, NW>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - NW * 64 * VEC * 8 - 64));
-    attr_set = true;
-  }
-  const size_t lds = (size_t)(a.hubf + 1) * a.LF * VEC * sizeof(float);
-  int per_cu = 0;  // resident workgroups per CU (registers and LDS): the persistent grid
-  WG_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)cheb_step_hub_kernel<VEC, NW>,
-                                                          NW * 64, lds));
-  const int grid = std::min<int>(plan.tab.total_blocks, n_cu * std::max(1, per_cu));
-  hipLaunchKernelGGL((cheb_step_hub_kernel<VEC, NW>), dim3(grid), dim3(NW * 64), lds, stream, a,
-                     (const Seg*)plan.d_segs, plan.tab.n, plan.tab.total_blocks);
-  WG_LAUNCH_CHECK();
-  return WG_OK;
-}
-
 template <int VEC>
 int launch_step_vec(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const SegTable& tab = plan.tab;
-  if (VEC == 4 && a.hubf > 0 && a.LF > 1 && a.bcast && tab.total_blocks > 0 && a.phase == 0) {
-    int rc = plan.nw == 16 ? launch_hub<4, 16>(plan, a, stream)
-             : plan.nw == 8 ? launch_hub<4, 8>(plan, a, stream)
-                            : launch_hub<4, 4>(plan, a, stream);
-    if (rc) return rc;
-  } else if (VEC == 1 && plan.hot > 0 && tab.total_blocks > 0 && a.phase == 0) {
+  if (VEC == 1 && plan.hot > 0 && tab.total_blocks > 0 && a.phase == 0) {
     int rc = plan.nw == 16 ? launch_hot<16>(plan, a, stream) : launch_hot<4>(plan, a, stream);
     if (rc) return rc;
   } else if (tab.total_blocks > 0) {
@@ -610,64 +539,31 @@ void default_knobs(const Tuning& t, int G, int64_t nnz, int* iter, int* block_it
 //   block rows: len <= 4G*block_iter       (one workgroup per row)
 //   split rows: longer                     (one workgroup per CH = 4G*chunk_iter nnz + combine_kernel)
 // Classification is by power-of-two length bucket (rows are sorted by length).
-//
-// Row-block plans (block >= 0): the same classification over internal rows [r0, r1) only (the
-// row-sharded chain streams each block's rows to the peers while the next block computes,
-// dist.hip); the block's split rows index rowchunks / arrivals from r0.
-int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, int block, int64_t r0, int64_t r1,
-             bool hybrid) {
+int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, bool hybrid) {
   active_only = active_only && L->reordered;
   const int NW = (L->tune.waves == 16 || L->tune.waves == 8) ? L->tune.waves : 4;
-  const bool ranged = block >= 0;
-  hybrid = hybrid && !ranged;
   const int64_t key = (int64_t)(((LF * 8 + VEC) * 2 + (active_only ? 1 : 0)) * 32 + NW +
-                                (L->tune.hot > 0 && !ranged ? (1 << 28) : 0) + (hybrid ? (1 << 29) : 0)) +
-                      (ranged ? ((int64_t)(block + 1) << 32) : 0);
+                                (L->tune.hot > 0 ? (1 << 28) : 0) + (hybrid ? (1 << 29) : 0));
   auto it = L->plans.find(key);
-  if (it != L->plans.end() && (!ranged || (it->second.row0 == r0 && it->second.row1 == r1))) {
+  if (it != L->plans.end()) {
     *out = &it->second;
     return WG_OK;
   }
-  if (it != L->plans.end()) {  // the block's rows changed: rebuild
-    it->second.release();
-    L->plans.erase(it);
-  }
-  if (ranged && (!L->reordered || r0 < 0 || r1 > L->n_rows || r1 <= r0))
-    return fail(WG_ERR_INVALID, "row-block plan: rows [%lld, %lld) of %lld (reordered %d)", (long long)r0,
-                (long long)r1, (long long)L->n_rows, (int)L->reordered);
   Plan p;
   p.width = LF * VEC;
   p.nw = NW;
-  if (LF == 1 && VEC == 1 && L->tune.hot > 0 && !ranged)
+  if (LF == 1 && VEC == 1 && L->tune.hot > 0)
     p.hot = (int32_t)std::min<int64_t>({(int64_t)L->tune.hot, L->n_cols, (int64_t)((160 * 1024 - NW * 64 * 8) / 4)});
   const int G = 64 / LF;
   const int64_t n = active_only ? L->n_active : L->n_rows;
   unsigned int bucket[kBuckets];
-  const int64_t base = ranged ? r0 : 0;  // first row of the plan
-  if (!ranged) {
-    for (int b = 0; b < kBuckets; ++b) bucket[b] = L->bucket[b];
-    bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
-  } else {
-    // the block's rows by length bucket (internal rows are in descending length: each bucket's
-    // rows of the block are contiguous, in descending bucket order)
-    if ((int64_t)L->h_rowptr.size() != L->n_rows + 1) {
-      L->h_rowptr.resize(L->n_rows + 1);
-      WG_HIP_TRY(hipMemcpy(L->h_rowptr.data(), L->rowptr, sizeof(int32_t) * (L->n_rows + 1), hipMemcpyDeviceToHost));
-    }
-    for (int b = 0; b < kBuckets; ++b) bucket[b] = 0;
-    int prev = kBuckets;
-    for (int64_t r = r0; r < r1; ++r) {
-      const int32_t l = L->h_rowptr[r + 1] - L->h_rowptr[r];
-      const int b = (l > 1) ? 32 - __builtin_clz((unsigned)(l - 1)) : 0;
-      if (b > prev) return fail(WG_ERR_INVALID, "row-block plan: rows not in descending length at %lld", (long long)r);
-      prev = b;
-      ++bucket[b];
-    }
-  }
+  const int64_t base = 0;  // first row of the plan
+  for (int b = 0; b < kBuckets; ++b) bucket[b] = L->bucket[b];
+  bucket[0] -= (unsigned int)(L->n_rows - n);  // closed-form rows: length 0, at the very end
   p.row0 = base;
-  p.row1 = ranged ? r1 : n;
+  p.row1 = n;
   int iter, block_iter, chunk_iter;
-  default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter, hybrid, ranged ? r1 - r0 : n);
+  default_knobs(L->tune, G, L->nnz, &iter, &block_iter, &chunk_iter, hybrid, n);
   const int64_t team_max = (int64_t)G * iter;
   const int64_t block_max = (int64_t)NW * G * block_iter;
   const int64_t CH = (int64_t)NW * G * chunk_iter;
@@ -794,30 +690,25 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start) {
 
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out,
-                const ClenArgs* cl, const PhaseArgs* ph) {
+                const ClenArgs* cl) {
   if (L->n_rows == 0) return WG_OK;
-  if (ph && ph->block >= 0 && (ph->phase != 0 || H || S_out))
-    return fail(WG_ERR_INVALID, "launch_step: a row-block step is a plain step without H or fused finalize");
-  if (ph && ph->phase != 0 && (!ph->rsplit || !ph->part || S_out || (ph->phase == 3 && !ph->rsplit2)))
-    return fail(WG_ERR_INVALID, "launch_step: a phased step needs rsplit (phase 3: rsplit2), part, no fused finalize");
   if (int rc = prof_mark(L, stream, true)) return rc;
   const int vec = pick_vec(F, {xm1, xm2, xk, S, H, S_out});
   int64_t max_tile = 64 * (int64_t)vec;  // LF <= 64
   if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
   const bool fuse_h = (H != nullptr) && F <= max_tile;
   if (S_out && !(fuse_h && S)) return fail(WG_ERR_INVALID, "launch_step: fused finalize needs one tile and S");
-  auto tiles_loop = [&](hipStream_t stream, const PhaseArgs* ph) -> int {
+  // hyb: the hybrid step's tail pass (phase 4 over the tail-first columns, + the blocks' sums)
+  auto tiles_loop = [&](const TilePlan* hyb) -> int {
     for (int64_t f0 = 0; f0 < F; f0 += max_tile) {
       const int64_t fw = std::min<int64_t>(max_tile, F - f0);
       const int LF = (int)(fw / vec);
       Plan* plan = nullptr;
-      const bool ranged = ph && ph->block >= 0;
-      int rc = ranged ? get_plan(L, LF, vec, false, &plan, ph->block, ph->row_begin, ph->row_end)
-                      : get_plan(L, LF, vec, active_only, &plan, -1, 0, 0, /*hybrid=*/ph && ph->col);
-      if (rc) return rc;
+      if (int rc = get_plan(L, LF, vec, active_only, &plan, /*hybrid=*/hyb != nullptr)) return rc;
+      int rc = WG_OK;
       StepArgs a{};
       a.rowptr = L->rowptr;
-      a.col = (ph && ph->col) ? ph->col : L->col;
+      a.col = hyb ? hyb->tcol : L->col;
       a.val = L->val;
       a.iso = L->iso;
       a.xm1 = xm1 + f0;
@@ -845,20 +736,12 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.uout = cl->final_ ? 0 : cl->uout;
         if (a.uin) a.val = nullptr;  // unweighted: the gathered u needs no values
       }
-      if (ph && ph->phase != 0) {
-        a.phase = ph->phase;
-        a.rsplit = ph->rsplit;
-        a.rsplit2 = ph->rsplit2;
-        a.part = ph->part + f0;
-        a.part2 = ph->part2 ? ph->part2 + f0 : nullptr;
-        if (a.phase == 1 || a.phase == 3) {  // nothing but the sums: no epilogue operands, no T / S / H stores
-          a.xk = nullptr;
-          a.S = nullptr;
-          a.H = nullptr;
-        }
+      if (hyb) {
+        a.phase = 4;
+        a.rsplit = hyb->tsplit;
+        a.part = hyb->part + f0;
       }
       a.probe = L->tune.probe;
-      a.xcd = L->tune.xcd;
       if (a.probe && !a.xk) a.xk = S ? S + f0 : nullptr;  // the final step of a chain stores into S
       a.chunks = plan->chunks;
       a.partial = plan->partial;
@@ -866,24 +749,17 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       a.rowchunks = plan->rowchunks ? plan->rowchunks - plan->row0 : nullptr;
       a.arrivals = (L->tune.inkernel_combine && plan->n_split > 0) ? plan->arrivals - plan->row0 : nullptr;
       a.seg_mask = L->tune.seg_mask;
-      // non-temporal T_k / S stores only for large per-step streams (ogbn-arxiv F=40, 30 MB of
-      // T_k + S per step: 40.6 us plain vs 42.0 nt; F=64, 48 MB: 55.3 vs 56.5; Reddit-size F=44,
-      // 82 MB: 1773 plain vs 1738 nt)
-      const int64_t stream_rows = (active_only && L->reordered) ? L->n_active : L->n_rows;
-      a.nt = L->tune.nt >= 0 ? L->tune.nt : ((stream_rows * F * 8 <= ((int64_t)64 << 20)) ? 0 : 4);
+      // T_k stores write-through (sc1: the line leaves the XCD's L2, so the step's output stream
+      // does not evict the rows it is gathering): ogbn-arxiv F=40 37.59 / 37.61 vs 38.29 / 37.91 us
+      // per step plain, F=64 51.74 vs 52.14, Reddit-size F=41 746.6-747.2 vs 748.3-748.4 with nt
+      // stores (profiles/r03/s29).  Before: nt stores only for > 64 MB step streams (arxiv F=40
+      // 40.6 us plain vs 42.0 nt; Reddit-size F=44, 82 MB: 1773 plain vs 1738 nt)
+      a.nt = L->tune.nt >= 0 ? L->tune.nt : 8;
       a.bcast = L->tune.bcast;
       // F == 1 gathers on large graphs: int4 index loads and narrower teams (8M R-MAT 8-way
       // shard: 275.7 us per step with vidx + iter 8 vs 296.9 without; ogbn-arxiv-size F=1:
       // vidx 12.3 vs 11.5, so only from 16 M nonzeros)
       a.vidx = L->tune.vidx >= 0 ? L->tune.vidx : (L->nnz >= ((int64_t)16 << 20) ? 1 : 0);
-      a.xm1_bytes = (L->n_cols * F - f0) * (int64_t)sizeof(float);
-      a.gbuf = (L->tune.gbuf && a.xm1_bytes < ((int64_t)1 << 31)) ? 1 : 0;
-      // hub rows: LDS = (hubf + 1) * tile + the block-mode buffer (NW*64*VEC doubles) <= 160 KiB
-      a.hubf = (vec == 4 && a.xm1_bytes < ((int64_t)1 << 31) && !ranged)
-                   ? (int32_t)std::min<int64_t>({(int64_t)L->tune.hubf, L->n_cols,
-                                                 (int64_t)((160 * 1024 - 64 - plan->nw * 64 * vec * 8) /
-                                                           (LF * vec * 4)) - 1})
-                   : 0;
       if (vec == 4) rc = launch_step_vec<4>(*plan, a, stream);
       else if (vec == 2) rc = launch_step_vec<2>(*plan, a, stream);
       else rc = launch_step_vec<1>(*plan, a, stream);
@@ -892,47 +768,24 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     return WG_OK;
   };
   auto finish = [&]() -> int {
-    if (H && !fuse_h && !(ph && (ph->phase == 1 || ph->phase == 3))) {
+    if (H && !fuse_h) {
       hipLaunchKernelGGL(l1_normalize_kernel, dim3(ceil_div(L->n_rows, 4)), dim3(kBlock), 0, stream, L->n_rows, F, S, H);
       WG_LAUNCH_CHECK();
     }
     return prof_mark(L, stream, false);
   };
   // hybrid step (tiles.hip): the value-free Clenshaw steps of wide signals on large unweighted
-  // graphs sum their dense blocks on the matrix cores (part) and gather only each row's tail:
-  // either after the blocks (phase 4), or -- tiles_overlap -- the tail into part2 on a side
-  // stream while the blocks run, then an epilogue-only launch (phase 6)
-  if (cl && cl->uin && !(ph && (ph->phase != 0 || ph->block >= 0)) && !L->tune.probe && tiles_wanted(L, F)) {
+  // graphs sum their dense blocks on the matrix cores (part), then gather each row's tail
+  if (cl && cl->uin && !L->tune.probe && tiles_wanted(L, F)) {
     TilePlan* tp = nullptr;
     if (int rc = get_tile_plan(L, active_only, F, &tp)) return rc;
     if (tp) {
-      PhaseArgs hyb;
-      hyb.rsplit = tp->tsplit;
-      hyb.col = tp->tcol;
-      if (L->tune.tiles_overlap) {
-        if (int rc = side_stream(L)) return rc;
-        PhaseArgs p1 = hyb;
-        p1.phase = 1;
-        p1.part = tp->part2;
-        WG_HIP_TRY(hipEventRecord(L->side_fork, stream));
-        WG_HIP_TRY(hipStreamWaitEvent(L->side, L->side_fork, 0));
-        if (int rc = tiles_loop(L->side, &p1)) return rc;
-        WG_HIP_TRY(hipEventRecord(L->side_join, L->side));
-        if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
-        WG_HIP_TRY(hipStreamWaitEvent(stream, L->side_join, 0));
-        hyb.phase = 6;
-        hyb.part = tp->part2;
-        hyb.part2 = tp->part;
-      } else {
-        if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
-        hyb.phase = 4;
-        hyb.part = tp->part;
-      }
-      if (int rc = tiles_loop(stream, &hyb)) return rc;
+      if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
+      if (int rc = tiles_loop(tp)) return rc;
       return finish();
     }
   }
-  if (int rc = tiles_loop(stream, ph)) return rc;
+  if (int rc = tiles_loop(nullptr)) return rc;
   return finish();
 }
 
@@ -1020,50 +873,6 @@ int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, flo
     hipLaunchKernelGGL(permute_in_closed_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
                        L->n_active, coef, S, H);
   WG_LAUNCH_CHECK();
-  return WG_OK;
-}
-
-namespace {
-// first entry of each row whose column is >= split (rows sorted by column)
-__global__ void row_split_kernel(int64_t n, int32_t split, const int32_t* __restrict__ rowptr,
-                                 const int32_t* __restrict__ col, int32_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int32_t lo = rowptr[i], hi = rowptr[i + 1];
-  while (lo < hi) {
-    const int32_t mid = lo + ((hi - lo) >> 1);
-    if (col[mid] < split) lo = mid + 1;
-    else hi = mid;
-  }
-  out[i] = lo;
-}
-}  // namespace
-
-int get_row_split(wg_laplacian_s* L, int64_t split, const int32_t** out) {
-  *out = nullptr;
-  if (!L->cols_sorted) return WG_OK;
-  const bool first = split == L->n_rows;  // the own / halo split; else the halo tier split
-  int32_t*& slot = first ? L->rsplit : L->rsplit2;
-  if (slot && !first && L->rsplit2_at != split) {
-    (void)hipFree(slot);
-    slot = nullptr;
-  }
-  if (!slot) {
-    int32_t* p = nullptr;
-    if (int rc = dmalloc(&p, (size_t)std::max<int64_t>(1, L->n_rows))) return rc;
-    if (L->n_rows > 0) {
-      hipLaunchKernelGGL(row_split_kernel, dim3((unsigned)ceil_div(L->n_rows, 256)), dim3(256), 0, nullptr, L->n_rows,
-                         (int32_t)split, L->rowptr, L->col, p);
-      const hipError_t e = hipDeviceSynchronize();
-      if (e != hipSuccess) {
-        (void)hipFree(p);
-        return fail(WG_ERR_HIP, "row_split: %s", hipGetErrorString(e));
-      }
-    }
-    slot = p;
-    if (!first) L->rsplit2_at = split;
-  }
-  *out = slot;
   return WG_OK;
 }
 

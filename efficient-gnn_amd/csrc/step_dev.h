@@ -33,9 +33,6 @@ struct StepArgs {
   int32_t nt;
   int32_t bcast;
   int32_t vidx;
-  int32_t gbuf;        // F > 1 bcast gathers as raw buffer loads (accumulate_bcast_buf)
-  int32_t hubf;        // F > 1, hub kernel: rows [0, hubf) of the tile from LDS
-  int64_t xm1_bytes;   // extent of T_{k-1} from xm1 (gbuf: < 2^31)
   int32_t clen;        // 0 = forward recurrence + heat sum; 1 / 2 = Clenshaw step / final (ClenArgs)
   const float* x0;     // Clenshaw: X0 rows (internal order, stride ld)
   double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc - xm2
@@ -44,76 +41,27 @@ struct StepArgs {
   // uout: xk gets u.
   const double* dinv;
   int32_t uin, uprev, uout;
-  // two-phase step (row-sharded chain, exchange overlapped): phase 1 sums each row's entries
-  // [e0, rsplit[row]) (the own columns) into part[row] (float64, row stride ld); phase 2 sums
-  // [rsplit[row], e1) (the halo columns), adds part[row] and runs the epilogue.  0 = whole row.
-  // Two halo tiers: phase 3 adds [rsplit[row], rsplit2[row]) (tier 0) into part between them,
-  // and phase 2 sums [rsplit2[row], e1).
+  // hybrid step (tiles.hip; col = the tail-first column array, rsplit = each row's tail end):
+  // phase 4 sums the tail [e0, rsplit[row]), adds part (the dense blocks' float64 sums, row
+  // stride ld) to rows with dense entries and runs the epilogue.  0 = the whole row.
   int32_t phase;
   const int32_t* rsplit;
-  const int32_t* rsplit2;
-  double* part;
-  int32_t probe;  // timing probe (knob "probe"): gathers only -- no epilogue operands, acc stored to xk
-  // hybrid step (tiles.hip; col = the tail-first column array, rsplit = each row's tail end):
-  // phase 4 sums the tail [e0, rsplit[row]), adds part (the dense blocks' sums) to rows with
-  // dense entries and runs the epilogue; with the dense blocks overlapped, phase 1 sums the
-  // tail into part on a side stream and phase 6 (no entries) adds part + part2 (the blocks'
-  // sums, rows with dense entries) and runs the epilogue
-  const double* part2;
-  int32_t xcd;  // knob xcd: XCD-contiguous unit order (cheb_step_kernel)
+  const double* part;
+  int32_t probe;  // timing probe (-DWG_TIMING_PROBES builds, knob "probe"): gathers only, acc stored to xk
 };
 
 // the entry range of a row (or of a split-row chunk) this launch's phase covers
 __device__ __forceinline__ void phase_range(const StepArgs& a, int64_t row, int32_t& e0, int32_t& e1) {
   if (a.phase == 0) return;
-  const int32_t sp = a.rsplit[row];
-  if (a.phase == 1 || a.phase == 4) {
-    e1 = min(e1, sp);
-  } else if (a.phase == 6) {
-    e1 = e0;
-  } else if (a.phase == 3) {
-    e0 = max(e0, sp);
-    e1 = min(e1, a.rsplit2[row]);
-  } else {
-    e0 = max(e0, a.rsplit2 ? a.rsplit2[row] : sp);
-  }
+  e1 = min(e1, a.rsplit[row]);
   if (e1 < e0) e1 = e0;
 }
 
-// phases 1 and 3 end in part (no epilogue)
-__device__ __forceinline__ bool to_part(const StepArgs& a) { return a.phase == 1 || a.phase == 3; }
-
-// phase 1: the row's own-column sum goes to part; phase 3 adds its tier-0 sum; phase 2 adds
-// part before the epilogue (a fixed order: own, tier 0, tier 1)
-template <int VEC>
-__device__ __forceinline__ void part_store(const StepArgs& a, int64_t row, int fs, const double (&acc)[VEC]) {
-  double* p = a.part + row * a.ld + (int64_t)fs * VEC;
-  if (a.phase == 3) {
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) p[j] = p[j] + acc[j];
-  } else {
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) p[j] = acc[j];
-  }
-}
-
+// the hybrid step: the dense blocks' sums, for rows with dense entries
 template <int VEC>
 __device__ __forceinline__ void part_add(const StepArgs& a, int64_t row, int fs, double (&acc)[VEC]) {
-  const int64_t off = row * a.ld + (int64_t)fs * VEC;
-  if (a.phase >= 4) {  // hybrid step: the blocks' sums only for rows with dense entries
-    const bool dense = a.rsplit[row] != a.rowptr[row + 1];
-    if (a.phase == 6) {
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] += a.part[off + j];
-    }
-    const double* p2 = a.phase == 6 ? a.part2 : a.part;
-    if (dense) {
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] += p2[off + j];
-    }
-    return;
-  }
-  const double* p = a.part + off;
+  if (a.phase != 4 || a.rsplit[row] == a.rowptr[row + 1]) return;
+  const double* p = a.part + row * a.ld + (int64_t)fs * VEC;
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] += p[j];
 }
@@ -457,80 +405,6 @@ __device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, i
   }
 }
 
-// Branch-free form of accumulate_bcast (same elements, same order, so the same
-// sums bit for bit).  The gathers are raw buffer loads of T_{k-1}: a masked
-// slot gets an out-of-range offset, which the hardware answers with zeros and
-// no memory request.  The inner loop has a fixed trip count, and the next LF
-// (col, val) pairs are loaded from a clamped index while the current ones are
-// gathered.  With the loads behind branches (accumulate_bcast), the waitcnt
-// pass drains every in-flight gather (vmcnt(0)) at each batch of U.
-// xoff_f: this lane's column offset in floats (fs * VEC); rs spans T_{k-1}.
-// HUB: rows [0, a.hubf) of the gathered tile come from the LDS copy at
-// g_hub_lds ([hubf][W] floats, then W zeros): their global load gets the
-// dropped offset, every other column reads the LDS zero row; x = global + LDS.
-extern __shared__ float g_hub_lds[];
-
-template <int VEC, int U, bool HUB>
-__device__ __forceinline__ void accumulate_bcast_buf(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
-                                                     __amdgpu_buffer_rsrc_t rs, uint32_t xoff_b,
-                                                     double (&acc)[VEC], int fs, int base) {
-  constexpr uint32_t kDrop = 0x80000000u;
-  const int LF = a.LF;
-  const uint32_t ldb = (uint32_t)a.ld * 4u;
-  if (e >= e1) return;
-  const int32_t n = (e1 - e + stride - 1) / stride;
-  int32_t idx = e + min(fs, n - 1) * stride;
-  int32_t myc = a.col[idx];
-  float myv = a.val[idx];
-  for (int32_t t0 = 0; t0 < n; t0 += LF) {
-    const int32_t cc = myc;
-    const float cv = myv;
-    idx = e + min(t0 + LF + fs, n - 1) * stride;  // next LF pairs (clamped: always a valid entry)
-    myc = a.col[idx];
-    myv = a.val[idx];
-    const int cnt = min(LF, n - t0);
-    for (int j = 0; j < LF; j += U) {
-      int32_t c[U];
-      float v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int src = base + min(j + u, LF - 1);  // stays inside the sub-group
-        c[u] = __shfl(cc, src, 64);
-        v[u] = __shfl(cv, src, 64);
-      }
-      float x[U][VEC];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool hub = HUB && c[u] < a.hubf;
-        const uint32_t off = (j + u < cnt && !hub) ? (uint32_t)c[u] * ldb + xoff_b : kDrop;
-        // the builtins return integer data: reinterpret the bits
-        if constexpr (VEC == 4) {
-          const f32x4 g = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-          x[u][0] = g[0]; x[u][1] = g[1]; x[u][2] = g[2]; x[u][3] = g[3];
-        } else if constexpr (VEC == 2) {
-          const f32x2 g = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
-          x[u][0] = g[0]; x[u][1] = g[1];
-        } else {
-          x[u][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-        }
-        if constexpr (HUB) {
-          const int W = LF * VEC;
-          const int hrow = (j + u < cnt && hub) ? c[u] : a.hubf;  // row hubf = zeros
-          const float* hp = g_hub_lds + hrow * W + fs * VEC;
-#pragma unroll
-          for (int q = 0; q < VEC; ++q) x[u][q] += hp[q];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const double vv = (j + u < cnt) ? (double)v[u] : 0.0;
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) acc[q] = fma(vv, (double)x[u][q], acc[q]);
-      }
-    }
-  }
-}
-
 // F == 1: each lane takes 4 consecutive nonzeros with one 16-B int4 / float4
 // load of col / val (4x fewer index instructions through the texture-address
 // unit).  Chunks are 4-aligned in the CSR (arrays padded by 4 entries), lane
@@ -559,28 +433,18 @@ __device__ __forceinline__ void accumulate_vidx1(const StepArgs& a, int32_t e0, 
   }
 }
 
-template <int VEC, bool BCAST, bool HOT, bool HUB = false>
+template <int VEC, bool BCAST, bool HOT>
 __device__ __forceinline__ void acc_range(const StepArgs& a, int32_t e, int32_t e1, int32_t stride,
                                           const float* __restrict__ xb, double (&acc)[VEC], int32_t H, int fs,
                                           int base) {
   if constexpr (HOT && VEC == 1) {
     accumulate_hot1(a, e, e1, stride, xb, H, acc);
   } else if constexpr (BCAST) {
-    if (HUB || a.gbuf) {  // T_{k-1} as a raw buffer: [xm1, xm1 + xm1_bytes), this lane's column offset from xb
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0, (int)a.xm1_bytes, 0x00020000);
-      const uint32_t xoff = (uint32_t)((xb - a.xm1) * 4);
-      if (a.LF % 5 == 0) accumulate_bcast_buf<VEC, 5, HUB>(a, e, e1, stride, rs, xoff, acc, fs, base);
-      else accumulate_bcast_buf<VEC, 4, HUB>(a, e, e1, stride, rs, xoff, acc, fs, base);
-    } else if (a.LF % 5 == 0) {
-      accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
-    } else {
-      accumulate_bcast<VEC, WG_BCAST_U>(a, e, e1, stride, xb, acc, fs, base);
-    }
+    if (a.LF % 5 == 0) accumulate_bcast<VEC, 5>(a, e, e1, stride, xb, acc, fs, base);
+    else accumulate_bcast<VEC, WG_BCAST_U>(a, e, e1, stride, xb, acc, fs, base);
   } else {
     accumulate<VEC>(a, e, e1, stride, xb, acc);
   }
 }
-
 
 }  // namespace wg

@@ -12,8 +12,8 @@
 //   part[row] = sum over the row's dense entries of u_j      (this file)
 //   step      = cheb_step_kernel over the tail entries (each row's tail first in
 //               tcol; its own plan, get_plan(hybrid)), + part, epilogue: phase 4
-//               after the blocks, or (tiles_overlap) phase 1 into part2 on a side
-//               stream beside them, then phase 6
+//               after the blocks (the tail on a side stream beside them measured
+//               slower: Reddit-size F=41 1176 vs 1136 us, 8-way shard 158 vs 155)
 //
 // The block sum is a 128 x 32 by 32 x W product A.U with A a 0/1 matrix (exact in
 // bf16).  U is split exactly into three bf16 pieces, u = hi + mid + lo
@@ -441,7 +441,6 @@ void TilePlan::release() {
   (void)hipFree(tcol);
   (void)hipFree(tsplit);
   (void)hipFree(part);
-  (void)hipFree(part2);
   (void)hipFree(slots);
   bct = nullptr;
   bmask = nullptr;
@@ -450,7 +449,6 @@ void TilePlan::release() {
   tcol = nullptr;
   tsplit = nullptr;
   part = nullptr;
-  part2 = nullptr;
   slots = nullptr;
   width = 0;
 }
@@ -472,14 +470,6 @@ int launch_scale_rows(wg_laplacian_s* L, int64_t n, int64_t F, const float* x, f
                                  (long long)L->n_cols);
   hipLaunchKernelGGL(scale_rows_kernel, dim3((unsigned)ceil_div(n * F, 256)), dim3(256), 0, stream, n, F, x, L->dinv, u);
   WG_LAUNCH_CHECK();
-  return WG_OK;
-}
-
-int side_stream(wg_laplacian_s* L) {
-  if (L->side) return WG_OK;
-  WG_HIP_TRY(hipStreamCreateWithFlags(&L->side, hipStreamNonBlocking));
-  WG_HIP_TRY(hipEventCreateWithFlags(&L->side_fork, hipEventDisableTiming));
-  WG_HIP_TRY(hipEventCreateWithFlags(&L->side_join, hipEventDisableTiming));
   return WG_OK;
 }
 
@@ -513,14 +503,11 @@ int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out
   TilePlan* p = L->tiles[ai];
   if (p->width < F) {  // part / slots for this width
     (void)hipFree(p->part);
-    (void)hipFree(p->part2);
     (void)hipFree(p->slots);
     p->part = nullptr;
-    p->part2 = nullptr;
     p->slots = nullptr;
     p->width = 0;
     int rc = dmalloc(&p->part, (size_t)std::max<int64_t>(1, L->n_rows) * F);
-    if (!rc) rc = dmalloc(&p->part2, (size_t)std::max<int64_t>(1, L->n_rows) * F);
     if (!rc) rc = dmalloc(&p->slots, (size_t)std::max(1, p->n_slots) * p->rows * F);
     if (rc) return rc;
     p->width = (int32_t)F;

@@ -80,9 +80,6 @@ SIGNATURES = {
     "wg_wats_head_backward": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32] + [c_vp] * 15 + [c_vp]),
     "wg_dist_unique_id": (ctypes.c_int, [c_vp]),
     "wg_dist_create": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, ctypes.POINTER(c_vp)]),
-    "wg_dist_create_tiered": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp,
-                                             ctypes.POINTER(c_vp)]),
-    "wg_dist_stream_blocks": (ctypes.c_int, [c_vp, c_i32]),
     "wg_dist_destroy": (ctypes.c_int, [c_vp]),
     "wg_dist_set_graph": (ctypes.c_int, [c_vp, c_i32]),
     "wg_dist_wavelet_features": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_f64, c_vp, c_vp, c_vp]),

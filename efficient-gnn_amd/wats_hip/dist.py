@@ -71,22 +71,12 @@ class HaloPlan:
     r0: int
     r1: int
     n_halo: int
-    halo_global: np.ndarray                 # global ids of halo rows, grouped by (tier, owner)
-    recv_counts: list                       # halo rows received per (tier, peer), tier-major
-    send_counts: list                       # rows sent per (tier, peer), tier-major
-    send_rows: np.ndarray                   # local (caller-order) row ids to send, grouped by (tier, peer)
+    halo_global: np.ndarray                 # global ids of halo rows, grouped by owner
+    recv_counts: list                       # halo rows received per peer
+    send_counts: list                       # rows sent per peer
+    send_rows: np.ndarray                   # local (caller-order) row ids to send, grouped by peer
     local_indices: np.ndarray               # CSR columns renumbered to [own | halo]
     stats: dict = field(default_factory=dict)
-    tiers: int = 1                          # halo tiers: [tier 0 (hot) | tier 1], each grouped by owner
-
-    def tier_counts(self, counts: list, tier: int) -> list:
-        """The per-peer slice of ``recv_counts`` / ``send_counts`` of one tier."""
-        return list(counts[tier * self.world:(tier + 1) * self.world])
-
-    @property
-    def n_hot(self) -> int:
-        """Halo rows in tier 0 (all of them with one tier)."""
-        return int(sum(self.recv_counts[:self.world]))
 
     @property
     def n_own(self) -> int:
@@ -131,7 +121,7 @@ def exchange_int_lists(lists: list, group=None) -> list:
 
 
 def build_halo_plan(indptr_local: np.ndarray, indices_global, bounds: np.ndarray, group=None,
-                    compute_device=None, col_degree=None, tiers: int = 1, hot_frac: float = 0.25) -> HaloPlan:
+                    compute_device=None, col_degree=None) -> HaloPlan:
     """Renumber this rank's CSR columns to [own | halo] and agree with every
     peer on who sends which rows (collective).  The halo is grouped by owner
     rank; with ``col_degree`` (the global column degree, indexed by global
@@ -139,16 +129,8 @@ def build_halo_plan(indptr_local: np.ndarray, indices_global, bounds: np.ndarray
     halo columns of every peer are a prefix of its group -- the F = 1 hub
     kernel stages those prefixes in LDS (csrc/lds1.hip, build_shard_hub).
 
-    ``tiers=2`` splits the halo in two tiers, each grouped by owner: tier 0
-    holds the ``hot_frac`` of halo rows this shard's entries reference most
-    (on power-law graphs a small share of the rows carries most of the halo
-    entries), tier 1 the rest.  The native chain exchanges tier 0 first and
-    sums its entries while tier 1 is in flight (csrc/dist.hip).
-
     The column work (unique, searchsorted over nnz entries) runs with torch on
     ``compute_device`` (the GPU for large shards; default CPU)."""
-    if tiers not in (1, 2):
-        raise ValueError(f"tiers must be 1 or 2, not {tiers}")
     rank, world = _rank_world(group)
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
     dev = torch.device(compute_device) if compute_device is not None else torch.device("cpu")
@@ -161,41 +143,26 @@ def build_halo_plan(indptr_local: np.ndarray, indices_global, bounds: np.ndarray
     local = cols - r0
     halo_sorted = halo_t.cpu().numpy()
     owner_sorted = np.searchsorted(bounds, halo_sorted, side="right") - 1
-    tier_sorted = np.zeros(halo_sorted.size, np.int64)
-    if tiers == 2 and halo_sorted.size:
-        # entries per halo column in this shard; the hot_frac most referenced rows form tier 0
-        uses = torch.bincount(torch.searchsorted(halo_t, remote), minlength=halo_t.numel()).cpu().numpy()
-        n_hot = min(halo_sorted.size, max(1, int(round(hot_frac * halo_sorted.size))))
-        hot = np.lexsort((halo_sorted, -uses))[:n_hot]
-        tier_sorted[:] = 1
-        tier_sorted[hot] = 0
     if col_degree is not None and halo_sorted.size:
         deg = np.asarray(col_degree.cpu().numpy() if isinstance(col_degree, torch.Tensor) else col_degree)
-        order = np.lexsort((halo_sorted, -deg[halo_sorted].astype(np.float64), owner_sorted, tier_sorted))
+        order = np.lexsort((halo_sorted, -deg[halo_sorted].astype(np.float64), owner_sorted))
     else:
-        order = np.lexsort((halo_sorted, owner_sorted, tier_sorted))
+        order = np.lexsort((halo_sorted, owner_sorted))
     rank_of = np.empty(halo_sorted.size, np.int64)   # position in the halo of the id at sorted position i
     rank_of[order] = np.arange(halo_sorted.size)
     local[~own] = n_own + torch.from_numpy(rank_of).to(dev)[torch.searchsorted(halo_t, remote)]
     halo_global = halo_sorted[order]
     owner = owner_sorted[order]
-    tier = tier_sorted[order]
-    recv_lists, requested = [], []
-    for t in range(tiers):
-        rl = [halo_global[(owner == q) & (tier == t)] for q in range(world)]
-        recv_lists += rl
-        requested += exchange_int_lists(rl, group) if world > 1 else rl  # what each peer needs from us
+    recv_lists = [halo_global[owner == q] for q in range(world)]
+    requested = exchange_int_lists(recv_lists, group) if world > 1 else recv_lists  # what each peer needs from us
     send_rows = np.concatenate(requested).astype(np.int64) - r0 if world else np.zeros(0, np.int64)
     assert np.all((send_rows >= 0) & (send_rows < max(n_own, 1))) or send_rows.size == 0
     plan = HaloPlan(rank=rank, world=world, bounds=np.asarray(bounds), r0=r0, r1=r1, n_halo=int(halo_global.size),
                     halo_global=halo_global, recv_counts=[int(len(x)) for x in recv_lists],
                     send_counts=[int(len(x)) for x in requested], send_rows=send_rows.astype(np.int32),
-                    local_indices=local.to(torch.int32).cpu().numpy(), tiers=tiers)
+                    local_indices=local.to(torch.int32).cpu().numpy())
     plan.stats = dict(n_own=n_own, n_halo=plan.n_halo, nnz_local=int(cols.numel()),
                       nnz_remote=int(remote.numel()), send_rows=int(send_rows.size))
-    if tiers == 2:
-        li = plan.local_indices
-        plan.stats.update(n_hot=plan.n_hot, nnz_hot=int(((li >= n_own) & (li < n_own + plan.n_hot)).sum()))
     return plan
 
 
@@ -256,19 +223,15 @@ def halo_exchange(ext: torch.Tensor, plan: HaloPlan, pack, sendbuf: torch.Tensor
     if plan.world == 1:
         return
     pack(ext, sendbuf)
-    h0 = s0 = 0
-    for t in range(plan.tiers):   # one all-to-all-v per halo tier
-        rc, sc = plan.tier_counts(plan.recv_counts, t), plan.tier_counts(plan.send_counts, t)
-        recv = ext[plan.n_own + h0:plan.n_own + h0 + sum(rc)]
-        snd = sendbuf[s0:s0 + sum(sc)]
-        if not host_staged:
-            dist.all_to_all_single(recv, snd, output_split_sizes=rc, input_split_sizes=sc, group=group)
-        else:
-            r = torch.empty(sum(rc), ext.shape[1], dtype=ext.dtype)
-            dist.all_to_all_single(r, snd.cpu(), output_split_sizes=rc, input_split_sizes=sc, group=group)
-            recv.copy_(r.to(ext.device))
-        h0 += sum(rc)
-        s0 += sum(sc)
+    rc, sc = list(plan.recv_counts), list(plan.send_counts)
+    recv = ext[plan.n_own:plan.n_own + sum(rc)]
+    snd = sendbuf[:sum(sc)]
+    if not host_staged:
+        dist.all_to_all_single(recv, snd, output_split_sizes=rc, input_split_sizes=sc, group=group)
+    else:
+        r = torch.empty(sum(rc), ext.shape[1], dtype=ext.dtype)
+        dist.all_to_all_single(r, snd.cpu(), output_split_sizes=rc, input_split_sizes=sc, group=group)
+        recv.copy_(r.to(ext.device))
 
 
 class ShardedWavelet:
@@ -284,21 +247,12 @@ class ShardedWavelet:
     ``torch.distributed.all_to_all_single`` per step (RCCL/xGMI).
     ``exchange="host"``: that collective on host copies (gloo) -- lets several
     ranks share one GPU in tests (RCCL refuses two ranks on one device).
-
-    ``stream_blocks`` (``exchange="rccl"``): run each step as that many
-    launches over nnz-balanced row blocks and send every block's rows while
-    the next block computes (``wg_dist_stream_blocks``; 0 = off).
-
-    ``halo_tiers`` (default 1) and ``hot_frac``: the halo in a hot tier (the
-    ``hot_frac`` most referenced halo rows) and a cold one; with two-phase
-    steps (``L.tune(overlap=1)``) the native chain exchanges the hot tier first
-    and sums its entries while the cold tier is in flight
-    (:func:`build_halo_plan`, csrc/dist.hip).
+    Each step exchanges the halo, then computes (the overlap variants of round
+    2 measured slower and were removed).
     """
 
     def __init__(self, indptr_local, indices_global, values_local, n_global: int, bounds, group=None,
-                 exchange: str = "rccl", device=None, max_features: int = 1, halo_tiers=None,
-                 hot_frac: float = 0.1, stream_blocks: int = 0):
+                 exchange: str = "rccl", device=None, max_features: int = 1):
         from .laplacian import NormalizedLaplacian, require_gpu
         self.device = require_gpu(device)
         self.group = group
@@ -322,12 +276,8 @@ class ShardedWavelet:
         w_global = allreduce_column_degree(colsum, diag, group)
         del colsum, diag
         _trace("column degrees done; halo plan")
-        # one halo tier by default: the hot tier only pays with the two-phase steps (tuning
-        # key "overlap"), which cost more than they hide on the measured shards
-        if halo_tiers is None:
-            halo_tiers = 1
         self.plan = build_halo_plan(indptr_local, indices_global, bounds, group, compute_device=self.device,
-                                    col_degree=w_global, tiers=halo_tiers, hot_frac=hot_frac)
+                                    col_degree=w_global)
         p = self.plan
         w_cols = plan_column_degree(w_global, p).to(self.device)
         del w_global
@@ -345,14 +295,8 @@ class ShardedWavelet:
         self.profile = False          # record (exchange, step) event pairs per Chebyshev step
         self.events = []
         self._dist = None
-        self.stream_blocks = 0
         if exchange == "rccl":
             self._dist = self._create_native()
-            if stream_blocks and p.tiers == 1:
-                # row-block streaming (collective): each step's exchange trails its compute by a block
-                with torch.cuda.device(self.device):
-                    check(lib.wg_dist_stream_blocks(self._dist, int(stream_blocks)), "dist_stream_blocks")
-                self.stream_blocks = int(stream_blocks)
         elif exchange == "ipc":
             # the shared region is sized for max_features columns (large IPC
             # mappings are slow to set up: keep it to what the chain uses); a
@@ -379,9 +323,9 @@ class ShardedWavelet:
         rc = np.ascontiguousarray(p.recv_counts, dtype=np.int64)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            check(lib.wg_dist_create_tiered(self.L.handle, uid, p.rank, p.world, p.tiers,
-                                            ptr(self.send_rows) if self.send_rows.numel() else None,
-                                            sc.ctypes.data, rc.ctypes.data, ctypes.byref(h)), "dist_create")
+            check(lib.wg_dist_create(self.L.handle, uid, p.rank, p.world,
+                                     ptr(self.send_rows) if self.send_rows.numel() else None,
+                                     sc.ctypes.data, rc.ctypes.data, ctypes.byref(h)), "dist_create")
         return h
 
     def _create_ipc(self, max_features: int):
@@ -394,24 +338,19 @@ class ShardedWavelet:
         rc = np.ascontiguousarray(p.recv_counts, dtype=np.int64)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            check(lib.wg_dist_create_tiered(self.L.handle, None, p.rank, p.world, p.tiers,
-                                            ptr(self.send_rows) if self.send_rows.numel() else None,
-                                            sc.ctypes.data, rc.ctypes.data, ctypes.byref(h)), "dist_create")
+            check(lib.wg_dist_create(self.L.handle, None, p.rank, p.world,
+                                     ptr(self.send_rows) if self.send_rows.numel() else None,
+                                     sc.ctypes.data, rc.ctypes.data, ctypes.byref(h)), "dist_create")
             blob = (ctypes.c_uint8 * 128)()
             check(lib.wg_dist_ipc_local(h, int(max_features), blob), "dist_ipc_local")
         _trace("ipc region ready; exchanging handles")
         # what each owner sends me = its internal ids of my halo rows, in my halo order
-        # (halo grouped by (tier, owner): one list exchange per tier)
         send_int = self.send_rows.cpu().numpy().astype(np.int64)
         offs = np.concatenate([[0], np.cumsum(p.send_counts)]).astype(np.int64)
         if p.world > 1:
             blobs = [None] * p.world
             dist.all_gather_object(blobs, bytes(blob), group=self.group)
-            src = []
-            for t in range(p.tiers):
-                g = t * p.world
-                src += exchange_int_lists([send_int[offs[g + q]:offs[g + q + 1]] for q in range(p.world)],
-                                          self.group)
+            src = exchange_int_lists([send_int[offs[q]:offs[q + 1]] for q in range(p.world)], self.group)
         else:
             blobs = [bytes(blob)]
             src = [send_int]
@@ -499,30 +438,20 @@ class ShardedWavelet:
         st = self.L.profile_collect()
         self.L.profile_enable(False)
         self.profile = False
-        # two-phase (overlapped) steps record two launches per Chebyshev step (three with
-        # two halo tiers)
-        inf = self.info()
-        if inf.get("overlap_mode") == "blocks":   # K - 1 streamed steps of stream_blocks launches + the last
-            n = 1 + max(0, round((st["launches"] - 1) / self.stream_blocks))
-            per_step = 2
-        else:
-            per_step = (3 if inf.get("tiers", 1) == 2 else 2) if inf.get("overlapped") else 1
-            n = max(1, st["launches"] // per_step)
+        n = max(1, st["launches"])  # one step launch per Chebyshev step
         return dict(exchange_ms=sum(ex) / max(1, len(ex)), step_ms=st["sum_ms"] / n, max_step_ms=st["max_ms"],
-                    launches=st["launches"], overlapped=per_step > 1)
+                    launches=st["launches"])
 
     def info(self) -> dict:
-        """State of the native chain (wg_dist_info): overlapped (the last chain
-        ran two-phase steps, the exchange on its own stream), own / halo / sent
-        rows, world, exchange kind, captured graph present."""
+        """State of the native chain (wg_dist_info): own / halo / sent rows,
+        world, exchange kind, captured graph present."""
         if self._dist is None:
             return {}
         out = (ctypes.c_int64 * 8)()
         check(_lib.load().wg_dist_info(self._dist, out), "dist_info")
-        keys = ("overlapped", "n_own", "n_halo", "n_send", "world", "exchange", "captured", "tiers")
+        keys = ("overlap", "n_own", "n_halo", "n_send", "world", "exchange", "captured", "tiers")
         d = dict(zip(keys, [int(v) for v in out]))
-        d["overlap_mode"] = {0: "none", 1: "phases", 2: "blocks"}.get(d["overlapped"], "?")
-        d["overlapped"] = bool(d["overlapped"])
+        del d["overlap"], d["tiers"]
         d["exchange"] = {1: "ipc", 2: "rccl"}.get(d["exchange"], "none")
         return d
 

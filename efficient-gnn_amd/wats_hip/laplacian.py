@@ -233,7 +233,7 @@ class NormalizedLaplacian:
                                            float(alpha0), float(alpha_k), stream_handle(self.device)), "cheb_step")
 
     def tune(self, **knobs) -> None:
-        """Step-kernel tuning knobs: iter, chunk_iter, seg_mask (see wats_hip.h)."""
+        """Step-kernel tuning knobs: iter, chunk_iter, tiles, ... (wg_laplacian_tune in wats_hip.h)."""
         for k, v in knobs.items():
             check(_lib.load().wg_laplacian_tune(self.handle, k.encode(), int(v)), f"tune {k}")
 

@@ -238,13 +238,14 @@ int wg_chain_status(wg_laplacian_t L, int32_t* timed_out_host);
 
 /* Tuning: key "iter" (team-mode nonzeros per lane sub-group; default by
  * shape), "chunk_iter" (chunk-mode nonzeros per sub-group),
- * "seg_mask" (bitmask of plan segments to launch -- timing attribution only;
- * results are wrong unless all bits are set), "clenshaw" (wavelet_features'
- * heat sum, default 1), "tiles" (the hybrid step, DESIGN.md 4.6: -1 auto,
- * 0 off, 1 whenever it applies; with "tile_th", "tile_rows", "tile_max",
- * "tile_rg", "tiles_overlap"), and the kernel-variant keys listed in
+ * "clenshaw" (wavelet_features' heat sum, default 1), "tiles" (the hybrid
+ * step, DESIGN.md 4.6: -1 auto, 0 off, 1 whenever it applies; with "tile_th",
+ * "tile_rows", "tile_max", "tile_rg"), "nt" (store hints), and the keys listed in
  * efficient-gnn_amd/csrc/internal.h (struct Tuning).  Plan-shaping keys are
- * synchronous (they drop cached plans); launch-time keys are not. */
+ * synchronous (they drop cached plans); launch-time keys are not.  Timing
+ * probes whose results are wrong on purpose ("seg_mask", "probe",
+ * "probe_tailwin", "xdelay") exist only in a build
+ * with -DWG_TIMING_PROBES; this library rejects them as unknown keys. */
 int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value);
 /* Row shards: the halo columns [n_rows + offsets[q], n_rows + offsets[q+1])
  * come from peer q (q < n_groups; offsets[0] = 0, offsets[n_groups] = halo
@@ -289,9 +290,9 @@ int wg_gather_rows(const float* src, const int32_t* rows, int64_t n, int64_t F, 
  * step kernel runs.  The chain is captured into a hipGraph on its second call
  * with the same arguments and replayed from then on (wg_dist_set_graph(D, 0)
  * keeps it eager; profiling via wg_profile_enable(L) also runs eagerly).
- * With peers and column-sorted rows (the default) each step is split in two
- * launches: the entries of own columns run while the exchange proceeds on a
- * second stream, the halo entries after it (tuning key "overlap" = 0: off).
+ * Each step exchanges, then computes (the overlap variants measured in round
+ * 2 -- two-phase steps, two halo tiers, streamed row blocks -- were slower
+ * and are removed).
  * wg_dist_unique_id fills NCCL_UNIQUE_ID_BYTES (128) bytes on one rank; every
  * rank passes the same bytes to wg_dist_create (collective: blocks until all
  * ranks joined); unique_id NULL = no RCCL communicator (IPC exchange below).  X0, S, H: own rows (n_rows, F) in the caller's order.
@@ -301,33 +302,13 @@ int wg_dist_unique_id(void* id_out /* 128 bytes, host */);
 int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world,
                    const int32_t* send_rows, const int64_t* send_counts_host,
                    const int64_t* recv_counts_host, wg_dist_t* out);
-/* The same with the halo in `tiers` (1 or 2) tiers: send_counts / recv_counts
- * hold tiers * world entries, tier-major ([t * world + q]); the halo columns
- * and send_rows are ordered (tier, peer).  Tier 0 holds every peer's
- * highest-degree rows: it is exchanged first, and each step's entries on those
- * columns run (on a second stream) while tier 1 is exchanged.  tiers = 1 is
- * wg_dist_create. */
-int wg_dist_create_tiered(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_t world, int32_t tiers,
-                          const int32_t* send_rows, const int64_t* send_counts_host,
-                          const int64_t* recv_counts_host, wg_dist_t* out);
-/* Row-block streaming (RCCL exchange, one halo tier; collective): each
- * Chebyshev step of the gather-kernel chain runs as n_blocks launches over
- * nnz-balanced blocks of the shard's rows, and block b's rows are sent to the
- * peers (pack, grouped send / receive, unpack into the halo) on a second
- * stream while block b+1 computes, so a step's exchange trails its compute by
- * one block.  Streamed chains run eagerly (no hipGraph).  n_blocks = 0: off.
- * Every rank passes the same n_blocks. */
-int wg_dist_stream_blocks(wg_dist_t D, int32_t n_blocks);
 int wg_dist_destroy(wg_dist_t D);
 int wg_dist_set_graph(wg_dist_t D, int32_t enable);
 int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K, double s, float* S,
                              float* H, void* stream);
-/* State of the sharded chain, out8_host: [0] how the last chain overlapped
- * its halo exchanges: 0 not, 1 with each step's own-column half (two-phase
- * steps: 2 step launches per Chebyshev step), 2 streamed row blocks
- * (wg_dist_stream_blocks), [1] own rows, [2] halo rows,
- * [3] rows sent, [4] world, [5] exchange (1 IPC, 2 RCCL, 0 none), [6] 1 if a
- * captured hipGraph exists, [7] halo tiers. */
+/* State of the sharded chain, out8_host: [0] 0 (exchange, then the step),
+ * [1] own rows, [2] halo rows, [3] rows sent, [4] world, [5] exchange (1 IPC,
+ * 2 RCCL, 0 none), [6] 1 if a captured hipGraph exists, [7] 1 (halo tiers). */
 int wg_dist_info(wg_dist_t D, int64_t* out8_host);
 /* Total time (ms) and count of the halo exchanges (pack + RCCL, or the IPC
  * pull) recorded while profiling was enabled on the shard's handle; resets. */

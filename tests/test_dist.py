@@ -42,7 +42,7 @@ def test_partition_rows_balanced():
         assert w.max() <= (g.nnz + g.n) / world + np.diff(g.indptr).max() + 1
 
 
-def _cpu_worker(rank, world, port, kind, K, F, q, tiers=1):
+def _cpu_worker(rank, world, port, kind, K, F, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -57,23 +57,15 @@ def _cpu_worker(rank, world, port, kind, K, F, q, tiers=1):
         vals_l = None if g.values is None else g.values[lo:hi]
         # rmat: the halo groups in descending global degree (what ShardedWavelet passes)
         col_degree = np.bincount(g.indices, minlength=g.n) if kind == "rmat" else None
-        plan = build_halo_plan(indptr_l, cols_g, bounds, None, col_degree=col_degree, tiers=tiers, hot_frac=0.3)
-        assert len(plan.recv_counts) == len(plan.send_counts) == tiers * world
+        plan = build_halo_plan(indptr_l, cols_g, bounds, None, col_degree=col_degree)
+        assert len(plan.recv_counts) == len(plan.send_counts) == world
         owner = np.searchsorted(bounds, plan.halo_global, side="right") - 1
-        tier = np.repeat(np.arange(tiers), [sum(plan.tier_counts(plan.recv_counts, t)) for t in range(tiers)])
-        for t in range(tiers):
-            ot = owner[tier == t]
-            assert np.all(np.diff(ot) >= 0), "halo tier not grouped by owner"
-            assert np.array_equal(np.bincount(ot, minlength=world), plan.tier_counts(plan.recv_counts, t))
-            if col_degree is not None:
-                for peer in range(world):
-                    dq = col_degree[plan.halo_global[(owner == peer) & (tier == t)]]
-                    assert np.all(np.diff(dq) <= 0), "halo group not in descending degree"
-        if tiers == 2 and plan.n_halo:
-            # tier 0: the halo rows this shard's entries reference most
-            uses = np.bincount(plan.local_indices, minlength=plan.n_cols)[plan.n_own:]
-            assert plan.n_hot == max(1, round(0.3 * plan.n_halo))
-            assert uses[:plan.n_hot].min() >= uses[plan.n_hot:].max(initial=0)
+        assert np.all(np.diff(owner) >= 0), "halo not grouped by owner"
+        assert np.array_equal(np.bincount(owner, minlength=world), plan.recv_counts)
+        if col_degree is not None:
+            for peer in range(world):
+                dq = col_degree[plan.halo_global[owner == peer]]
+                assert np.all(np.diff(dq) <= 0), "halo group not in descending degree"
         # partial column degrees of this shard (the GPU path does this with wg_column_degree)
         cs = np.zeros(g.n)
         dg = np.zeros(g.n)
@@ -119,13 +111,12 @@ def _cpu_worker(rank, world, port, kind, K, F, q, tiers=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind,tiers", [(2, "rmat", 1), (3, "rmat", 1), (2, "weighted", 1), (3, "rmat", 2),
-                                              (2, "weighted", 2), (8, "rmat", 1), (8, "rmat", 2)])
-def test_sharded_chain_cpu_gloo(world, kind, tiers):
+@pytest.mark.parametrize("world,kind", [(2, "rmat"), (3, "rmat"), (2, "weighted"), (3, "weighted"), (8, "rmat")])
+def test_sharded_chain_cpu_gloo(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, kind, 5, 3, q, tiers)) for r in range(world)]
+    procs = [ctx.Process(target=_cpu_worker, args=(r, world, port, kind, 5, 3, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in range(world)]
@@ -139,7 +130,7 @@ def test_sharded_chain_cpu_gloo(world, kind, tiers):
 
 
 # ------------------------------------------------------------------ GPU, ranks share one device
-def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=1, tiles=0):
+def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiles=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -153,7 +144,7 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
         lo, hi = g.indptr[r0], g.indptr[r1]
         sw = ShardedWavelet(g.indptr[r0:r1 + 1] - lo, g.indices[lo:hi],
                             None if g.values is None else g.values[lo:hi], g.n, bounds, exchange=exchange,
-                            device="cuda:0", halo_tiers=tiers)
+                            device="cuda:0")
         # lds 4 (hub teams) with a 256-column hub: the shard's hub mixes its own top columns
         # with every peer group's (halo groups in descending degree), the rest is gathered
         sw.L.tune(lds=lds, **({"lds_cb": 256} if lds == 4 else {}))
@@ -163,8 +154,6 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
         hybrid = bool(tiles) and not (tiles == 2 and rank == 1)
         if tiles:
             sw.L.tune(tiles=1 if hybrid else 0, tile_th=8, tile_max=3)
-        elif exchange == "ipc":
-            sw.L.tune(overlap=1)   # the two-phase steps (off by default) on every other IPC case
         q_path = "u" if (F == 1 and sw.u_len() > 0) else "t"
         rng = np.random.default_rng(0)
         X = rng.standard_normal((g.n, F)).astype(np.float32)
@@ -173,12 +162,9 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
         H, S = outs[0]
         same = all(torch.equal(o[1], S) and torch.equal(o[0], H) for o in outs)
         if exchange == "ipc":
-            # the gather-kernel path overlaps each step's exchange with the step's own-column half
-            ov = sw.info()["overlapped"]
-            assert ov == (q_path == "t" and sw.plan.n_halo > 0 and not tiles), (ov, q_path, sw.plan.n_halo)
             if tiles:
                 assert ("tiles:" in sw.L.describe(F + (-F) % 16)) == hybrid, sw.L.describe(F)
-            assert sw.info()["tiers"] == tiers
+            assert sw.info()["exchange"] == "ipc"
             sw.check_exchange()
             sw.close()
         q.put((rank, S.cpu().numpy(), H.cpu().numpy(), q_path, same))
@@ -187,20 +173,18 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiers=
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,kind,F,lds,exchange,tiers,tiles", [
-    (2, "rmat", 1, 2, "host", 1, 0), (4, "rmat", 1, 2, "host", 1, 0), (2, "rmat", 1, 0, "host", 1, 0), (3, "rmat", 40, 2, "host", 1, 0),
-    (2, "weighted", 4, 2, "host", 1, 0), (2, "weighted", 1, 2, "host", 1, 0),
-    (2, "rmat", 1, 2, "ipc", 1, 0), (4, "rmat", 1, 2, "ipc", 1, 0), (2, "rmat", 1, 0, "ipc", 1, 0), (3, "rmat", 40, 2, "ipc", 1, 0),
-    (2, "weighted", 4, 2, "ipc", 1, 0), (3, "weighted", 1, 2, "ipc", 1, 0), (2, "rmat", 1, 4, "ipc", 1, 0), (2, "rmat", 1, 4, "host", 1, 0),
-    (3, "rmat", 40, 2, "ipc", 2, 0), (2, "weighted", 4, 2, "ipc", 2, 0), (4, "rmat", 1, 2, "ipc", 2, 0),
-    (3, "rmat", 8, 2, "host", 2, 0), (8, "rmat", 40, 2, "ipc", 1, 0), (8, "rmat", 1, 2, "ipc", 1, 0),
-    (8, "weighted", 4, 2, "ipc", 2, 0), (2, "rmat", 48, 2, "ipc", 1, 1), (3, "rmat", 41, 2, "ipc", 1, 1),
-    (4, "rmat", 48, 2, "ipc", 2, 1), (3, "rmat", 48, 2, "ipc", 1, 2), (2, "rmat", 41, 2, "ipc", 1, 2)])
-def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiers, tiles):
+@pytest.mark.parametrize("world,kind,F,lds,exchange,tiles", [
+    (2, "rmat", 1, 2, "host", 0), (4, "rmat", 1, 2, "host", 0), (2, "rmat", 1, 0, "host", 0), (3, "rmat", 40, 2, "host", 0),
+    (2, "weighted", 4, 2, "host", 0), (2, "weighted", 1, 2, "host", 0),
+    (2, "rmat", 1, 2, "ipc", 0), (4, "rmat", 1, 2, "ipc", 0), (2, "rmat", 1, 0, "ipc", 0), (3, "rmat", 40, 2, "ipc", 0),
+    (2, "weighted", 4, 2, "ipc", 0), (3, "weighted", 1, 2, "ipc", 0), (2, "rmat", 1, 4, "ipc", 0), (2, "rmat", 1, 4, "host", 0),
+    (4, "rmat", 1, 2, "ipc", 0), (3, "rmat", 8, 2, "host", 0), (8, "rmat", 40, 2, "ipc", 0), (8, "rmat", 1, 2, "ipc", 0),
+    (8, "weighted", 4, 2, "ipc", 0), (2, "rmat", 48, 2, "ipc", 1), (3, "rmat", 41, 2, "ipc", 1),
+    (4, "rmat", 48, 2, "ipc", 1), (3, "rmat", 48, 2, "ipc", 2), (2, "rmat", 41, 2, "ipc", 2)])
+def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiles):
     """Several ranks on one GPU: the Python exchange over gloo host copies, or
     the native chain with the one-sided IPC exchange (ranks pull from each
-    other's memory; same-device IPC stands in for xGMI peers).  tiers = 2:
-    the halo in a hot and a cold tier (three-phase steps).  tiles = 1: the
+    other's memory; same-device IPC stands in for xGMI peers).  tiles = 1: the
     hybrid step on every shard (dense blocks over [own | halo] columns); tiles = 2:
     on every shard but rank 1's (the ranks disagree on the plan)."""
     if not torch.cuda.is_available():
@@ -209,7 +193,7 @@ def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiers, tile
     q = ctx.Queue()
     port = _free_port()
     K = 8
-    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, kind, K, F, q, lds, exchange, tiers, tiles))
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, kind, K, F, q, lds, exchange, tiles))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -287,22 +271,16 @@ def test_native_chain_clenshaw_small_orders(K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,lds,graph,tiers,blocks,clen,tiles", [
-    (1, 2, 1, 1, 0, 1, 0), (1, 0, 1, 1, 0, 1, 0), (8, 3, 1, 1, 0, 1, 0), (8, 3, 0, 1, 0, 1, 0), (40, 3, 1, 1, 0, 1, 0),
-    (40, 3, 1, 2, 0, 1, 0), (8, 3, 0, 2, 0, 1, 0), (1, 0, 1, 2, 0, 1, 0), (1, 2, 1, 2, 0, 1, 0),
-    (40, 3, 1, 1, 4, 1, 0), (8, 3, 1, 1, 3, 0, 0), (1, 0, 1, 1, 4, 1, 0), (1, 0, 1, 1, 2, 0, 0), (1, 2, 1, 1, 4, 1, 0),
-    (12, 3, 1, 1, 1, 1, 0), (48, 3, 1, 1, 0, 1, 1), (41, 3, 0, 1, 0, 1, 1), (48, 3, 1, 2, 0, 1, 1)])
-def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen, tiles):
+@pytest.mark.parametrize("F,lds,graph,clen,tiles", [
+    (1, 2, 1, 1, 0), (1, 0, 1, 1, 0), (8, 3, 1, 1, 0), (8, 3, 0, 1, 0), (40, 3, 1, 1, 0), (40, 3, 0, 0, 0),
+    (8, 3, 1, 0, 0), (1, 0, 1, 0, 0), (12, 3, 1, 1, 0), (48, 3, 1, 1, 1), (41, 3, 0, 1, 1), (48, 3, 0, 1, 1)])
+def test_native_chain_loopback_exchange(F, lds, graph, clen, tiles):
     """The native exchange with real RCCL traffic on one GPU: a one-rank shard
     whose column space is [own | halo] where the halo columns are copies of own
     rows (every entry (i, j) with j % 3 == 0 and (i + j) odd reads the copy).
     Per step the pack kernel + ncclSend/ncclRecv to self must refresh the
-    copies, so the result equals the unsharded chain.  tiers = 2: the first
-    third of the copies is tier 0 (exchanged first, its entries summed by a
-    third step launch while tier 1 is in flight).  blocks > 0: row-block
-    streaming (each step in `blocks` launches, every block's rows sent while
-    the next computes; wg_dist_stream_blocks), with the Clenshaw or the
-    forward chain.  tiles = 1: the hybrid step (csrc/tiles.hip, dense blocks on the
+    copies, so the result equals the unsharded chain, with the Clenshaw or the
+    forward chain (clen).  tiles = 1: the hybrid step (csrc/tiles.hip, dense blocks on the
     matrix cores) over the [own | halo] column space, exchange-then-step."""
     import ctypes
     import wats_hip
@@ -321,8 +299,7 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen, tile
     w_ext = np.concatenate([deg, deg[J]])
     L = wats_hip.NormalizedLaplacian(n, torch.from_numpy(g.indptr), torch.from_numpy(cols.astype(np.int32)), None,
                                      n_cols=n + J.size, w_cols=torch.from_numpy(w_ext), device="cuda:0")
-    # the two-phase steps (off by default) unless the rows are streamed in blocks
-    L.tune(lds=lds, overlap=0 if (blocks or tiles) else 1, clenshaw=clen)
+    L.tune(lds=lds, clenshaw=clen)
     if tiles:
         L.tune(tiles=1, tile_th=8, tile_max=4)
     lib = _lib.load()
@@ -333,12 +310,10 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen, tile
     check(lib.wg_laplacian_map_rows(L.handle, 0, ptr(caller), caller.numel(), ptr(internal), st), "map_rows")
     uid = (ctypes.c_uint8 * 128)()
     check(lib.wg_dist_unique_id(uid), "unique_id")
-    counts = np.array([J.size], np.int64) if tiers == 1 else np.array([J.size // 3, J.size - J.size // 3], np.int64)
+    counts = np.array([J.size], np.int64)
     h = ctypes.c_void_p()
-    check(lib.wg_dist_create_tiered(L.handle, uid, 0, 1, tiers, ptr(internal), counts.ctypes.data,
-                                    counts.ctypes.data, ctypes.byref(h)), "dist_create")
-    if blocks:
-        check(lib.wg_dist_stream_blocks(h, blocks), "stream_blocks")
+    check(lib.wg_dist_create(L.handle, uid, 0, 1, ptr(internal), counts.ctypes.data, counts.ctypes.data,
+                             ctypes.byref(h)), "dist_create")
     try:
         check(lib.wg_dist_set_graph(h, graph), "set_graph")
         rng = np.random.default_rng(4)
@@ -357,13 +332,9 @@ def test_native_chain_loopback_exchange(F, lds, graph, tiers, blocks, clen, tile
         assert_parity(res[0], ref["S"], what=f"loopback F={F} lds={lds} graph={graph}")
         info = (ctypes.c_int64 * 8)()
         check(lib.wg_dist_info(h, info), "dist_info")
-        # the gather-kernel path overlaps the RCCL exchange with the own-column half of each step,
-        # or streams its row blocks
         if tiles:
             assert "tiles:" in L.describe(F), L.describe(F)
-        else:
-            assert info[0] == ((2 if blocks else 1) if (F > 1 or lds == 0) else 0), list(info)
-        assert info[7] == tiers, list(info)
+        assert info[0] == 0 and info[5] == 2 and info[7] == 1, list(info)
         L.profile_enable(True)
         check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")
         tot, cnt = ctypes.c_double(0), ctypes.c_int64(0)

@@ -286,11 +286,8 @@ def test_wats_dropin_on_gpu_matches_reference():
                                    dict(bcast=0, iter=4, block_iter=2, chunk_iter=2),
                                    dict(waves=16, block_iter=4, chunk_iter=2), dict(waves=8, iter=4, block_iter=8),
                                    dict(inkernel_combine=0, iter=2, block_iter=1, chunk_iter=1),
-                                   dict(gbuf=1), dict(hubf=64), dict(hubf=700, waves=16, chunk_iter=2, block_iter=2),
-                                   dict(hubf=5000, waves=8), dict(gbuf=1, iter=2, block_iter=1, chunk_iter=1),
                                    dict(inkernel_combine=1, iter=2, block_iter=1, chunk_iter=2, waves=8),
-                                   dict(fuse_finalize=0), dict(fuse_finalize=0, tile_f=8), dict(xcd=1),
-                                   dict(xcd=1, iter=2, block_iter=1, chunk_iter=1)])
+                                   dict(fuse_finalize=0), dict(fuse_finalize=0, tile_f=8), dict(nt=4), dict(nt=8)])
 def test_tuning_knobs_preserve_results(knobs):
     _check_knobs(knobs, F=12)
 
@@ -316,7 +313,7 @@ def _check_knobs(knobs, F):
     H1, S1 = wats_hip.graph_wavelet_features(L, k=8, X0=torch.from_numpy(X), return_S=True)
     assert_parity(_np(S1), ref["S"], what=f"{knobs} S")
     assert_parity(_np(H1), ref["H"], what=f"{knobs} H")
-    if set(knobs) <= {"bcast", "nt", "inkernel_combine", "xcd"}:
+    if set(knobs) <= {"bcast", "nt", "inkernel_combine"}:
         assert torch.equal(S0, S1), "same plan must give bitwise-identical results"
 
 
@@ -394,10 +391,9 @@ def test_clenshaw_value_free_directed_selfloops(seed):
                                    dict(lds=2, lds_perm=0), dict(lds=2, lds_perm=0, lds_k=1, lds_cb=1024),
                                    dict(lds=4), dict(lds=4, lds_cb=1024), dict(lds=4, lds_cb=32),
                                    dict(lds=4, lds_cb=4096, hub_iter=2, lds_wg=7), dict(lds=4, lds_cb=1024, lds_wg=1),
-                                   dict(lds=4, lds_cb=2048, hub_iter=64), dict(lds=4, lds_cb=1024, hub_vidx=0),
-                                   dict(lds=4, lds_cb=512, hub_vidx=1, hub_iter=1), dict(lds=4, lds_cb=1024, hub_split=1, hub_sell=0),
-                                   dict(lds=4, lds_cb=2048, hub_split=1, hub_iter=3, hub_sell=0),
-                                   dict(lds=4, hub_sell=0), dict(lds=4, lds_cb=4096, hub_pipe=1, hub_sell=0),
+                                   dict(lds=4, lds_cb=2048, hub_iter=64), dict(lds=4, lds_cb=512, hub_iter=1),
+                                   dict(lds=4, lds_cb=2048, hub_iter=3, hub_sell=0),
+                                   dict(lds=4, hub_sell=0), dict(lds=4, lds_cb=4096, hub_sell=0),
                                    dict(lds=4, lds_cb=2048, hub_iter=3), dict(lds=4, lds_cb=1024, hub_iter=64, lds_wg=3)])
 def test_lds1_plans_f1(knobs):
     """The LDS kernel (one and many column blocks, every team width, any

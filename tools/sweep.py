@@ -1,7 +1,8 @@
 """GPU tuning sweep for the step kernel (run on the GPU box).
 
 For a named config: time graph_wavelet_features' step kernels for a grid of
-(iter, chunk_iter) knobs, and attribute time per plan segment (seg_mask).
+(iter, chunk_iter) knobs, and (--segments, a -DWG_TIMING_PROBES build: the
+"seg_mask" key) attribute time per plan segment.
 Writes one JSON line per measurement to stdout."""
 import argparse
 import json
@@ -84,7 +85,7 @@ def main():
     for combo in itertools.product(*[v for _, v in grid]):
         knobs = dict(zip(names, combo))
         first = first or knobs
-        L.tune(seg_mask=-1, **knobs)
+        L.tune(**knobs)
         r = time_chain(L, X, K)
         r.update(config=a.config, keep_order=a.keep_order, F=F, K=K, GBs=bstep / (r["step_us"] * 1e-6) / 1e9, **knobs)
         print(json.dumps(r), flush=True)

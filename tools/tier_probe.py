@@ -1,15 +1,16 @@
-"""How much of a halo exchange the sharded chain hides, on one GPU (run on the GPU box).
+"""Per-rank cost of one shard of the sharded chain with its halo exchange, on one GPU
+(run on the GPU box, with a timing-probe build of the library).
 
 One rank's shard of a row-sharded graph ([own | halo] columns, as wats_hip.dist
 builds it) runs the native chain (csrc/dist.hip) at world 1 with a loopback
 exchange: the halo rows are refreshed from own rows by RCCL send/recv to self,
 then a spinning wave holds the stream for `xdelay` microseconds per exchange
-(the link time an N-GPU run has and one GPU does not; split over the halo tiers
-by rows).  For halo tiers 1 / 2 and overlap off / on, the chain time per
-Chebyshev step at each simulated link time: the difference to xdelay = 0 is
-the exposed part of the exchange.
+(the link time an N-GPU run has and one GPU does not).  Prints the chain time
+per Chebyshev step at each simulated link time (exchange, then the step).
 
-    python tools/tier_probe.py --config reddit --world 8 --F 41 --delays 0,30,60,90
+    make -C efficient-gnn_amd/csrc VARIANT=probes EXTRA_FLAGS=-DWG_TIMING_PROBES
+    WATS_HIP_LIB=$PWD/efficient-gnn_amd/wats_hip/libwats_hip_probes.so \\
+        python tools/tier_probe.py --config reddit --world 8 --F 48 --delays 0,30,60
 """
 import argparse
 import ctypes
@@ -29,8 +30,8 @@ from wats_hip.dist import partition_rows  # noqa: E402
 from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device  # noqa: E402
 
 
-def shard(indptr, ix, deg, b, rank, tiers, hot_frac, dev):
-    """[own | halo] local columns, halo ordered (tier, owner, -degree, id) as build_halo_plan does."""
+def shard(indptr, ix, deg, b, rank, dev):
+    """[own | halo] local columns, halo ordered (owner, -degree, id) as build_halo_plan does."""
     r0, r1 = int(b[rank]), int(b[rank + 1])
     cols = ix[int(indptr[r0]):int(indptr[r1])].to(torch.int64)
     own = (cols >= r0) & (cols < r1)
@@ -38,20 +39,12 @@ def shard(indptr, ix, deg, b, rank, tiers, hot_frac, dev):
     halo_t = torch.unique(remote, sorted=True)
     halo_sorted = halo_t.cpu().numpy()
     owner_sorted = np.searchsorted(b, halo_sorted, side="right") - 1
-    tier = np.zeros(halo_sorted.size, np.int64)
-    if tiers == 2:
-        uses = torch.bincount(torch.searchsorted(halo_t, remote), minlength=halo_t.numel()).cpu().numpy()
-        hot = np.lexsort((halo_sorted, -uses))[:max(1, int(round(hot_frac * halo_sorted.size)))]
-        tier[:] = 1
-        tier[hot] = 0
-    order = np.lexsort((halo_sorted, -deg[halo_sorted].astype(np.float64), owner_sorted, tier))
+    order = np.lexsort((halo_sorted, -deg[halo_sorted].astype(np.float64), owner_sorted))
     rank_of = np.empty(halo_sorted.size, np.int64)
     rank_of[order] = np.arange(halo_sorted.size)
     local = cols - r0
     local[~own] = (r1 - r0) + torch.from_numpy(rank_of).to(dev)[torch.searchsorted(halo_t, remote)]
-    halo = halo_sorted[order]
-    counts = np.bincount(tier, minlength=tiers).astype(np.int64)
-    return r0, r1, local.to(torch.int32), halo, counts
+    return r0, r1, local.to(torch.int32), halo_sorted[order]
 
 
 def main():
@@ -59,15 +52,10 @@ def main():
     ap.add_argument("--config", default="reddit")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
-    ap.add_argument("--F", type=int, default=41)
-    ap.add_argument("--hot-frac", type=float, default=0.1)
-    ap.add_argument("--delays", default="0,30,60,90")
+    ap.add_argument("--F", type=int, default=48)
+    ap.add_argument("--delays", default="0,30,60")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--graph", type=int, default=1, help="replay the chain as a hipGraph (1) or run it eagerly (0)")
-    ap.add_argument("--tiers", default="1,2")
-    ap.add_argument("--blocks", default="", help="comma-separated row-block counts to time streamed (tiers 1)")
-    ap.add_argument("--xskip", type=int, default=0, help="streamed blocks: the simulated link time only (no RCCL)")
-    ap.add_argument("--cu-reserve", type=int, default=0, help="CUs masked off the step kernels' stream")
     a = ap.parse_args()
     n, nnz_t, K, _ = NAMED_CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -77,72 +65,52 @@ def main():
     b = partition_rows(indptr, a.world)
     lib = _lib.load()
     st = torch.cuda.current_stream().cuda_stream
-    delays = [int(x) for x in a.delays.split(",")]
+    r0, r1, local, halo = shard(indptr, ix, deg, b, a.rank, dev)
+    n_own, n_cols = r1 - r0, (r1 - r0) + int(halo.size)
+    w = torch.from_numpy(np.concatenate([deg[r0:r1], deg[halo]]))
+    L = wats_hip.NormalizedLaplacian(n_own, torch.from_numpy(indptr[r0:r1 + 1] - indptr[r0]), local, None,
+                                     n_cols=n_cols, w_cols=w, device=dev)
+    # loopback: halo row h is refreshed from own row h % n_own
+    caller = torch.from_numpy((np.arange(halo.size) % n_own).astype(np.int32)).to(dev)
+    internal = torch.empty_like(caller)
+    check(lib.wg_laplacian_map_rows(L.handle, 0, ptr(caller), caller.numel(), ptr(internal), st), "map_rows")
+    uid = (ctypes.c_uint8 * 128)()
+    check(lib.wg_dist_unique_id(uid), "unique_id")
+    h = ctypes.c_void_p()
+    counts = np.array([halo.size], np.int64)
+    check(lib.wg_dist_create(L.handle, uid, 0, 1, ptr(internal), counts.ctypes.data, counts.ctypes.data,
+                             ctypes.byref(h)), "dist_create")
+    check(lib.wg_dist_set_graph(h, a.graph), "set_graph")
+    X = torch.randn(n_own, a.F, device=dev)
+    S = torch.empty(n_own, a.F, device=dev)
+    H = torch.empty(n_own, a.F, device=dev)
+    print(f"shard {a.rank}/{a.world} rows {n_own} halo {halo.size} nnz {L.nnz}", flush=True)
     res = []
-    for tiers in [int(t) for t in a.tiers.split(",")]:
-        r0, r1, local, halo, counts = shard(indptr, ix, deg, b, a.rank, tiers, a.hot_frac, dev)
-        n_own, n_cols = r1 - r0, (r1 - r0) + int(halo.size)
-        w = torch.from_numpy(np.concatenate([deg[r0:r1], deg[halo]]))
-        L = wats_hip.NormalizedLaplacian(n_own, torch.from_numpy(indptr[r0:r1 + 1] - indptr[r0]), local, None,
-                                         n_cols=n_cols, w_cols=w, device=dev)
-        # loopback: halo row h is refreshed from own row h % n_own
-        caller = torch.from_numpy((np.arange(halo.size) % n_own).astype(np.int32)).to(dev)
-        internal = torch.empty_like(caller)
-        check(lib.wg_laplacian_map_rows(L.handle, 0, ptr(caller), caller.numel(), ptr(internal), st), "map_rows")
-        uid = (ctypes.c_uint8 * 128)()
-        check(lib.wg_dist_unique_id(uid), "unique_id")
-        h = ctypes.c_void_p()
-        check(lib.wg_dist_create_tiered(L.handle, uid, 0, 1, tiers, ptr(internal), counts.ctypes.data,
-                                        counts.ctypes.data, ctypes.byref(h)), "dist_create")
-        check(lib.wg_dist_set_graph(h, a.graph), "set_graph")
-        X = torch.randn(n_own, a.F, device=dev)
-        S = torch.empty(n_own, a.F, device=dev)
-        H = torch.empty(n_own, a.F, device=dev)
-        print(f"tiers {tiers}: shard {a.rank}/{a.world} rows {n_own} halo {halo.size} (tier rows {counts.tolist()}) "
-              f"nnz {L.nnz}", flush=True)
-        modes = [(o, 0) for o in (0, 1)]
-        if tiers == 1 and a.blocks:
-            modes += [(0, int(x)) for x in a.blocks.split(",")]
-        for overlap, nb in modes:
-            check(lib.wg_dist_stream_blocks(h, nb), "stream_blocks")
-            for d in delays:
-                L.tune(overlap=overlap, xdelay=d, xskip=a.xskip if nb else 0, cu_reserve=a.cu_reserve)
-                run = lambda: check(lib.wg_dist_wavelet_features(h, ptr(X), a.F, K, 0.8, ptr(S), ptr(H), st),
-                                    "dist_wavelet_features")
-                for _ in range(3):
-                    run()
-                torch.cuda.synchronize()
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
-                ev[0].record()
-                t0 = time.perf_counter()
-                for i in range(a.reps):
-                    run()
-                    ev[i + 1].record()
-                host_ms = (time.perf_counter() - t0) * 1e3 / a.reps
-                torch.cuda.synchronize()
-                ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(a.reps))[a.reps // 2]
-                info = (ctypes.c_int64 * 8)()
-                check(lib.wg_dist_info(h, info), "dist_info")
-                r = dict(tiers=tiers, overlap=overlap, blocks=nb, xdelay_us=d, chain_ms=ms, us_per_step=ms * 1e3 / K,
-                         overlapped=int(info[0]), host_ms_per_chain=host_ms)
-                if not a.graph and d == 0:   # eager: the step launches' own durations (every phase)
-                    L.profile_enable(True)
-                    run()
-                    torch.cuda.synchronize()
-                    p = L.profile_collect()
-                    L.profile_enable(False)
-                    r.update(step_launches=p["launches"], launch_us_sum_per_step=p["sum_ms"] * 1e3 / K)
-                res.append(r)
-                print(r, flush=True)
-        lib.wg_dist_destroy(h)
-        L.close()
-        torch.cuda.empty_cache()
-    base = {(r["tiers"], r["overlap"], r["blocks"]): r["us_per_step"] for r in res if r["xdelay_us"] == 0}
-    print("exposed exchange (us per step over xdelay = 0):")
+    for d in [int(x) for x in a.delays.split(",")]:
+        L.tune(xdelay=d)   # a timing-probe build only (rejected as an unknown key otherwise)
+        run = lambda: check(lib.wg_dist_wavelet_features(h, ptr(X), a.F, K, 0.8, ptr(S), ptr(H), st),
+                            "dist_wavelet_features")
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
+        ev[0].record()
+        t0 = time.perf_counter()
+        for i in range(a.reps):
+            run()
+            ev[i + 1].record()
+        host_ms = (time.perf_counter() - t0) * 1e3 / a.reps
+        torch.cuda.synchronize()
+        ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(a.reps))[a.reps // 2]
+        r = dict(xdelay_us=d, chain_ms=ms, us_per_step=ms * 1e3 / K, host_ms_per_chain=host_ms)
+        res.append(r)
+        print(r, flush=True)
+    lib.wg_dist_destroy(h)
+    L.close()
+    b0 = res[0]["us_per_step"]
     for r in res:
-        b0 = base.get((r["tiers"], r["overlap"], r["blocks"]), float("nan"))
-        print(f"  tiers {r['tiers']} overlap {r['overlap']} blocks {r['blocks']} xdelay {r['xdelay_us']:4d}: "
-              f"{r['us_per_step']:8.1f} us/step, exposed {r['us_per_step'] - b0:7.1f}")
+        print(f"  xdelay {r['xdelay_us']:4d}: {r['us_per_step']:8.1f} us/step, over xdelay {res[0]['xdelay_us']}: "
+              f"{r['us_per_step'] - b0:7.1f}")
 
 
 if __name__ == "__main__":
