@@ -157,8 +157,12 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value != 1 && value != 2 && value != 4) return fail(WG_ERR_INVALID, "tile_rg must be 1, 2 or 4");
     L->tune.tile_rg = (int32_t)value;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "tile_mfma")) {
+    if (value != 0 && value != 16 && value != 32) return fail(WG_ERR_INVALID, "tile_mfma must be 0 (auto), 16 or 32");
+    L->tune.tile_mfma = (int32_t)value;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_max")) {
-    if (value < 0 || value > 1 << 20) return fail(WG_ERR_INVALID, "tile_max must be in [0 (auto), 2^20]");
+    if (value < 0 || value > 256) return fail(WG_ERR_INVALID, "tile_max must be in [0 (auto), 256]");
     L->tune.tile_max = (int32_t)value;
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;

@@ -190,6 +190,9 @@ struct Tuning {
   int32_t tile_rows = 128;   // hybrid step: rows per row block (64 or 128)
   int32_t probe_tailwin = 0; // timing only (-DWG_TIMING_PROBES): the hybrid tail's columns folded into 1/n of them
   int32_t tile_rg = 1;       // hybrid step, 128-row blocks: 16-row groups per wave (1: 8 waves, 2: 4 waves)
+  int32_t tile_mfma = 0;     // hybrid step, 128-row blocks of width 48 / 64: 16 = v_mfma_f32_16x16x32_bf16,
+                             // 32 = v_mfma_f32_32x32x16_bf16 (cheb_tiles32_kernel: each B read serves 32
+                             // rows); 0 = auto (32 at width 64, else 16; tiles.hip launch_tiles)
   int32_t chain = -1;        // F == 1 small unweighted graphs: the whole chain in one launch (chain.hip); -1 = auto
                              // (<= 2^18 nonzeros, <= 24576 active rows), 0 = off, 1 = whenever it applies
   int32_t chain_wg = 0;      // chain.hip workers (workgroups of 1024 threads; doubled until a worker fits LDS);

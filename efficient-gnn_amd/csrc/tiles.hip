@@ -43,11 +43,13 @@ namespace wg {
 namespace {
 
 constexpr int kTC = 32;  // columns per tile (the MFMA's K)
+constexpr int kItemMax = 256;  // dense blocks per work item (tile_max <= 256)
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 // LDS image of one bf16 piece of a 32-row tile: row r at dword r*S + X*bit3(r) + Y*bit4(r), so the
@@ -89,6 +91,12 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 #ifndef WG_TILES_FLUSH  // computed tiles per float32 -> float64 flush of the block sums
 #define WG_TILES_FLUSH 4  // 917 vs 928 us per step at 1 (Reddit-size F=41, r02_s70), same S to 1e-8
 #endif
+#ifndef WG_TILES_RING  // depth of the tile-load ring in barrier groups: 1 or 2 (3 spills at 80 VGPRs)
+#define WG_TILES_RING 2
+#endif
+#ifndef WG_TILES_GROUP  // dense blocks multiplied per barrier (1 or 2; Reddit-size F = 41: 719 vs 726 us per
+#define WG_TILES_GROUP 2  // step, tile kernel 278 vs 282 us, profiles/r03/s36_s39_tiles32)
+#endif
 #ifndef WG_TILES_MINW
 #define WG_TILES_MINW 6
 #endif
@@ -96,7 +104,7 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 // rows; FW = true: wave w multiplies column block w % NFB for RG row groups, so each B
 // fragment read from LDS serves RG row groups (NFB * 8 / RG waves for 128 rows)
 template <int NFB, int NWV, int RG, bool FW>
-__global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) void cheb_tiles_kernel(TileArgs t) {
+__global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 && NFB < 4 ? WG_TILES_MINW : 4)) void cheb_tiles_kernel(TileArgs t) {
   constexpr int NRW = FW ? NWV / NFB : NWV;  // waves along the rows
   constexpr int NFW = FW ? 1 : NFB;          // column blocks per wave
   constexpr int TR = 16 * NRW * RG;    // rows per row block (RG groups of 16 per wave)
@@ -105,8 +113,10 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) 
   constexpr int NV = kTC * W / 4;      // float4 per tile
   constexpr int PER = (NV + NT - 1) / NT;
   __shared__ uint4 lut[256];                                          // byte -> 8 bf16 (bit j ? 1.0 : 0)
-  __shared__ __attribute__((aligned(16))) uint16_t img[2][3][2 * img_dwords(NFB)];  // [buffer][piece hi/mid/lo][k, f]
-  __shared__ uint32_t msk[2][TR];                                     // [buffer][row] the block's row masks
+  constexpr int PT = NFB < 4 ? WG_TILES_GROUP : 1;     // tiles per barrier group (width 64: VGPRs)
+  constexpr int RD = PT == 1 ? WG_TILES_RING : 1;       // ring depth in groups
+  static_assert(RD == 1 || RD == 2, "ring depth 1 or 2");
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][PT][3][2 * img_dwords(NFB)];  // [buffer][tile][piece hi/mid/lo][k, f]
   const int tid = threadIdx.x;
   for (int e = tid; e < 256; e += NT) {
     uint32_t d[4];
@@ -118,47 +128,63 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) 
   const int4 it = t.items[blockIdx.x];
   const int64_t rb = it.x;
   const int lane = tid & 63, wave = tid >> 6;
+  const int rwave = FW ? wave / NFB : wave;        // the wave's slot along the rows
+  const int fb0 = FW ? wave % NFB : 0;             // its first column block
+  const int mrow = 16 * RG * rwave + (lane & 15);  // this lane's A row of row group 0 (of the block)
+  const int mshift = 8 * (lane >> 4);              // its byte of the 32-bit row mask
+  const int32_t b0 = it.y, n = it.z - it.y;  // n <= kItemMax (build_tile_plan)
+  __shared__ int32_t sbct[kItemMax];         // the item's column tiles: no global load ahead of each tile load
+  for (int e = tid; e < n; e += NT) sbct[e] = t.bct[b0 + e];
+  __syncthreads();
 
-  // a tile's staged data: PER float4 of u and (tid < TR) one row mask, in a 3-deep register
-  // ring (set = tile % 3): a tile's loads are issued three tiles before it is multiplied
-  float4 xs[3][PER];
-  uint32_t ws[3] = {0u, 0u, 0u};
-  auto load = [&](float4 (&x)[PER], uint32_t& w, int32_t b) {
-    const int64_t r0 = (int64_t)t.bct[b] * kTC;
+  // a tile's loads, in a register ring RD tiles deep: PER float4 of u (staged into LDS) and the
+  // row masks of this lane's A rows (never staged: its A fragments are looked up before the
+  // tile's barrier).  The loads are unconditional (threads past the tile and rows past
+  // col_limit read a valid row, zeroed when staged) so that no branch makes the compiler wait
+  // for them where they are issued.
+  int koff[PER], kkv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int v = (tid + i * NT) % NV;
+    kkv[i] = v / (W / 4);
+    koff[i] = (v % (W / 4)) * 4;
+  }
+  float4 xs[RD][PT][PER];
+  uint32_t ws[RD][PT][RG] = {}, oks[RD][PT] = {};
+  auto load = [&](float4 (&x)[PER], uint32_t (&w)[RG], uint32_t& ok, int32_t j) {
+    const int64_t r0 = (int64_t)sbct[j] * kTC;
+    ok = 0u;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int v = tid + i * NT;
-      x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (v < NV) {
-        const int kk = v / (W / 4), f = (v % (W / 4)) * 4;
-        if (r0 + kk < t.col_limit) x[i] = *reinterpret_cast<const float4*>(t.u + (r0 + kk) * t.ld + f);
-      }
+      const int64_t r = r0 + kkv[i];
+      ok |= (r < t.col_limit ? 1u : 0u) << i;
+      x[i] = *reinterpret_cast<const float4*>(t.u + (r < t.col_limit ? r : t.col_limit - 1) * t.ld + koff[i]);
     }
-    if (tid < TR) w = t.bmask[(int64_t)b * TR + tid];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) w[g] = t.bmask[(int64_t)(b0 + j) * TR + mrow + 16 * g];
   };
-  auto store = [&](const float4 (&x)[PER], uint32_t w, int buf) {
+  auto store = [&](const float4 (&x)[PER], uint32_t ok, int buf, int q) {
 #ifdef WG_TILES_PROBE_NO_STORE  // timing attribution only (results wrong): the tile is loaded, not staged
-    if (x[0].x == 12345.f) img[buf][0][tid] = 1;
-    if (tid < TR) msk[buf][tid] = w;
+    if (x[0].x == 12345.f) img[buf][q][0][tid] = 1;
     return;
 #endif
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int v = tid + i * NT;
       if (v < NV) {
-        const int kk = v / (W / 4), f = (v % (W / 4)) * 4;
+        const int kk = kkv[i], f = koff[i];
+        const float4 xv = (ok >> i) & 1u ? x[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         uint32_t h[4], m[4], l[4];
-        split3(x[i].x, h[0], m[0], l[0]);
-        split3(x[i].y, h[1], m[1], l[1]);
-        split3(x[i].z, h[2], m[2], l[2]);
-        split3(x[i].w, h[3], m[3], l[3]);
+        split3(xv.x, h[0], m[0], l[0]);
+        split3(xv.y, h[1], m[1], l[1]);
+        split3(xv.z, h[2], m[2], l[2]);
+        split3(xv.w, h[3], m[3], l[3]);
         const int o = img_row<NFB>(kk) + f;
-        *reinterpret_cast<uint2*>(&img[buf][0][o]) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-        *reinterpret_cast<uint2*>(&img[buf][1][o]) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
-        *reinterpret_cast<uint2*>(&img[buf][2][o]) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+        *reinterpret_cast<uint2*>(&img[buf][q][0][o]) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        *reinterpret_cast<uint2*>(&img[buf][q][1][o]) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+        *reinterpret_cast<uint2*>(&img[buf][q][2][o]) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
       }
     }
-    if (tid < TR) msk[buf][tid] = w;
   };
 
   double acc[RG][NFW][4];
@@ -174,10 +200,6 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) 
   const int trow = 8 * (lane >> 4) + ((lane & 15) >> 2);
   const int tcolo = 4 * (lane & 3);
   const int tr_lo = img_row<NFB>(trow) + tcolo, tr_hi = img_row<NFB>(trow + 4) + tcolo;
-  const int rwave = FW ? wave / NFB : wave;       // the wave's slot along the rows
-  const int fb0 = FW ? wave % NFB : 0;            // its first column block
-  const int mrow = 16 * RG * rwave + (lane & 15);  // this lane's A row of row group 0 (of the block)
-  const int mshift = 8 * (lane >> 4);              // its byte of the 32-bit row mask
   // float32 MFMA sums of the last <= WG_TILES_FLUSH computed tiles, added to the float64 acc
   f32x4 cacc[NFW][RG];
   int nacc = 0;
@@ -196,18 +218,7 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) 
   for (int fb = 0; fb < NFW; ++fb)
 #pragma unroll
     for (int g = 0; g < RG; ++g) cacc[fb][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int buf) {
-    uint32_t mw[RG];
-    bool any = false;
-#pragma unroll
-    for (int g = 0; g < RG; ++g) {
-      mw[g] = msk[buf][mrow + 16 * g];
-      any = any || mw[g] != 0u;
-    }
-    if (!__any(any)) return;  // none of the wave's rows has an entry in this tile (wave-uniform)
-    bf16x8 a[RG];
-#pragma unroll
-    for (int g = 0; g < RG; ++g) a[g] = __builtin_bit_cast(bf16x8, lut[(mw[g] >> mshift) & 0xFFu]);
+  auto compute = [&](int buf, int q, const bf16x8 (&a)[RG]) {
 #pragma unroll
     for (int fw = 0; fw < NFW; ++fw) {
       const int fb = fb0 + fw;
@@ -217,8 +228,8 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) 
 #ifdef WG_TILES_PROBE_NO_TR  // timing attribution only (results wrong): no B reads from LDS
         const s16x4 lo4 = {(short)(p + fb), 0, 0, 0}, hi4 = {0, 0, 0, (short)lane};
 #else
-        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_lo + 16 * fb]));
-        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_hi + 16 * fb]));
+        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][q][p][tr_lo + 16 * fb]));
+        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][q][p][tr_hi + 16 * fb]));
 #endif
         const s16x8 bv = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
         const bf16x8 b = __builtin_bit_cast(bf16x8, bv);
@@ -235,32 +246,54 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) 
     if (++nacc == WG_TILES_FLUSH) flush();
   };
 
-  const int32_t b0 = it.y, n = it.z - it.y;
+  if (n <= 0) return;
+  // every load unconditional (past the last tile: the last tile again), so the ring's registers
+  // are written only by their loads and the compiler waits for each load only where it is staged
+  // groups of PT tiles (the last group's missing tiles are never multiplied)
+  const int32_t ng = (n + PT - 1) / PT;
+  auto load_group = [&](int slot, int32_t g) {
 #pragma unroll
-  for (int q = 0; q < 3; ++q)
-    if (q < n) load(xs[q], ws[q], b0 + q);
-  if (n > 0) store(xs[0], ws[0], 0);
-  // tile j (j % 6 == I): multiplied from LDS buffer I % 2; its register set I % 3 is refilled
-  // with tile j + 3 first; tile j + 1 is split into the other buffer after
-  auto tile = [&](auto I, int32_t j) {
-    constexpr int i = decltype(I)::value;
-    __syncthreads();  // tile j staged; the other buffer no longer read
-    if (j + 3 < n) load(xs[i % 3], ws[i % 3], b0 + j + 3);
-    compute(i % 2);
-    if (j + 1 < n) store(xs[(i + 1) % 3], ws[(i + 1) % 3], (i + 1) % 2);
+    for (int q = 0; q < PT; ++q) {
+      const int32_t j = g * PT + q;
+      load(xs[slot][q], ws[slot][q], oks[slot][q], j < n ? j : n - 1);
+    }
   };
-  for (int32_t j = 0; j < n; j += 6) {
-    tile(std::integral_constant<int, 0>{}, j);
-    if (j + 1 >= n) break;
-    tile(std::integral_constant<int, 1>{}, j + 1);
-    if (j + 2 >= n) break;
-    tile(std::integral_constant<int, 2>{}, j + 2);
-    if (j + 3 >= n) break;
-    tile(std::integral_constant<int, 3>{}, j + 3);
-    if (j + 4 >= n) break;
-    tile(std::integral_constant<int, 4>{}, j + 4);
-    if (j + 5 >= n) break;
-    tile(std::integral_constant<int, 5>{}, j + 5);
+  auto store_group = [&](int slot, int buf) {
+#pragma unroll
+    for (int q = 0; q < PT; ++q) store(xs[slot][q], oks[slot][q], buf, q);
+  };
+#pragma unroll
+  for (int r = 0; r < RD; ++r) load_group(r, r);
+  store_group(0, 0);
+  // group g (g % 2 == I): its A fragments looked up from register set I % RD, then (barrier) it
+  // is multiplied from LDS buffer I % 2 while set I % RD is refilled with group g + RD; group
+  // g + 1 is split into the other buffer after
+  auto group = [&](auto I, int32_t g) {
+    constexpr int i = decltype(I)::value;
+    bf16x8 a[PT][RG];
+    bool any[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      any[q] = false;
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) {
+        a[q][rg] = __builtin_bit_cast(bf16x8, lut[(ws[i % RD][q][rg] >> mshift) & 0xFFu]);
+        any[q] = any[q] || ws[i % RD][q][rg] != 0u;
+      }
+      // some row of the wave has an entry in this tile (wave-uniform), and the tile exists
+      any[q] = __any(any[q]) && g * PT + q < n;
+    }
+    __syncthreads();  // group g staged; the other buffer no longer read
+    load_group(i % RD, g + RD < ng ? g + RD : ng - 1);
+#pragma unroll
+    for (int q = 0; q < PT; ++q)
+      if (any[q]) compute(i % 2, q, a[q]);
+    if (g + 1 < ng) store_group((i + 1) % RD, (i + 1) % 2);
+  };
+  for (int32_t g = 0; g < ng; g += 2) {
+    group(std::integral_constant<int, 0>{}, g);
+    if (g + 1 >= ng) break;
+    group(std::integral_constant<int, 1>{}, g + 1);
   }
   if (nacc > 0) flush();
   // D layout of 16x16x32: column = lane & 15, row = 4 (lane >> 4) + i
@@ -275,6 +308,147 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 ? WG_TILES_MINW : 4)) 
 #pragma unroll
       for (int fw = 0; fw < NFW; ++fw) dst[16 * (fb0 + fw) + (lane & 15)] = acc[g][fw][i];
     }
+}
+
+// The same product on v_mfma_f32_32x32x16_bf16 (tile_mfma = 32; widths 48 and 64, 128-row
+// blocks).  Wave w multiplies rows 32 (w & 3) .. +31 by signal columns 32 (w >> 2) .. +31 (a
+// 48-wide signal pads its second column block with zero columns whose sums are not stored):
+// each B fragment (16 tile columns x 32 signal columns) read from LDS serves 32 rows instead of
+// 16, so a tile costs 12 transposed reads per wave (48 KB per workgroup) against 18 (72 KB) at
+// width 48 and 24 (96 KB) at width 64.  The LDS image rows are 96 bf16 (48 dwords) apart: the
+// four rows a 16-lane group reads in one transposed read hit distinct banks.
+constexpr int kImg32 = 96;  // bf16 per image row
+#ifndef WG_TILES32_MINW
+#define WG_TILES32_MINW 4  // 16 float64 sums per lane: 6 waves per SIMD (80 VGPRs) spills
+#endif
+template <int W>
+__global__ __launch_bounds__(512, WG_TILES32_MINW) void cheb_tiles32_kernel(TileArgs t) {
+  constexpr int NT = 512, TR = 128;
+  constexpr int NV = kTC * W / 4;  // float4 per tile
+  static_assert(NV <= NT && (W == 48 || W == 64), "one float4 of the tile per thread, two 32-column blocks");
+  __shared__ uint4 lut[256];
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][3][kTC * kImg32];  // [buffer][piece][k * 96 + f]
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 256; e += NT) {
+    uint32_t d[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      d[q] = (((e >> (2 * q)) & 1) ? 0x3F80u : 0u) | (((e >> (2 * q + 1)) & 1) ? 0x3F800000u : 0u);
+    lut[e] = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+  if (W < 64)  // the padding columns W .. 63 of every image row: zero once (never stored to)
+    for (int e = tid; e < 2 * 3 * kTC * (64 - W) / 8; e += NT) {
+      const int q = e % ((64 - W) / 8), r = e / ((64 - W) / 8);  // r = (buffer, piece, k)
+      *reinterpret_cast<uint4*>(&img[0][0][0] + r * kImg32 + W + 8 * q) = make_uint4(0u, 0u, 0u, 0u);
+    }
+  const int4 it = t.items[blockIdx.x];
+  const int64_t rb = it.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int32_t b0 = it.y, n = it.z - it.y;
+  __shared__ int32_t sbct[kItemMax];
+  for (int e = tid; e < n; e += NT) sbct[e] = t.bct[b0 + e];
+  __syncthreads();
+  const int rgrp = wave & 3, nb = wave >> 2;
+  const int mrow = 32 * rgrp + (lane & 31);  // this lane's A row: tile columns 8 (lane >> 5) + 0..7 (+16)
+  const int mshift = 8 * (lane >> 5);
+  // the load ring of cheb_tiles_kernel (unconditional loads, the lane's own row mask)
+  constexpr int RD = WG_TILES_RING;
+  const int kk = (tid % NV) / (W / 4), f = ((tid % NV) % (W / 4)) * 4;
+  float4 xs[RD];
+  uint32_t ws[RD] = {}, oks[RD] = {};
+  auto load = [&](float4& x, uint32_t& w, uint32_t& ok, int32_t j) {
+    const int64_t r = (int64_t)sbct[j] * kTC + kk;
+    ok = r < t.col_limit ? 1u : 0u;
+    x = *reinterpret_cast<const float4*>(t.u + (r < t.col_limit ? r : t.col_limit - 1) * t.ld + f);
+    w = t.bmask[(int64_t)(b0 + j) * TR + mrow];
+  };
+  auto store = [&](const float4& x0, uint32_t ok, int buf) {
+    if (tid < NV) {
+      const float4 x = ok ? x0 : make_float4(0.f, 0.f, 0.f, 0.f);
+      uint32_t h[4], m[4], l[4];
+      split3(x.x, h[0], m[0], l[0]);
+      split3(x.y, h[1], m[1], l[1]);
+      split3(x.z, h[2], m[2], l[2]);
+      split3(x.w, h[3], m[3], l[3]);
+      const int o = kk * kImg32 + f;
+      *reinterpret_cast<uint2*>(&img[buf][0][o]) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      *reinterpret_cast<uint2*>(&img[buf][1][o]) = make_uint2(m[0] | (m[1] << 16), m[2] | (m[3] << 16));
+      *reinterpret_cast<uint2*>(&img[buf][2][o]) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+    }
+  };
+
+  // B fragment of k-half h: lane holds tile columns k = 16 h + 8 (lane >> 5) + 0..7 of signal column
+  // 32 nb + (lane & 31); its 16-lane group reads rows k0 + (lane & 15) / 4 (+4), 4 columns each
+  const int tr_lo = (8 * (lane >> 5) + ((lane & 15) >> 2)) * kImg32 + 32 * nb + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const int tr_hi = tr_lo + 4 * kImg32;
+  double acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+  f32x16 cacc = {};
+  int nacc = 0;
+  auto compute = [&](int buf, const bf16x8& a0, const bf16x8& a1) {
+#pragma unroll
+    for (int p = 2; p >= 0; --p) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_lo + 16 * h * kImg32]));
+        const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(&img[buf][p][tr_hi + 16 * h * kImg32]));
+        const s16x8 bv = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+        cacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(h ? a1 : a0, __builtin_bit_cast(bf16x8, bv), cacc, 0, 0, 0);
+      }
+    }
+    if (++nacc == WG_TILES_FLUSH) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] += (double)cacc[i];
+      cacc = f32x16{};
+      nacc = 0;
+    }
+  };
+
+  if (n <= 0) return;
+  // every load unconditional (past the last tile: the last tile again), so the ring's registers
+  // are written only by their loads and the compiler waits for each load only where it is staged
+#pragma unroll
+  for (int q = 0; q < RD; ++q) load(xs[q], ws[q], oks[q], q < n ? q : n - 1);
+  store(xs[0], oks[0], 0);
+  auto tile = [&](auto I, int32_t j) {
+    constexpr int i = decltype(I)::value;
+    const uint32_t mw = ws[i % RD];
+    const bf16x8 a0 = __builtin_bit_cast(bf16x8, lut[(mw >> mshift) & 0xFFu]);
+    const bf16x8 a1 = __builtin_bit_cast(bf16x8, lut[(mw >> (16 + mshift)) & 0xFFu]);
+    const bool any = __any(mw != 0u);
+    __syncthreads();
+    load(xs[i % RD], ws[i % RD], oks[i % RD], j + RD < n ? j + RD : n - 1);
+    if (any) compute(i % 2, a0, a1);
+    if (j + 1 < n) store(xs[(i + 1) % RD], oks[(i + 1) % RD], (i + 1) % 2);
+  };
+  for (int32_t j = 0; j < n; j += 6) {
+    tile(std::integral_constant<int, 0>{}, j);
+    if (j + 1 >= n) break;
+    tile(std::integral_constant<int, 1>{}, j + 1);
+    if (j + 2 >= n) break;
+    tile(std::integral_constant<int, 2>{}, j + 2);
+    if (j + 3 >= n) break;
+    tile(std::integral_constant<int, 3>{}, j + 3);
+    if (j + 4 >= n) break;
+    tile(std::integral_constant<int, 4>{}, j + 4);
+    if (j + 5 >= n) break;
+    tile(std::integral_constant<int, 5>{}, j + 5);
+  }
+  if (nacc > 0)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += (double)cacc[i];
+  // D layout of 32x32x16: column = lane & 31, row = 8 (i / 4) + 4 (lane >> 5) + i % 4
+  const int col = 32 * nb + (lane & 31);
+  if (col >= W) return;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int rl = 32 * rgrp + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
+    const int64_t row = rb * TR + rl;
+    if (it.w < 0 && row >= t.n_plan) continue;
+    double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * TR + rl) * W;
+    dst[col] = acc[i];
+  }
 }
 
 // row blocks split over several workgroups: part = their slots summed in slot order
@@ -396,6 +570,7 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   // shards want more workgroups: 259 vs 242 and 184 vs 153; profiles/r02/s80-s81)
   const int64_t nblk = (int64_t)bct.size();
   if (tmax <= 0) tmax = n_plan >= 100000 ? 128 : 64;
+  tmax = std::min(tmax, kItemMax);
   for (size_t q0 = 0; q0 < rbs.size(); ++q0) {
     const int rb = rbs[q0].x, first = rbs[q0].y;
     const int32_t nb = (int32_t)((q0 + 1 < rbs.size() ? rbs[q0 + 1].y : nblk) - first);
@@ -535,13 +710,19 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
     // each B fragment (half the LDS reads)
     const int rg = p->rows == 128 ? L->tune.tile_rg : 1;
     const dim3 grid(p->n_items), block(4 * p->rows / rg);
+    // 32x32x16 at width 64 by default (Reddit-size F = 64: 845 vs 872 us per step; at width 48
+    // the padded shape loses, 785 vs 723: profiles/r03/s36_s39_tiles32)
+    const int shape = L->tune.tile_mfma > 0 ? L->tune.tile_mfma : (F == 64 ? 32 : 16);
+    const bool m32 = shape == 32 && p->rows == 128 && (F == 48 || F == 64);
 #define WG_TILES(NFB)                                                                                  \
   if (p->rows == 64) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 1, false>), grid, block, 0, stream, t);             \
   else if (rg == 4) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 2 * NFB, 4, true>), dim3(p->n_items), dim3(128 * NFB), 0, \
                                        stream, t);                                                                  \
   else if (rg == 2) hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 4, 2, false>), grid, block, 0, stream, t);             \
   else hipLaunchKernelGGL((cheb_tiles_kernel<NFB, 8, 1, false>), grid, block, 0, stream, t);
-    switch (F / 16) {
+    if (m32 && F == 48) hipLaunchKernelGGL(cheb_tiles32_kernel<48>, grid, dim3(512), 0, stream, t);
+    else if (m32) hipLaunchKernelGGL(cheb_tiles32_kernel<64>, grid, dim3(512), 0, stream, t);
+    else switch (F / 16) {
       case 1: WG_TILES(1) break;
       case 2: WG_TILES(2) break;
       case 3: WG_TILES(3) break;

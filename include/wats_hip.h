@@ -240,7 +240,7 @@ int wg_chain_status(wg_laplacian_t L, int32_t* timed_out_host);
  * shape), "chunk_iter" (chunk-mode nonzeros per sub-group),
  * "clenshaw" (wavelet_features' heat sum, default 1), "tiles" (the hybrid
  * step, DESIGN.md 4.6: -1 auto, 0 off, 1 whenever it applies; with "tile_th",
- * "tile_rows", "tile_max", "tile_rg"), "nt" (store hints), and the keys listed in
+ * "tile_rows", "tile_max", "tile_rg", "tile_mfma"), "nt" (store hints), and the keys listed in
  * efficient-gnn_amd/csrc/internal.h (struct Tuning).  Plan-shaping keys are
  * synchronous (they drop cached plans); launch-time keys are not.  Timing
  * probes whose results are wrong on purpose ("seg_mask", "probe",
