@@ -199,6 +199,10 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
     const float xg = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
     return xl + xg;
   };
+  // the column ids stream once per step (8M R-MAT: 1 GB against a 4 MB L2 per XCD): non-temporal
+  // loads keep them from evicting the gathered u lines (8M R-MAT K=32 step 1030 vs 1147 us;
+  // non-temporal u gathers instead: 2068 us; profiles/r03/s50_hub_nt)
+  auto ld_id = [](const int32_t* p) { return __builtin_nontemporal_load(p); };
   for (;;) {
     int g = 0;
     if (lane == 0) g = atomicAdd(&s_next, 1);
@@ -220,27 +224,28 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
       const int32_t* __restrict__ cs = a.csell + (int64_t)gs.x * 64 + lane;
       int32_t i = 0;
       for (; i + 3 < gs.y; i += 4) {
-        const int32_t c0 = cs[(int64_t)i * 64], c1 = cs[(int64_t)(i + 1) * 64], c2 = cs[(int64_t)(i + 2) * 64],
-                      c3 = cs[(int64_t)(i + 3) * 64];
+        const int32_t c0 = ld_id(cs + (int64_t)i * 64), c1 = ld_id(cs + (int64_t)(i + 1) * 64),
+                      c2 = ld_id(cs + (int64_t)(i + 2) * 64), c3 = ld_id(cs + (int64_t)(i + 3) * 64);
         const float x0 = x_of(c0), x1 = x_of(c1), x2 = x_of(c2), x3 = x_of(c3);
         acc += (double)x0;
         acc += (double)x1;
         acc += (double)x2;
         acc += (double)x3;
       }
-      for (; i < gs.y; ++i) acc += (double)x_of(cs[(int64_t)i * 64]);
+      for (; i < gs.y; ++i) acc += (double)x_of(ld_id(cs + (int64_t)i * 64));
     } else if (act) {
       const int32_t e1 = rp[row + 1];
       int32_t e = rp[row] + q;
       for (; e + 3 * ln < e1; e += 4 * ln) {
-        const int32_t c0 = col[e], c1 = col[e + ln], c2 = col[e + 2 * ln], c3 = col[e + 3 * ln];
+        const int32_t c0 = ld_id(col + e), c1 = ld_id(col + e + ln), c2 = ld_id(col + e + 2 * ln),
+                      c3 = ld_id(col + e + 3 * ln);
         const float x0 = x_of(c0), x1 = x_of(c1), x2 = x_of(c2), x3 = x_of(c3);
         acc += (double)x0;
         acc += (double)x1;
         acc += (double)x2;
         acc += (double)x3;
       }
-      for (; e < e1; e += ln) acc += (double)x_of(col[e]);
+      for (; e < e1; e += ln) acc += (double)x_of(ld_id(col + e));
     }
     for (int o = ln >> 1; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
     if (act && q == 0) lds1_epilogue(a, row, acc);
