@@ -213,6 +213,44 @@ def _rel_err(got, ref) -> float:
 
 
 # ----------------------------------------------------------------------------- row-sharded runs
+_GRAPHS: dict = {}
+
+
+def shared_graph(config, seed, world, rank, device):
+    """The row-sharded runs' graph (GPU R-MAT generator), generated ONCE, by
+    rank 0, and broadcast to every rank: (indptr int64, indices int32) on this
+    rank's device, cached per (config, seed).  Ranks used to generate it each
+    for themselves; with several ranks on ONE device (the one-GPU rehearsal of
+    the N > 1 bench) the concurrent generators sat in torch.unique's radix sort
+    for minutes (profiles/r03/s49_rehearse, DESIGN.md 7: its onesweep passes
+    spin on their predecessors' look-back, and kernels of several processes
+    time-share one device's queues), so no rank depends on that any more."""
+    key = (config, seed)
+    if key in _GRAPHS:
+        return _GRAPHS[key]
+    from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
+    n_t, nnz_t = NAMED_CONFIGS[config][:2]
+    if world == 1:
+        ip, ix = rmat_graph_device(n_t, nnz_t, seed=seed, device=device)
+    else:
+        on = device if dist.get_backend() == "nccl" else torch.device("cpu")
+        size = torch.zeros(1, dtype=torch.int64, device=on)
+        if rank == 0:
+            ip, ix = rmat_graph_device(n_t, nnz_t, seed=seed, device=device)
+            size[0] = ix.numel()
+            ip, ix = ip.to(on), ix.to(on)
+        dist.broadcast(size, 0)
+        if rank != 0:
+            ip = torch.empty(n_t + 1, dtype=torch.int64, device=on)
+            ix = torch.empty(int(size.item()), dtype=torch.int32, device=on)
+        dist.broadcast(ip, 0)
+        dist.broadcast(ix, 0)
+        ip, ix = ip.to(device), ix.to(device)
+        _log(f"graph {config}: {ix.numel()} nonzeros generated on rank 0, broadcast to {world} ranks")
+    _GRAPHS[key] = (ip, ix)
+    return ip, ix
+
+
 def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, exchange="rccl",
                 median_reps: int = 0, check: bool = True, min_time: float = 0.0):
     """One graph (generated identically on every rank, on the GPU) split into
@@ -222,13 +260,13 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     Returns the result dict (meaningful on rank 0)."""
     from wats_hip import NormalizedLaplacian, graph_wavelet_features
     from wats_hip.dist import ShardedWavelet, partition_rows
-    from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
+    from wats_hip.graphgen import NAMED_CONFIGS
 
     n_t, nnz_t, K_def, F_def = NAMED_CONFIGS[config]
     K = K if K is not None else K_def
     F = F if F is not None else F_def
     _log(f"sharded {config} ({exchange}): generating")
-    indptr_d, indices_d = rmat_graph_device(n_t, nnz_t, seed=seed, device=device)
+    indptr_d, indices_d = shared_graph(config, seed, world, rank, device)
     indptr = indptr_d.cpu().numpy()
     _log(f"sharded {config} ({exchange}): generated; building the shard")
     bounds = partition_rows(indptr, world)
@@ -236,8 +274,6 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     lo, hi = int(indptr[r0]), int(indptr[r1])
     cols = indices_d[lo:hi].cpu().numpy()
     nnz_global = int(indptr[-1])
-    if not check:
-        del indptr_d, indices_d
     torch.cuda.empty_cache()
     with _stdout_to_stderr():   # RCCL prints its version banner at communicator init: keep stdout one JSON line
         sw = ShardedWavelet(indptr[r0:r1 + 1] - lo, cols, None, n_t, bounds, exchange=exchange, device=device,
@@ -302,7 +338,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     if check:
         chk = _check_vs_unsharded(sw, indptr_d, indices_d, n_t, r0, r1, F, K, s_heat, world, device,
                                   NormalizedLaplacian, graph_wavelet_features)
-        del indptr_d, indices_d
+    del indptr_d, indices_d
     if world > 1:
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
     nnz_lhat = _allreduce(float(sw.L.nnz), dist.ReduceOp.SUM, device) if world > 1 else float(sw.L.nnz)
@@ -383,7 +419,7 @@ def _check_vs_unsharded(sw, indptr_d, indices_d, n, r0, r1, F, K, s_heat, world,
                     "the same GPU; max over ranks and columns of max|dS| / max|S|"}
 
 
-def one_gpu_chain(config, K, F, steps, seed, s_heat, device) -> dict:
+def one_gpu_chain(config, K, F, steps, seed, s_heat, device, world=1, rank=0) -> dict:
     """The N > 1 headline's workload unsharded on ONE GPU (every rank runs it on
     its own device, no collective; rank 0's is reported): the same graph
     (GPU generator, same seed), K, F and s through wg_wavelet_features, so the
@@ -391,11 +427,11 @@ def one_gpu_chain(config, K, F, steps, seed, s_heat, device) -> dict:
     (VERDICT r2 item 6)."""
     import wats_hip
     from wats_hip import NormalizedLaplacian
-    from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
+    from wats_hip.graphgen import NAMED_CONFIGS
     n_t, nnz_t, K_def, F_def = NAMED_CONFIGS[config]
     K = K if K is not None else K_def
     F = F if F is not None else F_def
-    ip, ix = rmat_graph_device(n_t, nnz_t, seed=seed, device=device)
+    ip, ix = shared_graph(config, seed, world, rank, device)
     L = NormalizedLaplacian(n_t, ip, ix, device=device)
     del ip, ix
     gen = torch.Generator(device=device)
@@ -848,7 +884,8 @@ def main():
                                  "same_config_1gpu: the same config unsharded on one GPU")
         try:
             torch.cuda.empty_cache()
-            line["same_config_1gpu"] = one_gpu_chain(cfg, args.K, args.F, args.steps, args.seed, args.s, device)
+            line["same_config_1gpu"] = one_gpu_chain(cfg, args.K, args.F, args.steps, args.seed, args.s, device,
+                                                     world, rank)
             line["same_config_1gpu"]["speedup"] = line["value"] / line["same_config_1gpu"]["value"]
         except Exception as exc:  # noqa: BLE001
             line["same_config_1gpu"] = {"error": f"{type(exc).__name__}: {exc}"}

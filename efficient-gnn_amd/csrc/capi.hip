@@ -6,6 +6,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <tuple>
 #include <vector>
 
 #include "internal.h"
@@ -30,6 +33,30 @@ __global__ void map_rows_kernel(int64_t n, const int32_t* __restrict__ map, cons
   if (i < n) out[i] = map[rows[i]];
 }
 }  // namespace
+
+int ensure_dyn_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<const void*, int, int>> done;
+  int dev = 0;
+  WG_HIP_TRY(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_tuple(fn, dev, bytes);
+  if (done.count(key)) return WG_OK;
+  WG_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.insert(key);
+  return WG_OK;
+}
+
+int n_cus(int dev) {
+  static int cached[64] = {0};
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
 
 int fail(int code, const char* fmt, ...) {
   char buf[1024];
@@ -172,9 +199,21 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "chain_wg")) {
     if (value < 0 || value > 64) return fail(WG_ERR_INVALID, "chain_wg must be in [0 (auto), 64]");
     L->tune.chain_wg = (int32_t)value;
+  } else if (!strcmp(key, "chain_fault")) {
+    if (value < 0 || value > kChainMaxK) return fail(WG_ERR_INVALID, "chain_fault must be in [0, %d]", kChainMaxK);
+    L->tune.chain_fault = (int32_t)value;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "chain_xcd")) {
     L->tune.chain_xcd = value ? 1 : 0;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "gather4")) {
+    if (value != 0 && value != 1 && value != 21 && value != 22 && value != 31 && value != 41)
+      return fail(WG_ERR_INVALID, "gather4 must be 0 (off), 1 (default loop), 21, 22, 31 or 41");
+    L->tune.gather4 = (int32_t)(value == 1 ? 21 : value);
+    return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "sell")) {
+    L->tune.sell = value ? 1 : 0;
+    return WG_OK;  // launch-time choice (the SELL arrays are built with the plan on first use)
   } else if (!strcmp(key, "graph")) {
     if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "graph must be -1 (auto), 0 or 1");
     L->tune.graph = (int32_t)value;
@@ -187,6 +226,16 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;
   } else if (!strcmp(key, "probe")) {
     L->tune.probe = value ? 1 : 0;  // the gathers alone: no epilogue operands
+    return WG_OK;
+  } else if (!strcmp(key, "trace")) {
+    L->tune.trace = (int32_t)std::max<int64_t>(0, value);  // 1-based step launch to record, 0 = off
+    L->trace_seq = 0;
+    return WG_OK;
+  } else if (!strcmp(key, "probe_h2")) {
+    L->tune.probe_h2 = (int32_t)value;  // negative: the skeleton probes (step.hip, step_dev.h)
+    return WG_OK;
+  } else if (!strcmp(key, "probe_fold")) {
+    L->tune.probe_fold = (int32_t)value;  // -1: ids from one 4-KB window (accumulate_u4)
     return WG_OK;
   } else if (!strcmp(key, "probe_tailwin")) {
     L->tune.probe_tailwin = (int32_t)std::max<int64_t>(0, std::min<int64_t>(value, 1024));  // plan-time
@@ -351,7 +400,10 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
   if (!lp && L->tune.clenshaw && K >= 1 && L->unit && L->tune.uscale &&
       L->tune.hot == 0 && !L->tune.probe && tiles_wanted(L, Fp))
     if (int rc0 = get_tile_plan(L, /*active_only=*/true, Fp, &tp0)) return rc0;
-  const bool u0 = tp0 != nullptr;
+  // the padded-CSR gathers (step.hip accumulate_u4) are value-free: the first step too, on u_0
+  const bool g4 = !lp && !tp0 && L->tune.clenshaw && K >= 1 && L->unit && L->tune.uscale && L->tune.hot == 0 &&
+                  gather4_applies(L, Fp) && step_single_tile(L, Fp, {L->ws});
+  const bool u0 = tp0 != nullptr || g4;
   const size_t need = (u0 ? 4 : 3) * stride + 2 * ustride;
   if (L->ws_floats < need) {
     WG_HIP_TRY(hipStreamSynchronize(stream));
@@ -460,6 +512,7 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     return fail(WG_ERR_INVALID, "wg_wavelet_features: sharded handle (halo columns); use wg_cheb_step");
   hipStream_t stream = as_stream(stream_);
   if (L->n_rows == 0) return WG_OK;
+  if (int rc = chain1_check(L)) return rc;
   if (L->warm_gen != L->tune_gen) {  // a tune drops plans: every width builds again
     L->warm_widths.clear();
     L->warm_gen = L->tune_gen;
@@ -531,6 +584,17 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
   WG_HIP_TRY(hipStreamWaitEvent(stream, g.join, 0));
   return WG_OK;
 }
+
+#ifdef WG_TIMING_PROBES
+// probe builds only (not in the ABI header): the recorded step-launch timeline, 4 x u64 per wave
+int wg_probe_trace(wg_laplacian_t L, unsigned long long* host, int64_t n, int64_t* got) {
+  if (!L || !got) return fail(WG_ERR_INVALID, "wg_probe_trace: NULL argument");
+  WG_HIP_TRY(hipDeviceSynchronize());
+  *got = std::min<int64_t>(n, L->trace_n);
+  if (*got > 0 && host) WG_HIP_TRY(hipMemcpy(host, L->trace_buf, sizeof(unsigned long long) * *got, hipMemcpyDeviceToHost));
+  return WG_OK;
+}
+#endif
 
 int wg_chain_status(wg_laplacian_t L, int32_t* timed_out) {
   if (!L || !timed_out) return fail(WG_ERR_INVALID, "wg_chain_status: NULL argument");

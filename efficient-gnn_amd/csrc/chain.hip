@@ -63,7 +63,10 @@ struct ChainArgs {
   const float* x0;            // [n_act] X0 in internal order
   const float* u0;            // [n_act] u_0 = X0 * dinv (prologue)
   uint64_t* gbuf;             // [2][ustride] tagged granules {float bits, tag << 32}
-  int32_t* bar;               // [2] error flag, [3] launch epoch (bumped by the prologue)
+  int32_t* bar;               // [2] epoch of the last timed-out launch, [3] launch epoch (bumped by the prologue)
+  int32_t* host_flag;         // host-mapped: epoch of the last timed-out launch (read by the next API call)
+  int64_t wait_ticks;         // a granule wait gives up after this many wall-clock ticks (~0.5 s)
+  int32_t fault_phase;        // fault injection (tuning key "chain_fault", tests): worker 0 skips this phase's publish
   float* S;                   // caller order
   float* H;
   double c[kChainMaxK + 1];   // heat coefficients exp(-s k)
@@ -93,17 +96,19 @@ __device__ __forceinline__ uint64_t ld_sc1_u64(const uint64_t* p) {
 
 // u[0, n) <- the granules of one phase (n <= kChainThreads * kStageMax): every element of the
 // thread in flight at once (one memory round trip when the producers are done), re-polled with
-// a short sleep until every tag is the phase's; false after ~0.5 s (a worker never published)
+// a short sleep until every tag is the phase's; false after wait_ticks of the constant-rate
+// wall clock (a worker never published)
 constexpr int kStageMax = 24;
 #ifndef WG_CHAIN_SLEEP  // s_sleep units (64 cycles) between polls of granules not yet published
 #define WG_CHAIN_SLEEP 1
 #endif
-__device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, int n, uint32_t tag, int tid) {
+__device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, int n, uint32_t tag, int tid,
+                                             int64_t wait_ticks) {
   uint32_t pending = 0;
 #pragma unroll
   for (int q = 0; q < kStageMax; ++q)
     if (tid + q * kChainThreads < n) pending |= 1u << q;
-  int spins = 0;
+  const uint64_t t0 = wall_clock64();
   while (pending) {
     uint64_t v[kStageMax];
 #pragma unroll
@@ -117,7 +122,7 @@ __device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, int n,
     }
     if (pending) {
       __builtin_amdgcn_s_sleep(WG_CHAIN_SLEEP);
-      if (++spins > (1 << 22)) return false;
+      if ((int64_t)(wall_clock64() - t0) > wait_ticks) return false;
     }
   }
   return true;
@@ -164,6 +169,12 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
   uint16_t* id = reinterpret_cast<uint16_t*>(smem + lay.id);         // [ne]
   int2* pas = reinterpret_cast<int2*>(smem + lay.pas);               // [npass] the worker's wave passes
   const uint32_t ep = (uint32_t)a.bar[3] & 0x3ffffffu;             // this launch's epoch (tags ep * 64 + j)
+  // A granule wait that gave up leaves stale u in this worker's LDS: from then on the worker
+  // publishes NaN for its rows and writes NaN S / H, so every result that depends on the
+  // missing data is NaN (never silently wrong), and the launch's epoch is recorded in bar[2]
+  // and in the host-mapped flag (wg_wavelet_features / wg_chain_status report it).
+  __shared__ int s_bad;
+  if (tid == 0) s_bad = 0;
   // ---- stage the worker's rows, its pass table and u_0
   for (int i = tid; i < nr; i += kChainThreads) {
     const double di = a.dinv[row0 + i];
@@ -185,6 +196,7 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
   const int wave = tid >> 6, lane = tid & 63;
   const int pb = wp[wave] - pass0, pe = wp[wave + 1] - pass0;  // this wave's passes (no workgroup sync inside a phase)
   const int K = a.K;
+  bool bad = false;  // uniform over the workgroup (read after a barrier)
   for (int j = 1; j <= K; ++j) {
     const int k = K - j;
     const double cacc = (j == 1) ? (k == 0 ? a.c[K] : 2.0 * a.c[K]) : (k == 0 ? 1.0 : 2.0);
@@ -228,13 +240,15 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
           const double t = ck * (double)x0o[li] + cacc * lb - (prevs ? (double)pu[li] * rdi : 0.0);
           if (k > 0) {
             pu[li] = ui;  // b_{k+1} (as u): the next phase's b_{k+2}
-            const float un = (float)(t * di);
+            const float un = bad ? __int_as_float(0x7fc00000) : (float)(t * di);
             if (a.P == 1) u2[row] = un;
-            else __hip_atomic_store(gnext + row, tag | __float_as_uint(un), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (!(j == a.fault_phase && w == 0))
+              __hip_atomic_store(gnext + row, tag | __float_as_uint(un), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           } else {
             const int32_t r = a.perm[row];
-            a.S[r] = (float)t;
-            a.H[r] = (float)(t / (fabs(t) + 1e-8));
+            const float nan = __int_as_float(0x7fc00000);
+            a.S[r] = bad ? nan : (float)t;
+            a.H[r] = bad ? nan : (float)(t / (fabs(t) + 1e-8));
           }
         }
       }
@@ -249,10 +263,14 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
       float* t = u;
       u = u2;
       u2 = t;
-    } else if (!stage_tagged(u, gnext, a.n_act, (uint32_t)(tag >> 32), tid)) {
-      __hip_atomic_store(a.bar + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // results invalid
+    } else if (!stage_tagged(u, gnext, a.n_act, (uint32_t)(tag >> 32), tid, a.wait_ticks)) {
+      if (atomicExch(&s_bad, 1) == 0) {  // one lane per worker records the failed launch
+        __hip_atomic_store(a.bar + 2, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.host_flag) __hip_atomic_store(a.host_flag, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
     __syncthreads();
+    bad = s_bad != 0;
 #ifdef WG_CHAIN_TRACE
     tr[ntr++] = clock64();
 #endif
@@ -371,6 +389,10 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   if (!rc) rc = dmalloc(&p->u0, (size_t)std::max<int64_t>(na, 1));
   if (!rc) rc = dmalloc(&p->x0, (size_t)std::max<int64_t>(na, 1));
   if (rc) return rc;
+  WG_HIP_TRY(hipHostMalloc((void**)&p->host_flag, sizeof(int32_t), hipHostMallocMapped));
+  *p->host_flag = 0;
+  WG_HIP_TRY(hipHostGetDevicePointer((void**)&p->d_host_flag, p->host_flag, 0));
+  p->seen = 0;
   WG_HIP_TRY(hipMemset(p->bar, 0, 4 * sizeof(int32_t)));
   WG_HIP_TRY(hipMemset(p->gbuf, 0, 2 * p->ustride * sizeof(uint64_t)));  // tag 0: never a live phase's
   char buf[192];
@@ -387,6 +409,7 @@ void ChainPlan::release() {
   for (void* q : {(void*)ids, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar, (void*)gbuf, (void*)u0,
                   (void*)x0})
     (void)hipFree(q);
+  if (host_flag) (void)hipHostFree(host_flag);
   *this = ChainPlan{};
 }
 
@@ -433,11 +456,14 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   hipLaunchKernelGGL(chain_prologue_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, n,
                      (int64_t)p->n_act, L->perm, X0, L->dinv, coef, p->x0, p->u0, S, H, p->bar + 3);
   WG_LAUNCH_CHECK();
-  static bool attr_set = false;
-  if (!attr_set) {
-    WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_chain1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kChainLds));
-    attr_set = true;
+  if (int rc = ensure_dyn_lds((const void*)cheb_chain1_kernel, kChainLds)) return rc;
+  static int wall_khz[64] = {0};  // the wall clock's rate per device (constant)
+  int dev = 0;
+  WG_HIP_TRY(hipGetDevice(&dev));
+  if (dev >= 0 && dev < 64 && !wall_khz[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) != hipSuccess || v <= 0) v = 100000;
+    wall_khz[dev] = v;
   }
   ChainArgs a{};
   a.n_act = p->n_act;
@@ -457,6 +483,9 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.u0 = p->u0;
   a.gbuf = p->gbuf;
   a.bar = p->bar;
+  a.host_flag = p->d_host_flag;
+  a.wait_ticks = (int64_t)((dev >= 0 && dev < 64) ? wall_khz[dev] : 100000) * 500;  // 0.5 s
+  a.fault_phase = L->tune.chain_fault;
   a.S = S;
   a.H = H;
   for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
@@ -467,13 +496,27 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   return prof_mark(L, stream, false);
 }
 
+int chain1_check(wg_laplacian_s* L) {
+  // a previous launch of the one-launch chain that gave up a wait (its S / H are NaN): reported
+  // by the next call instead of launching over it (the flag is host-mapped: no sync)
+  ChainPlan* p = L->chain1;
+  if (!p || !p->host_flag) return WG_OK;
+  const int32_t failed = __atomic_load_n(p->host_flag, __ATOMIC_ACQUIRE);
+  if (failed == p->seen) return WG_OK;
+  p->seen = failed;
+  return fail(WG_ERR_TIMEOUT,
+              "wg_wavelet_features: a previous one-launch chain (csrc/chain.hip) gave up waiting for a worker; its "
+              "S / H were written as NaN (was the GPU shared with another kernel?)");
+}
+
 int chain1_status(wg_laplacian_s* L, int32_t* timed_out) {
   *timed_out = 0;
   if (!L->chain1) return WG_OK;
-  int32_t h[4] = {0, 0, 0, 0};
   WG_HIP_TRY(hipDeviceSynchronize());
-  WG_HIP_TRY(hipMemcpy(h, L->chain1->bar, sizeof(h), hipMemcpyDeviceToHost));
-  *timed_out = h[2];
+  ChainPlan* p = L->chain1;
+  const int32_t failed = __atomic_load_n(p->host_flag, __ATOMIC_ACQUIRE);
+  *timed_out = failed != p->seen ? 1 : 0;  // since the last report (here or by wg_wavelet_features)
+  p->seen = failed;
   return WG_OK;
 }
 

@@ -76,22 +76,10 @@ struct IpcPull {
   int32_t world, rank;
 };
 
-// signal: first record that this rank completed one more phase (count += 1,
-// stored into every peer's flag for this rank, after a system-scope release);
-// then wait until every peer has completed as many phases as this rank
-__device__ __forceinline__ void ipc_wait(const IpcPull& p, bool signal) {
+// wait until every peer has completed as many phases as this rank (ipc_signal_kernel counts them)
+__device__ __forceinline__ void ipc_wait(const IpcPull& p) {
   __shared__ int64_t s_target;
-  if (threadIdx.x == 0) {
-    int64_t c = *p.count;
-    if (signal) {
-      __threadfence_system();
-      c += 1;
-      *p.count = c;
-      for (int q = 0; q < p.world; ++q)
-        if (q != p.rank) __hip_atomic_store(p.peer_flags[q] + p.rank, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    s_target = c;
-  }
+  if (threadIdx.x == 0) s_target = *p.count;
   __syncthreads();
   if (threadIdx.x < 64) {
     const int q = threadIdx.x;
@@ -166,12 +154,32 @@ __global__ void spin_kernel(uint64_t ticks) {
 }
 #endif
 
-// (signal the previous phase and) wait for the peers; one workgroup
-__global__ void ipc_wait_kernel(IpcPull p, int signal) { ipc_wait(p, signal != 0); }
+// wait for the peers; one workgroup
+__global__ void ipc_wait_kernel(IpcPull p, int) { ipc_wait(p); }
 
-// this rank completed one more phase: count += 1, then tell every peer
-__global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, int64_t* const* peer_flags) {
+// this rank completed one more phase: every XCD's L2 written back, count += 1, then every peer told.
+// Cross-device ordering: a peer pulls this rank's slot rows with system-scope loads
+// over xGMI, which read memory (HBM / Infinity Cache), never this device's L2s; the slot rows were
+// written by the phase's kernels on up to all 8 XCDs, with write-through (sc1) stores (the step
+// kernels' u_k) or plain stores (permute-in, scale_rows: the first vector).  So that this does not
+// rest on the scope of the runtime's end-of-kernel release (which this code cannot read, eager or
+// replayed from a hipGraph), kIpcSignalBlocks workgroups (one or more on every XCD: workgroups are
+// dealt round-robin) each write back their XCD's L2 (__threadfence_system = buffer_wbl2 sc0 sc1 +
+// its wait), count their XCD in a mask and arrive on a monotonic counter; the last to arrive
+// checks that n_xcc distinct XCDs released (else err |= 2: the ordering is not guaranteed) and
+// stores the flags with system-scope release stores.
+constexpr int kIpcSignalBlocks = 64;
+__global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, int64_t* const* peer_flags,
+                                  uint32_t* arrive, int32_t n_xcc, int32_t* err) {
   if (threadIdx.x != 0) return;
+  __threadfence_system();
+  uint32_t xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  __hip_atomic_fetch_or(arrive + 1, 1u << (xcc & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if ((old + 1) % kIpcSignalBlocks != 0) return;
+  const uint32_t mask = __hip_atomic_exchange(arrive + 1, 0u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (__popc(mask) < n_xcc) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __threadfence_system();
   const int64_t c = *count + 1;
   *count = c;
@@ -225,7 +233,9 @@ struct wg_dist_s {
   int64_t F_max = 0, slot_floats = 0;
   float* region = nullptr;            // [slot 0][slot 1][flags: world int64]
   int64_t* count = nullptr;           // phases completed (device)
-  int32_t* err = nullptr;             // wait timed out (device)
+  int32_t* err = nullptr;             // 1: a wait timed out; 2: a signal's release missed an XCD (device)
+  uint32_t* arrive = nullptr;         // ipc_signal_kernel: [0] arrivals (monotonic), [1] XCD mask
+  int32_t n_xcc = 1;                  // XCDs of this device
   int32_t* halo_owner = nullptr;
   int32_t* halo_src = nullptr;
   std::vector<void*> peer_region;     // IPC-mapped, nullptr for self
@@ -237,7 +247,8 @@ struct wg_dist_s {
     if (comm) (void)ncclCommDestroy(comm);
     for (void* q : peer_region)
       if (q) (void)hipIpcCloseMemHandle(q);
-    for (void* q : {(void*)region, (void*)count, (void*)err, (void*)halo_owner, (void*)halo_src, (void*)peer_flags})
+    for (void* q : {(void*)region, (void*)count, (void*)err, (void*)arrive, (void*)halo_owner, (void*)halo_src,
+                    (void*)peer_flags})
       (void)hipFree(q);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (fork) (void)hipEventDestroy(fork);
@@ -264,13 +275,17 @@ struct wg_dist_s {
   }
 
   int ipc_signal(hipStream_t st) {
-    hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, st, count, world, rank, peer_flags);
+    hipLaunchKernelGGL(ipc_signal_kernel, dim3(kIpcSignalBlocks), dim3(64), 0, st, count, world, rank, peer_flags,
+                       arrive, n_xcc, err);
     WG_LAUNCH_CHECK();
     return WG_OK;
   }
 
+  // (signal the previous phase, then) wait for the peers
   int ipc_wait_only(hipStream_t st, bool signal_first = false) {
-    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, st, pull, signal_first ? 1 : 0);
+    if (signal_first)
+      if (int rc = ipc_signal(st)) return rc;
+    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, st, pull, 0);
     WG_LAUNCH_CHECK();
     return WG_OK;
   }
@@ -425,6 +440,12 @@ struct wg_dist_s {
       // shard that declined its plan must not send unscaled rows to one that took it).
       const bool u0 = useu && K >= 1;
       if (!rc && u0) rc = launch_scale_rows(L, n_own, Fp, x0, A[0], st);
+      // the closed-form own rows [n_active, n_own) are never written by the steps (active rows only)
+      // nor gathered, but a hybrid step's dense tile stages whole 32-row column tiles: keep them
+      // zero in the other slot (finite u_0 in A[0]) so that 0 x stale never enters an MFMA sum
+      if (!rc && L->n_active < n_own &&
+          hipMemsetAsync(A[1] + L->n_active * Fp, 0, sizeof(float) * (n_own - L->n_active) * Fp, st) != hipSuccess)
+        rc = fail(WG_ERR_HIP, "wg_dist: zero the closed-form rows");
       for (int32_t j = 1; j <= K && !rc; ++j) {
         const int32_t k = K - j;  // this phase computes b_k (k = 0: the final S)
         float* cur = A[(j - 1) & 1];
@@ -436,10 +457,20 @@ struct wg_dist_s {
         cl.uprev = useu && prev_stored;
         cl.uout = useu;                   // ignored on the final step (k == 0 writes S)
         rc = exchange(cur, sendbuf, Fp, st, (j - 1) & 1);
+        // only the active rows: purely isolated own rows (no entries, w = 0; relabelled to the end
+        // of the shard by the prologue) are never gathered by any rank and have T_k = (-1)^k X0, so
+        // their S is written in closed form by the finalize below (WATS.py:55, -1 diagonal)
         if (!rc)
           rc = launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr, k == 0 ? nullptr : A[j & 1],
-                           k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, st, false, nullptr, &cl);
+                           k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, st, /*active_only=*/true, nullptr, &cl);
       }
+      if (!rc) {
+        double coef = 0.0;  // closed-form rows: S = X0 * sum_k (-1)^k c_k (as wg_wavelet_features)
+        for (int32_t k = 0; k <= K; ++k) coef += ((k & 1) ? -1.0 : 1.0) * c[k];
+        if (sig) rc = ipc_signal(st);  // phase K
+        if (!rc) rc = launch_finalize(L, F, sint, x0, coef, S, H, st, Fp);
+      }
+      return rc;
     } else {
       for (int32_t k = 1; k <= K && !rc; ++k) {
         float* cur = A[(k - 1) & 1];
@@ -614,6 +645,14 @@ int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
   if (int rc = dmalloc(reinterpret_cast<char**>(&D->region), bytes)) return rc;
   if (int rc = dmalloc(&D->count, 1)) return rc;
   if (int rc = dmalloc(&D->err, 1)) return rc;
+  if (int rc = dmalloc(&D->arrive, 2)) return rc;
+  WG_HIP_TRY(hipMemset(D->arrive, 0, 2 * sizeof(uint32_t)));
+  {
+    int dev = 0, nx = 1;
+    WG_HIP_TRY(hipGetDevice(&dev));
+    if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || nx < 1) nx = 1;
+    D->n_xcc = std::min(nx, 16);
+  }
   WG_HIP_TRY(hipMemset(D->region, 0, bytes));
   WG_HIP_TRY(hipMemset(D->count, 0, sizeof(int64_t)));
   WG_HIP_TRY(hipMemset(D->err, 0, sizeof(int32_t)));

@@ -15,6 +15,12 @@ namespace wg {
 
 int fail(int code, const char* fmt, ...);
 
+// hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) once per (kernel, current device):
+// the attribute is per device, so a process-wide "done" flag would skip it on a second device
+int ensure_dyn_lds(const void* fn, int bytes);
+// compute units of device `dev` (cached per device)
+int n_cus(int dev);
+
 #define WG_HIP_TRY(expr)                                                                       \
   do {                                                                                         \
     hipError_t e_ = (expr);                                                                    \
@@ -76,6 +82,11 @@ struct Plan {
   double* partial = nullptr;    // device [n_chunks][width]
   int2* rowchunks = nullptr;    // device [n_split] {first chunk, chunk count}
   int32_t* arrivals = nullptr;  // device [n_split] monotonic arrival counters (in-kernel combine)
+  // value-free VEC-4 team waves (step.hip build_sell): each wave's column ids in SELL-G order --
+  // turn t, chunk c (4 ids), sub-group g at sell[wmeta[w].x + (2 t + c) G + g] -- padded with
+  // kPadCol to the wave's longest sub-group, wmeta[w] = {first chunk, turns} per wave w
+  int2* wmeta = nullptr;        // device [total_blocks * nw]
+  int4* sell = nullptr;         // device
   std::string text;
   void release();
 };
@@ -189,6 +200,9 @@ struct Tuning {
                              // 0 = auto: 128 from 100 k rows, else 64 (tiles.hip, r02_s80-s81)
   int32_t tile_rows = 128;   // hybrid step: rows per row block (64 or 128)
   int32_t probe_tailwin = 0; // timing only (-DWG_TIMING_PROBES): the hybrid tail's columns folded into 1/n of them
+  int32_t trace = 0;         // timing only (-DWG_TIMING_PROBES): record the trace-th step launch's per-wave timeline
+  int32_t probe_h2 = 0;      // timing only (-DWG_TIMING_PROBES): see StepArgs
+  int32_t probe_fold = 0;    // timing only (-DWG_TIMING_PROBES): see StepArgs
   int32_t tile_rg = 1;       // hybrid step, 128-row blocks: 16-row groups per wave (1: 8 waves, 2: 4 waves)
   int32_t tile_mfma = 0;     // hybrid step, 128-row blocks of width 48 / 64: 16 = v_mfma_f32_16x16x32_bf16,
                              // 32 = v_mfma_f32_32x32x16_bf16 (cheb_tiles32_kernel: each B read serves 32
@@ -200,6 +214,11 @@ struct Tuning {
                              // (PubMed-size K=16: 8 / 16 / 32 / 64 workers 187 / 139 / 119 / 113 us per chain,
                              // profiles/r03/s13_chain1_worker_sweep.log)
   int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works)
+  int32_t chain_fault = 0;   // chain.hip fault injection (tests of the timeout path): worker 0 does not publish
+                             // phase chain_fault; the launch's S / H come out NaN and the next call fails
+  int32_t gather4 = 21;      // value-free VEC-4 steps on the padded CSR (step.hip build_pcol / accumulate_u4):
+                             // 0 = off, else 10 x chunks per turn + turns of ids in flight (21, 22, 31, 41)
+  int32_t sell = 1;          // padded-CSR steps: team waves read their ids in SELL order (step.hip build_sell)
   int32_t graph = 0;         // wg_wavelet_features: replay the chain as a hipGraph from its 3rd call with the same
                              // arguments (1 = on; -1 = small chains only, active nnz x width <= 2^22).  Off: the
                              // replay measured SLOWER than eager launches on this stack, +2.7 us per kernel node
@@ -216,7 +235,10 @@ struct ChainPlan {
   int4* wdesc = nullptr;      // device [P]: {row0, row1, e0, e1}
   int32_t* wpass = nullptr;   // device [P][17]: each worker's waves' ranges of passes
   int2* passes = nullptr;     // device: one wave pass {first row, rows | log2 team size << 8}
-  int32_t* bar = nullptr;     // device [4]: [2] error flag, [3] launch epoch
+  int32_t* bar = nullptr;     // device [4]: [2] epoch of the last timed-out launch, [3] launch epoch
+  int32_t* host_flag = nullptr;    // host-mapped (pinned): epoch of the last timed-out launch
+  int32_t* d_host_flag = nullptr;  // its device address
+  int32_t seen = 0;                // the host_flag value already reported
   uint64_t* gbuf = nullptr;   // device [2][ustride]: tagged u granules {float bits, tag << 32}
   float* u0 = nullptr;        // device [n_act]: u_0 = X0 * dinv
   float* x0 = nullptr;        // device [n_act]: X0 in internal order
@@ -269,6 +291,10 @@ struct wg_laplacian_s {
   bool values_null = false;   // created with values == NULL (unweighted by construction: every shard of the
                               // graph agrees, so a row-sharded chain may exchange u = b * dinv)
   double* dinv = nullptr;     // [n_cols] internal column order: 1 / sqrt(w_j) (w_j == 0 -> 1)
+  unsigned long long* trace_buf = nullptr;  // -DWG_TIMING_PROBES timeline (knob "trace")
+  int64_t trace_n = 0, trace_seq = 0;
+  int32_t* prp = nullptr;     // padded CSR of the value-free VEC-4 gathers (build_pcol): row pointers
+  int32_t* pcol = nullptr;    // ... and column ids, rows padded to multiples of 4 (lazily)
   std::vector<int64_t> halo_off;  // row shard: halo columns [n_rows + halo_off[q], n_rows + halo_off[q+1])
                                   // come from peer q, each group in descending degree (wg_dist_create)
   wg::Lds1Plan* lds1[2] = {nullptr, nullptr};  // [active_only]
@@ -333,6 +359,9 @@ int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, flo
 // caller rows (stride F) -> internal rows (stride Fp), pad columns zeroed
 int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);
+int build_pcol(wg_laplacian_s* L);
+// the value-free VEC-4 gathers on the padded CSR apply to an F-wide (internal width) signal
+bool gather4_applies(const wg_laplacian_s* L, int64_t F);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);
 int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start);
 // tiles.hip: the hybrid step's plan (*out = nullptr: not applicable) and its dense-block pass,
@@ -350,6 +379,8 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
                   hipStream_t stream);
 void release_chain1(wg_laplacian_s* L);
 int chain1_status(wg_laplacian_s* L, int32_t* timed_out);
+// WG_ERR_TIMEOUT (once) when a launch of the one-launch chain gave up a wait since the last report
+int chain1_check(wg_laplacian_s* L);
 // lds1.hip
 int get_lds1_plan(wg_laplacian_s* L, bool active_only, Lds1Plan** out);  // *out = nullptr: not applicable
 void release_lds1(wg_laplacian_s* L);

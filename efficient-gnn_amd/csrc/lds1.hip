@@ -734,17 +734,6 @@ __global__ __launch_bounds__(256) void lds2_fill_kernel(int32_t n, int32_t nb, i
   }
 }
 
-int n_cus(int dev) {
-  static int cached[64] = {0};
-  if (dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    cached[dev] = v;
-  }
-  return cached[dev];
-}
-
 // row groups of the teams kernels (modes 1 and 4) and their workgroup split.
 // h: block-major row pointers [nb * n + 1] (entries of block b, row r =
 // [h[b*n+r], h[b*n+r+1])).
@@ -1201,7 +1190,6 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
                      hipStream_t stream) {
   if (p->n == 0) return WG_OK;
   if (int rc = prof_mark(L, stream, true)) return rc;
-  static bool attr_set[2] = {false, false};
   const size_t lds = (size_t)p->lchunks * 32 * sizeof(float);
   Lds1Args a{};
   a.brp = p->brp;
@@ -1224,12 +1212,7 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
   a.alpha0 = alpha0;
   a.alpha_k = alpha_k;
   if (p->mode == 4) {
-    static bool attr4 = false;
-    if (!attr4) {
-      WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_hub1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024 - 64));
-      attr4 = true;
-    }
+    if (int rc = ensure_dyn_lds((const void*)cheb_hub1_kernel, 160 * 1024 - 64)) return rc;
     a.brp = L->rowptr;
     a.gcol = p->hcol ? p->hcol : L->col;
     a.hub = p->hub;
@@ -1248,12 +1231,7 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
     const void* fn2 = depth == 8   ? (const void*)cheb_lds2_kernel<8>
                       : depth == 4 ? (const void*)cheb_lds2_kernel<4>
                                    : (const void*)cheb_lds2_kernel<2>;
-    static bool attr2[3] = {false, false, false};
-    const int ai = depth == 8 ? 2 : depth == 4 ? 1 : 0;
-    if (!attr2[ai]) {
-      WG_HIP_TRY(hipFuncSetAttribute(fn2, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
-      attr2[ai] = true;
-    }
+    if (int rc = ensure_dyn_lds(fn2, 160 * 1024 - 64)) return rc;
     Lds2Args A{};
     A.chunk = p->chunk;
     A.wdesc = p->wdesc;
@@ -1264,11 +1242,7 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
     const int kpl = L->tune.lds_k;
     if (kpl == 2 || kpl == 4) {
       const void* fn3 = kpl == 4 ? (const void*)cheb_lds3_kernel<4> : (const void*)cheb_lds3_kernel<2>;
-      static bool attr3[2] = {false, false};
-      if (!attr3[kpl == 4]) {
-        WG_HIP_TRY(hipFuncSetAttribute(fn3, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
-        attr3[kpl == 4] = true;
-      }
+      if (int rc = ensure_dyn_lds(fn3, 160 * 1024 - 64)) return rc;
       if (kpl == 4)
         hipLaunchKernelGGL(cheb_lds3_kernel<4>, dim3(p->n_wg), dim3(kLdsThreads), lds + sizeof(float), stream, A);
       else
@@ -1286,10 +1260,7 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
   }
   const bool direct = p->nb == 1;
   const void* fn = direct ? (const void*)cheb_lds1_kernel<true> : (const void*)cheb_lds1_kernel<false>;
-  if (!attr_set[direct]) {
-    WG_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 64));
-    attr_set[direct] = true;
-  }
+  if (int rc = ensure_dyn_lds(fn, 160 * 1024 - 64)) return rc;
   if (direct)
     hipLaunchKernelGGL(cheb_lds1_kernel<true>, dim3(p->n_wg), dim3(kLdsThreads), lds, stream, a);
   else

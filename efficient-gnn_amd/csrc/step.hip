@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "internal.h"
 
@@ -43,7 +44,9 @@ namespace {
 
 // One work unit of the plan (a group of team rows, a block row or a split
 // chunk) processed by one workgroup of NW waves.
-template <int VEC, bool BCAST, int NW, bool HOT>
+// P4: 0 = the gather loops of acc_range; else the padded-CSR value-free loop accumulate_u4 with
+// P4 / 10 chunks per turn and the ids of P4 % 10 turns ahead in flight
+template <int VEC, bool BCAST, int NW, bool HOT, int P4 = 0>
 __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restrict__ segs, int nseg, int32_t unit,
                                           int32_t H) {
   __shared__ double red[NW * 64 * VEC];
@@ -52,6 +55,9 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     if (unit >= segs[i].blk_begin) si = i;
   const Seg seg = segs[si];
   if (!((a.seg_mask >> si) & 1)) return;  // timing attribution only
+#ifdef WG_TIMING_PROBES
+  if (a.probe_h2 == -4) return;  // skeleton probe: the unit lookup alone
+#endif
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int LF = a.LF;
@@ -71,8 +77,25 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     const int64_t row = (int64_t)seg.begin + (int64_t)(unit - seg.blk_begin) * (NW * tpw) + wave * tpw + team;
     const bool active = team < tpw && row < seg.end;
     EpiIn<VEC> in;
+#ifdef WG_TIMING_PROBES
+    if (a.probe_h2 == -3) {  // skeleton probe: no row work at all, one store per row
+      if (active && ns == 0) store_vec<VEC>(a.xk + row * a.ld + fs * VEC, acc);
+      return;
+    }
+#endif
     if (active) {
       if (ns == 0) epi_prefetch<VEC>(a, row, fs, in);
+#ifdef WG_TIMING_PROBES
+      if (a.probe_h2 == -2) {  // skeleton probe: no ids or gathers (the row pointers, epilogue kept)
+        acc[0] += (double)(a.prp[row + 1] - a.prp[row]);
+      } else
+#endif
+      if constexpr (P4 && VEC == 4) {  // padded CSR: the row's 4-entry chunks ns, ns + LN, ...
+        if (a.sell)  // the same chunks in the wave's SELL order (one coalesced id read per turn)
+          accumulate_sell(a, a.wmeta[(int64_t)unit * NW + wave], 64 / LF, lane / LF, fs, acc);
+        else
+          accumulate_u4<P4 / 10, P4 % 10>(a, a.prp[row] + 4 * ns, a.prp[row + 1], 4 * LN, fs, acc);
+      } else {
       int32_t e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
       phase_range(a, row, e0, e1);
       if constexpr (VEC == 1 && !HOT) {
@@ -80,6 +103,7 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
         else acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
       } else {
         acc_range<VEC, BCAST, HOT>(a, e0 + ns, e1, LN, a.xm1 + fs * VEC, acc, H, fs, lane - fs);
+      }
       }
     }
     reduce_subgroups<VEC>(acc, LN, LF, team * TS, fs);
@@ -112,7 +136,14 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
   const int fs = lane - sg * LF;
   EpiIn<VEC> in;
   if (seg.mode == 1 && threadIdx.x < LF) epi_prefetch<VEC>(a, row, threadIdx.x, in);
-  if constexpr (VEC == 1 && !HOT) {
+  if constexpr (P4 && VEC == 4) {
+    // padded CSR: a split chunk's range maps to the same offsets in the padded row (pads only at
+    // its end; chunk lengths are multiples of 4); the workgroup's sub-groups deal its 4-entry chunks
+    const int32_t pr0 = a.prp[row];
+    const int32_t q0 = pr0 + (e0 - a.rowptr[row]);
+    const int32_t q1 = (e1 == a.rowptr[row + 1]) ? a.prp[row + 1] : pr0 + (e1 - a.rowptr[row]);
+    if (sg < G) accumulate_u4<P4 / 10, P4 % 10>(a, q0 + 4 * (wave * G + sg), q1, 4 * NW * G, fs, acc);
+  } else if constexpr (VEC == 1 && !HOT) {
     if (a.vidx && LF == 1) {
       // chunk-aligned ranges: for split chunks e0 is a multiple of CH (>= 4) from the row start, so
       // neighbouring chunks never both take an aligned 4-group (masking keeps the bounds exact anyway)
@@ -182,11 +213,30 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
   }
 }
 
-template <int VEC, bool BCAST, int NW>
+template <int VEC, bool BCAST, int NW, int P4 = 0>
 __global__ __launch_bounds__(NW * 64) void cheb_step_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
   // units are dealt to the 8 XCDs round-robin (blockIdx order): the units are in descending row
   // length, so an XCD-contiguous order gave one XCD every hub row (3x slower, r02_s65)
-  unit_body<VEC, BCAST, NW, false>(a, segs, nseg, (int32_t)blockIdx.x, 0);
+#ifdef WG_TIMING_PROBES
+  const unsigned long long r0 = wall_clock64(), c0 = clock64();
+#endif
+  unit_body<VEC, BCAST, NW, false, P4>(a, segs, nseg, (int32_t)blockIdx.x, 0);
+#ifdef WG_TIMING_PROBES
+  // timeline probe: per wave {block | wave << 24 | xcc << 28 | hw_id << 32, start, end (100 MHz wall
+  // clock), shader cycles}
+  if (a.trace && (threadIdx.x & 63) == 0) {
+    const unsigned long long r1 = wall_clock64(), c1 = clock64();
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    unsigned long long* t = a.trace + ((size_t)blockIdx.x * NW + (threadIdx.x >> 6)) * 4;
+    t[0] = (unsigned long long)blockIdx.x | ((unsigned long long)(threadIdx.x >> 6) << 24) |
+           ((unsigned long long)(xcc & 15) << 28) | ((unsigned long long)hw << 32);
+    t[1] = r0;
+    t[2] = r1;
+    t[3] = c1 - c0;
+  }
+#endif
 }
 
 // Persistent F == 1 variant: one workgroup per CU stages T_{k-1}[0, H) in LDS
@@ -405,6 +455,18 @@ int divisor_at_least(int G, int64_t want) {
 template <int VEC, int NW>
 void launch_main(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const dim3 grid(plan.tab.total_blocks), block(NW * 64);
+  if constexpr (VEC == 4) {
+    if (a.pcol) {  // a.vidx carries the padded-CSR loop variant (gather4 tuning value)
+      const Seg* sg = plan.d_segs;
+      switch (a.vidx) {
+        case 31: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 31>), grid, block, 0, stream, a, sg, plan.tab.n); break;
+        case 22: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 22>), grid, block, 0, stream, a, sg, plan.tab.n); break;
+        case 41: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 41>), grid, block, 0, stream, a, sg, plan.tab.n); break;
+        default: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 21>), grid, block, 0, stream, a, sg, plan.tab.n);
+      }
+      return;
+    }
+  }
   if (a.bcast && a.LF > 1)
     hipLaunchKernelGGL((cheb_step_kernel<VEC, true, NW>), grid, block, 0, stream, a, (const Seg*)plan.d_segs,
                        plan.tab.n);
@@ -415,19 +477,11 @@ void launch_main(const Plan& plan, const StepArgs& a, hipStream_t stream) {
 
 template <int NW>
 int launch_hot(const Plan& plan, const StepArgs& a, hipStream_t stream) {
-  static int n_cu = 0;
-  static bool attr_set = false;
-  if (!n_cu) {
-    int dev = 0;
-    WG_HIP_TRY(hipGetDevice(&dev));
-    WG_HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+  int dev = 0;
+  WG_HIP_TRY(hipGetDevice(&dev));
+  const int n_cu = n_cus(dev);
   const size_t lds = (size_t)plan.hot * sizeof(float);
-  if (!attr_set) {
-    WG_HIP_TRY(hipFuncSetAttribute((const void*)cheb_step_hot_kernel<NW>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - NW * 64 * 8));
-    attr_set = true;
-  }
+  if (int rc = ensure_dyn_lds((const void*)cheb_step_hot_kernel<NW>, 160 * 1024 - NW * 64 * 8)) return rc;
   const int grid = std::min<int>(plan.tab.total_blocks, n_cu);
   hipLaunchKernelGGL(cheb_step_hot_kernel<NW>, dim3(grid), dim3(NW * 64), lds, stream, a, (const Seg*)plan.d_segs,
                      plan.tab.n, plan.tab.total_blocks, plan.hot);
@@ -468,6 +522,10 @@ int upload_segs(Plan& p) {
 }  // namespace
 
 void Plan::release() {
+  (void)hipFree(wmeta);
+  (void)hipFree(sell);
+  wmeta = nullptr;
+  sell = nullptr;
   (void)hipFree(d_segs);
   d_segs = nullptr;
   (void)hipFree(chunks);
@@ -688,6 +746,107 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start) {
   return WG_OK;
 }
 
+// The padded CSR of the value-free VEC-4 gathers (accumulate_u4): every row's column ids padded
+// to a multiple of 4 with kPadCol, row pointers prp, kPcolTail pad ids after the last row.  Built
+// once per handle (host pass over the operator's CSR).
+bool gather4_applies(const wg_laplacian_s* L, int64_t F) {
+  return L->tune.gather4 && !L->tune.probe && L->tune.hot == 0 && F % 4 == 0 && F * 4 <= 256 &&
+         F <= 64 * 4 && L->n_cols < kPadCol;
+}
+
+int build_pcol(wg_laplacian_s* L) {
+  if (L->pcol) return WG_OK;
+  const int64_t n = L->n_rows;
+  std::vector<int32_t> rp(n + 1);
+  WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+  std::vector<int32_t> col(std::max<int64_t>(rp[n], 1));
+  if (rp[n]) WG_HIP_TRY(hipMemcpy(col.data(), L->col, sizeof(int32_t) * rp[n], hipMemcpyDeviceToHost));
+  std::vector<int32_t> prp(n + 1);
+  prp[0] = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t len = rp[r + 1] - rp[r];
+    const int64_t padded = prp[r] + (len + 3) / 4 * 4;
+    if (padded > INT32_MAX - kPcolTail) return fail(WG_ERR_INVALID, "build_pcol: padded CSR exceeds int32");
+    prp[r + 1] = (int32_t)padded;
+  }
+  std::vector<int32_t> pc((size_t)prp[n] + kPcolTail, kPadCol);
+  for (int64_t r = 0; r < n; ++r)
+    std::copy(col.begin() + rp[r], col.begin() + rp[r + 1], pc.begin() + prp[r]);
+  int32_t *dprp = nullptr, *dpc = nullptr;
+  if (int rc = dmalloc(&dprp, prp.size())) return rc;
+  if (int rc = dmalloc(&dpc, pc.size())) {
+    (void)hipFree(dprp);
+    return rc;
+  }
+  WG_HIP_TRY(hipMemcpy(dprp, prp.data(), sizeof(int32_t) * prp.size(), hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipMemcpy(dpc, pc.data(), sizeof(int32_t) * pc.size(), hipMemcpyHostToDevice));
+  L->prp = dprp;
+  L->pcol = dpc;
+  return WG_OK;
+}
+
+// The SELL order of a plan's value-free team waves (accumulate_sell): for wave w = unit * NW + wave
+// of a team segment, sub-group g (row begin + (unit - blk_begin) NW tpw + wave tpw + g / LN, share
+// ns = g % LN of the row's 4-entry chunks: ns, ns + LN, ...), its k-th chunk at
+// sell[wmeta[w].x + k G + g] with k = 2 t + c; every sub-group padded with kPadCol chunks to the
+// wave's turn count wmeta[w].y (2 chunks per turn), plus 2 turns of pads after the last wave.
+int build_sell(wg_laplacian_s* L, Plan* p, int LF) {
+  if (p->sell) return WG_OK;
+  const int G = 64 / LF;
+  const int NW = p->nw;
+  const int64_t n = L->n_rows;
+  std::vector<int32_t> rp(n + 1);
+  WG_HIP_TRY(hipMemcpy(rp.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+  std::vector<int32_t> col(std::max<int64_t>(rp[n], 1));
+  if (rp[n]) WG_HIP_TRY(hipMemcpy(col.data(), L->col, sizeof(int32_t) * rp[n], hipMemcpyDeviceToHost));
+  std::vector<int2> wm((size_t)p->tab.total_blocks * NW, int2{0, 0});
+  std::vector<int4> sell;
+  const int4 pad4{kPadCol, kPadCol, kPadCol, kPadCol};
+  for (int si = 0; si < p->tab.n; ++si) {
+    const Seg& sg = p->tab.s[si];
+    if (sg.mode != 0) continue;
+    const int LN = sg.ln, tpw = G / LN;
+    const int32_t nblk = (si + 1 < p->tab.n ? p->tab.s[si + 1].blk_begin : p->tab.total_blocks) - sg.blk_begin;
+    for (int32_t u = 0; u < nblk; ++u) {
+      for (int w = 0; w < NW; ++w) {
+        const int64_t r0 = (int64_t)sg.begin + (int64_t)u * NW * tpw + (int64_t)w * tpw;
+        int64_t turns = 0;
+        for (int g = 0; g < G; ++g) {  // the wave's longest sub-group
+          const int64_t r = r0 + g / LN, ns = g % LN;
+          if (g / LN >= tpw || r >= sg.end) continue;
+          const int64_t nch = (rp[r + 1] - rp[r] + 3) / 4;
+          const int64_t mine = ns < nch ? (nch - ns + LN - 1) / LN : 0;
+          turns = std::max<int64_t>(turns, (mine + 1) / 2);
+        }
+        const size_t wi = (size_t)(sg.blk_begin + u) * NW + w;
+        if (sell.size() + (size_t)(2 * G * (turns + 2)) >= ((size_t)1 << 27))  // 16-B chunks at 32-bit byte offsets
+          return fail(WG_ERR_UNSUPPORTED, "build_sell: id array exceeds 2 GB (tuning key sell = 0)");
+        wm[wi] = int2{(int)sell.size(), (int)turns};
+        const size_t base = sell.size();
+        sell.resize(base + (size_t)2 * turns * G, pad4);
+        for (int g = 0; g < G; ++g) {
+          const int64_t r = r0 + g / LN, ns = g % LN;
+          if (g / LN >= tpw || r >= sg.end) continue;
+          const int64_t len = rp[r + 1] - rp[r];
+          const int64_t nch = (len + 3) / 4;
+          for (int64_t k = 0; ns + k * LN < nch; ++k) {
+            const int64_t ch = ns + k * LN;
+            int32_t id[4];
+            for (int i = 0; i < 4; ++i) id[i] = ch * 4 + i < len ? col[rp[r] + ch * 4 + i] : kPadCol;
+            sell[base + (size_t)k * G + g] = int4{id[0], id[1], id[2], id[3]};
+          }
+        }
+      }
+    }
+  }
+  sell.resize(sell.size() + (size_t)4 * G, pad4);  // the next-turn id reads past the last wave
+  if (int rc = dmalloc(&p->wmeta, wm.size())) return rc;
+  if (int rc = dmalloc(&p->sell, sell.size())) return rc;
+  WG_HIP_TRY(hipMemcpy(p->wmeta, wm.data(), sizeof(int2) * wm.size(), hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipMemcpy(p->sell, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice));
+  return WG_OK;
+}
+
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk, float* S,
                 float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only, float* S_out,
                 const ClenArgs* cl) {
@@ -741,7 +900,37 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.rsplit = hyb->tsplit;
         a.part = hyb->part + f0;
       }
+      // value-free steps at VEC 4 on the padded CSR (accumulate_u4): the plain step, all columns
+      // in one tile, gathered rows addressable by 24-bit ids
+      if (vec == 4 && a.uin && !hyb && F == fw && gather4_applies(L, F)) {
+        if (int rc2 = build_pcol(L)) return rc2;
+        a.prp = L->prp;
+        a.pcol = L->pcol;
+        a.u_bytes = (uint32_t)(L->n_cols * F * 4);
+        a.vidx = L->tune.gather4;  // the loop variant (launch_main)
+        if (L->tune.sell && plan->tab.total_blocks > 0) {  // team waves on SELL-ordered ids
+          if (int rc2 = build_sell(L, plan, LF)) return rc2;
+          a.wmeta = plan->wmeta;
+          a.sell = plan->sell;
+        }
+      }
+#ifdef WG_TIMING_PROBES
+      if (L->tune.trace && L->trace_seq++ == L->tune.trace - 1) {
+        const size_t need = (size_t)plan->tab.total_blocks * plan->nw * 4;
+        if (L->trace_n < (int64_t)need) {
+          (void)hipFree(L->trace_buf);
+          L->trace_buf = nullptr;
+          L->trace_n = 0;
+          if (int rc2 = dmalloc(&L->trace_buf, need)) return rc2;
+          L->trace_n = (int64_t)need;
+        }
+        WG_HIP_TRY(hipMemsetAsync(L->trace_buf, 0, sizeof(unsigned long long) * L->trace_n, stream));
+        a.trace = L->trace_buf;
+      }
+#endif
       a.probe = L->tune.probe;
+      a.probe_h2 = L->tune.probe_h2;
+      a.probe_fold = L->tune.probe_fold;
       if (a.probe && !a.xk) a.xk = S ? S + f0 : nullptr;  // the final step of a chain stores into S
       a.chunks = plan->chunks;
       a.partial = plan->partial;

@@ -48,7 +48,26 @@ struct StepArgs {
   const int32_t* rsplit;
   const double* part;
   int32_t probe;  // timing probe (-DWG_TIMING_PROBES builds, knob "probe"): gathers only, acc stored to xk
+  // timing probes of the gather's request count / footprint (-DWG_TIMING_PROBES, results wrong):
+  // probe_h2: columns below it gather one aligned 128-B line (lanes of columns 32.. skip);
+  // probe_fold: every gathered column folded into [0, probe_fold)
+  int32_t probe_h2, probe_fold;
+  // value-free gathers on the padded CSR (cheb_step_kernel<..., P4 = true>): each row's column ids
+  // padded to a multiple of 4 with kPadCol (prp / pcol); the gathered vector xm1 as a raw buffer
+  // of u_bytes bytes, so a pad id's offset falls outside it and its load returns 0 with no request
+  const int32_t* prp;
+  const int32_t* pcol;
+  uint32_t u_bytes;
+  unsigned long long* trace;  // -DWG_TIMING_PROBES, knob "trace": per-wave timeline of one launch
+  const int2* wmeta;  // team waves in SELL order (Plan::sell): per wave {first chunk, turns}
+  const int4* sell;
 };
+
+// a padded-CSR column id whose byte offset (id * row bytes <= 256) lies past every gathered buffer
+constexpr int32_t kPadCol = 0xFFFFFF;
+// kPadCol ids after the last row of pcol: a sub-group's id loads run up to (PF + 1) turns of CPT
+// steps (<= 4096 ids each) past its range
+constexpr int32_t kPcolTail = 65536;
 
 // the entry range of a row (or of a split-row chunk) this launch's phase covers
 __device__ __forceinline__ void phase_range(const StepArgs& a, int64_t row, int32_t& e0, int32_t& e1) {
@@ -390,6 +409,29 @@ __device__ __forceinline__ void accumulate_bcast(const StepArgs& a, int32_t e, i
         v[u] = __shfl(myv, src, 64);
       }
       float x[U][VEC];
+#ifdef WG_TIMING_PROBES
+      // branch-free timing probes: probe_fold = 2^m folds every column into [0, 2^m) (an AND);
+      // probe_h2 > 0: columns below it gather ONE aligned 128-B line (lanes 8, 9 repeat lanes
+      // 0, 1's addresses); probe_h2 < 0: no gathers at all (x = the column id)
+      if (a.probe_fold > 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] &= a.probe_fold - 1;
+      }
+      if (a.probe_h2 < 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) x[u][q] = (float)(c[u] + q);
+      } else if (a.probe_h2 > 0) {
+        const float* base = xb - fs * VEC;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool one = c[u] < a.probe_h2;
+          const int64_t off = one ? (int64_t)c[u] * 32 + (fs & 7) * 4 : (int64_t)c[u] * ld + fs * VEC;
+          if (j + u < cnt) load_vec<VEC>(base + off, x[u]);
+        }
+      } else
+#endif
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (j + u < cnt) load_vec<VEC>(xb + (int64_t)c[u] * ld, x[u]);  // no dummy gathers
@@ -430,6 +472,152 @@ __device__ __forceinline__ void accumulate_vidx1(const StepArgs& a, int32_t e0, 
       const bool ok = (q + u >= e0) && (q + u < e1);
       if (ok) acc[0] = fma((double)vv[u], (double)x[u], acc[0]);
     }
+  }
+}
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// Value-free gathers (unweighted graphs, u = b * dinv), VEC = 4, on the padded CSR: a sub-group
+// walks the 4-entry chunks q, q + step, ... of its range [q, e1) (multiples of 4), CPT chunks per
+// turn.  Each lane loads a chunk's four ids with ONE 16-B load (the sub-group's lanes share the
+// address: no index broadcast), gathers its 16-B slice of each entry's row as a raw buffer load
+// (pad ids return 0 without a memory request), sums the turn's slices in float32 pairs
+// (v_pk_add_f32, a fixed tree) and adds that to the float64 accumulators.  The ids of the next PF
+// turns are in flight while a turn's gathers are consumed: a turn's wait is ONE memory latency
+// under load, and a wave's time is its turns x that latency (DESIGN.md 4.1, r04 timelines).
+template <int CPT, int PF>
+__device__ __forceinline__ void accumulate_u4(const StepArgs& a, int32_t q, int32_t e1, int32_t step, int fs,
+                                              double (&acc)[4]) {
+  if (q >= e1) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0,
+                                                                      (int)a.u_bytes, 0x00020000);
+  const uint32_t rb = (uint32_t)a.ld * 4u;
+  const uint32_t lo = (uint32_t)fs * 16u;
+  const int32_t* __restrict__ pc = a.pcol;
+  const int32_t T = CPT * step;  // entries between a sub-group's turns
+  const int4 pad = make_int4(kPadCol, kPadCol, kPadCol, kPadCol);
+#ifdef WG_TIMING_PROBES
+  const int32_t idmask = a.probe_fold < 0 ? 1023 : -1;  // probe: ids from one 4-KB window
+#else
+  constexpr int32_t idmask = -1;
+#endif
+  // the ids as raw buffer loads with the volatile bit (aux bit 31): the compiler may not sink a
+  // volatile load to its use in the next turn (MachineSink did, serialising id and gather latency)
+  const __amdgpu_buffer_rsrc_t rpc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(pc), 0, 0x7fffffff,
+                                                                       0x00020000);
+  auto ld_ids = [&](int32_t qq, int4 (&id)[CPT]) {  // unconditional: pcol is padded by kPcolTail ids
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rpc, (uint32_t)((qq + c * step) & idmask) * 4u, 0,
+                                                              (int)(1u << 31));
+      id[c] = make_int4((int)v.x, (int)v.y, (int)v.z, (int)v.w);
+    }
+  };
+  int4 ids[PF + 1][CPT];
+#pragma unroll
+  for (int t = 0; t <= PF; ++t) ld_ids(q + t * T, ids[t]);
+  // one turn on id slot S: gathers, the next-but-PF turn's ids into the slot, the sums
+  auto turn = [&](int4 (&id)[CPT]) -> bool {
+    int32_t cc[4 * CPT];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const bool ok = q + c * step < e1;
+      cc[4 * c + 0] = ok ? id[c].x : kPadCol;
+      cc[4 * c + 1] = ok ? id[c].y : kPadCol;
+      cc[4 * c + 2] = ok ? id[c].z : kPadCol;
+      cc[4 * c + 3] = ok ? id[c].w : kPadCol;
+    }
+#ifdef WG_TIMING_PROBES
+    if (a.probe_fold > 0) {
+#pragma unroll
+      for (int u = 0; u < 4 * CPT; ++u) cc[u] = cc[u] == kPadCol ? kPadCol : (cc[u] & (a.probe_fold - 1));
+    }
+#endif
+    u32x4_t x[4 * CPT];
+#ifdef WG_TIMING_PROBES
+    if (a.probe_h2 < 0) {
+#pragma unroll
+      for (int u = 0; u < 4 * CPT; ++u) x[u] = u32x4_t{(uint32_t)cc[u], 0u, 0u, 0u};
+    } else
+#endif
+#pragma unroll
+    for (int u = 0; u < 4 * CPT; ++u)
+      x[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24((uint32_t)cc[u], rb) + lo, 0, 0);
+    ld_ids(q + (PF + 1) * T, id);
+    f32x2 l2[4 * CPT], h2[4 * CPT];
+#pragma unroll
+    for (int u = 0; u < 4 * CPT; ++u) {
+      l2[u] = f32x2{__uint_as_float(x[u].x), __uint_as_float(x[u].y)};
+      h2[u] = f32x2{__uint_as_float(x[u].z), __uint_as_float(x[u].w)};
+    }
+#pragma unroll
+    for (int w = 1; w < 4 * CPT; w *= 2)  // fixed pairwise tree
+#pragma unroll
+      for (int u = 0; u + w < 4 * CPT; u += 2 * w) {
+        l2[u] += l2[u + w];
+        h2[u] += h2[u + w];
+      }
+    acc[0] += (double)l2[0].x;
+    acc[1] += (double)l2[0].y;
+    acc[2] += (double)h2[0].x;
+    acc[3] += (double)h2[0].y;
+    q += T;
+    return q < e1;
+  };
+  for (;;) {
+    if (!turn(ids[0])) break;
+    if (!turn(ids[1])) break;
+    if constexpr (PF >= 2) {
+      if (!turn(ids[2])) break;
+    }
+  }
+}
+
+// A team wave's sub-group g on the SELL-ordered ids (Plan::sell): turn t's two chunks of every
+// sub-group of the wave are contiguous (one coalesced 2 x G x 16-B id read per turn for the wave,
+// instead of G scattered 16-B reads), every sub-group runs the wave's turn count (pads are
+// kPadCol: dropped loads, no masking), the next turn's ids are in flight during this turn's
+// gathers.  Same chunks, same float32 tree and float64 order as accumulate_u4<2, 1> (bitwise equal).
+__device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int G, int g, int fs, double (&acc)[4]) {
+  if (wm.y <= 0) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0,
+                                                                      (int)a.u_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(const_cast<int4*>(a.sell), 0, 0x7fffffff,
+                                                                      0x00020000);
+  const uint32_t rb = (uint32_t)a.ld * 4u;
+  const uint32_t lo = (uint32_t)fs * 16u;
+  uint32_t off = ((uint32_t)wm.x + (uint32_t)g) * 16u;  // byte offset of this sub-group's chunk 0
+  const uint32_t cstep = (uint32_t)G * 16u;                // next chunk of the same sub-group
+  // volatile (aux bit 31): the next turn's ids are not sunk to their use (accumulate_u4)
+  auto ld = [&](uint32_t o) { return __builtin_amdgcn_raw_buffer_load_b128(ri, o, 0, (int)(1u << 31)); };
+  u32x4_t c0 = ld(off), c1 = ld(off + cstep);
+  for (int t = 0;;) {
+    off += 2 * cstep;
+    const u32x4_t n0 = ld(off), n1 = ld(off + cstep);  // the array is padded past its last turn
+    const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    u32x4_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24(cc[u], rb) + lo, 0, 0);
+    f32x2 l2[8], h2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      l2[u] = f32x2{__uint_as_float(x[u].x), __uint_as_float(x[u].y)};
+      h2[u] = f32x2{__uint_as_float(x[u].z), __uint_as_float(x[u].w)};
+    }
+#pragma unroll
+    for (int w = 1; w < 8; w *= 2)
+#pragma unroll
+      for (int u = 0; u + w < 8; u += 2 * w) {
+        l2[u] += l2[u + w];
+        h2[u] += h2[u + w];
+      }
+    acc[0] += (double)l2[0].x;
+    acc[1] += (double)l2[0].y;
+    acc[2] += (double)h2[0].x;
+    acc[3] += (double)h2[0].y;
+    if (++t >= wm.y) break;
+    c0 = n0;
+    c1 = n1;
   }
 }
 

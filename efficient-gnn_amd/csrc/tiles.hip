@@ -496,7 +496,9 @@ int upload(T** d, const std::vector<T>& h) {
 int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   const int64_t n = L->n_rows, nnz = L->nnz;
   const int64_t n_plan = active_only ? L->n_active : n;
-  const int64_t col_limit = active_only ? L->n_active : L->n_cols;  // closed-form rows are never gathered
+  // closed-form rows are never gathered: on a whole graph they end the column space; on a row shard
+  // they sit between the active own rows and the halo (dist.hip keeps their u rows zero)
+  const int64_t col_limit = (active_only && L->n_cols == L->n_rows) ? L->n_active : L->n_cols;
   const int th = std::max(1, L->tune.tile_th);
   int tmax = L->tune.tile_max;  // <= 0: auto (below)
   const int kTR = L->tune.tile_rows == 128 ? 128 : 64;

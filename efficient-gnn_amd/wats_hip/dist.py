@@ -382,8 +382,10 @@ class ShardedWavelet:
         if self._dist is not None:
             t = ctypes.c_int32(0)
             check(_lib.load().wg_dist_status(self._dist, ctypes.byref(t)), "dist_status")
-            if t.value:
+            if t.value & 1:
                 raise RuntimeError("wats_hip: a peer did not complete its phase within 60 s (IPC exchange)")
+            if t.value & 2:
+                raise RuntimeError("wats_hip: an IPC phase signal did not release every XCD's L2 (DESIGN.md 7)")
 
     def set_graph(self, enable: bool) -> None:
         """Replay the native chain as a hipGraph (default) or run it eagerly."""

@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import check, ptr
+from ._lib import WaveletError, check, ptr
 from .laplacian import NormalizedLaplacian, require_gpu, stream_handle
 
 
@@ -277,6 +277,11 @@ def graph_wavelet_features(adj_matrix, k: int = 3, s: float = 0.8, X0=None, retu
     with torch.cuda.device(L.device):
         check(_lib.load().wg_wavelet_features(L.handle, ptr(X), F, int(k), float(s), ptr(S), ptr(H),
                                               stream_handle(L.device)), "wavelet_features")
+    if F == 1 and L.chain_status():
+        # the one-launch chain (csrc/chain.hip) gave up a wait: its rows depending on the
+        # missing data are NaN.  The reference returns host arrays, so this sync is its own.
+        raise WaveletError("graph_wavelet_features: the one-launch chain timed out waiting for a worker "
+                           "(results invalid, written as NaN)")
     return (H, S) if return_S else H
 
 

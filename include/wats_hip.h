@@ -36,7 +36,8 @@ enum wg_status {
   WG_ERR_INVALID = -1,   /* bad argument (shape, null pointer, range) */
   WG_ERR_HIP = -2,       /* a HIP runtime call failed */
   WG_ERR_OOM = -3,       /* device allocation failed */
-  WG_ERR_UNSUPPORTED = -4
+  WG_ERR_UNSUPPORTED = -4,
+  WG_ERR_TIMEOUT = -5    /* an in-kernel wait gave up (the one-launch chain): that launch's outputs are NaN */
 };
 
 /* creation flags */
@@ -230,10 +231,14 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
 /* F == 1 on a small unweighted graph (<= 2^18 nonzeros, <= 24576 active rows;
  * tuning key "chain": -1 auto, 0 off, 1 on, "chain_wg" workers) with S and H
  * given, wg_wavelet_features runs the whole chain in ONE launch of P
- * cooperating workgroups separated by a device-counter barrier per step
- * (csrc/chain.hip).  A barrier wait gives up after ~0.5 s
- * instead of hanging; wg_chain_status (synchronous) reports that in
- * *timed_out_host (1 = a chain's results are invalid). */
+ * cooperating workgroups that hand each step's vector over as tagged granules
+ * (csrc/chain.hip).  A wait gives up after 0.5 s instead of
+ * hanging; that launch then writes NaN for every S / H row that depends on the
+ * missing data and records the failure in host-mapped memory, and the NEXT
+ * wg_wavelet_features call on the handle returns WG_ERR_TIMEOUT without
+ * launching.  wg_chain_status (synchronous) reports a failure since the last
+ * report in *timed_out_host (1 = a chain's results are invalid; tuning key
+ * "chain_fault" = j injects one: worker 0 skips publishing phase j). */
 int wg_chain_status(wg_laplacian_t L, int32_t* timed_out_host);
 
 /* Tuning: key "iter" (team-mode nonzeros per lane sub-group; default by

@@ -168,6 +168,10 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiles=
             sw.check_exchange()
             sw.close()
         q.put((rank, S.cpu().numpy(), H.cpu().numpy(), q_path, same))
+    except Exception as exc:  # noqa: BLE001 -- reported to the parent at once, not by its queue timeout
+        import traceback
+        q.put((rank, None, None, f"{exc!r}\n{traceback.format_exc()}", False))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -197,10 +201,19 @@ def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiles):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    res = []
+    try:
+        for _ in range(world):
+            res.append(q.get(timeout=150))
+            if res[-1][1] is None:
+                pytest.fail(f"rank {res[-1][0]}: {res[-1][3]}")
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(res) == world and res[-1][1] is not None else 5)
+            if p.is_alive():
+                p.kill()
+    res.sort(key=lambda t: t[0])
+    assert all(p.exitcode == 0 for p in procs)
     g = _graph(kind)
     rng = np.random.default_rng(0)
     X = rng.standard_normal((g.n, F)).astype(np.float32)

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 import wats_hip  # noqa: E402
 from wats_hip import NormalizedLaplacian  # noqa: E402
-from wats_hip.graphgen import named_graph, random_graph, rmat_graph  # noqa: E402
+from wats_hip.graphgen import connect_isolated, named_graph, random_graph, rmat_graph  # noqa: E402
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -208,6 +208,32 @@ def test_arxiv_config_vs_oracle():
     H, S = wats_hip.graph_wavelet_features(A, k=16, X0=torch.from_numpy(X), return_S=True)
     assert_parity(_np(S), ref["S"], what="arxiv S")
     assert_parity(_np(H), ref["H"], what="arxiv H")
+
+
+@pytest.mark.parametrize("F", [4, 8, 40, 64])
+def test_padded_csr_gathers(F):
+    """The value-free VEC-4 step on the padded CSR (rows padded to 4-entry chunks of
+    dropped pad ids; team waves reading their ids in SELL order, step.hip
+    build_sell) against the oracle, on the arxiv-size graph (every plan segment:
+    split, block and team rows) and the same graph with no closed-form rows; SELL
+    and the per-row padded-CSR loop are bitwise equal (same chunks, same sums),
+    the old gather loop (gather4 = 0) equal to rounding."""
+    g = named_graph("ogbn-arxiv")
+    for gg in (g, connect_isolated(g, seed=7)):
+        A = gg.to_scipy()
+        X = np.random.default_rng(F).standard_normal((gg.n, F)).astype(np.float32)
+        ref = O.graph_wavelet_features(A, k=16, s=0.8, X0=X, return_all=True)
+        L = NormalizedLaplacian.from_graph(gg)
+        out = {}
+        for knobs in ({}, {"sell": 0}, {"gather4": 41, "sell": 0}, {"gather4": 0}):
+            L.tune(**knobs)
+            H, S = wats_hip.graph_wavelet_features(L, k=16, X0=torch.from_numpy(X), return_S=True)
+            out[str(knobs)] = (_np(S), _np(H))
+            assert_parity(out[str(knobs)][0], ref["S"], what=f"padded CSR F={F} {knobs} S")
+            assert_parity(out[str(knobs)][1], ref["H"], what=f"padded CSR F={F} {knobs} H")
+            L.tune(gather4=1, sell=1)
+        assert np.array_equal(out["{}"][0], out["{'sell': 0}"][0])
+        L.close()
 
 
 def test_hub_rows_long_row_path():
@@ -733,6 +759,41 @@ def test_chain1_vs_oracle(n, nnz, K, knobs):
     L.tune(chain=0)   # the multi-launch path gives the same result to rounding
     _, S0 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=Xt, return_S=True)
     assert_parity(S1.cpu().numpy(), S0.cpu().numpy().astype(np.float64), what="chain1 vs multi-launch")
+    L.close()
+
+
+def test_chain1_timeout_is_an_error():
+    """A worker that never publishes (fault injection: tuning key chain_fault)
+    makes the one-launch chain give up its waits: the launch's dependent S / H
+    rows come out NaN (never silently wrong), graph_wavelet_features raises,
+    the C API's next call returns WG_ERR_TIMEOUT without launching, and a clean
+    launch afterwards is exact again."""
+    g = rmat_graph(19717, 88648, seed=3)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(chain_wg=16)
+    H0, S0 = wats_hip.graph_wavelet_features(L, k=16, s=0.8, return_S=True)
+    torch.cuda.synchronize()
+    assert "chain1:" in L.describe(1) and torch.isfinite(S0).all()
+    L.tune(chain_fault=3)
+    with pytest.raises(wats_hip.WaveletError, match="timed out"):
+        wats_hip.graph_wavelet_features(L, k=16, s=0.8)
+    # the C ABI alone: the failed launch returns WG_OK (asynchronous), writes NaN, and the next
+    # call reports WG_ERR_TIMEOUT (-5) without launching
+    lib = wats_hip._lib.load()
+    X = L.log1p_degree()
+    S = torch.zeros(L.n, 1, device=X.device)
+    H = torch.zeros(L.n, 1, device=X.device)
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.wg_wavelet_features(L.handle, X.data_ptr(), 1, 16, 0.8, S.data_ptr(), H.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.isnan(S).any() and torch.isnan(H).any()
+    assert lib.wg_wavelet_features(L.handle, X.data_ptr(), 1, 16, 0.8, S.data_ptr(), H.data_ptr(), st) == -5
+    assert "gave up" in lib.wg_last_error().decode()
+    L.tune(chain_fault=0)
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=16, s=0.8, return_S=True)
+    torch.cuda.synchronize()
+    assert not L.chain_status()
+    assert torch.equal(S1, S0) and torch.equal(H1, H0)
     L.close()
 
 
