@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--traffic-json", default="auto",
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py); "
                          "'auto': the committed PMC summary of the default workload (profiles/r03/s35_traffic.json, "
-                         "tools/traffic_pass.sh) when the workload is the default one; 'none' to omit")
+                         "tools/session.sh pmc) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--sharded-extra", default="reddit-f41,reddit,rmat-8m,ogbn-arxiv",
                     help="comma-separated configs also measured row-sharded over all ranks (halo exchange), attached "
@@ -86,7 +86,7 @@ def parse():
                     help="N > 1: seconds the row-sharded headline may take before an error line is printed")
     ap.add_argument("--sharded-timeout", type=float, default=420.0,
                     help="seconds the extras may take before the line is printed without the unfinished ones")
-    ap.add_argument("--exchange", default="rccl,ipc",
+    ap.add_argument("--exchange", default="ipc,rccl",
                     help="comma-separated sharded halo exchanges: native chain with grouped ncclSend/ncclRecv "
                          "(rccl) or the one-sided IPC pull (ipc), or torch all_to_all_single per step (nccl); the "
                          "first is the headline's (N > 1) and the extras'; the others are timed for the first "
@@ -136,11 +136,11 @@ def _byte_model(info) -> str:
     return "lds (16-bit ids, no values; DESIGN.md 4.4)"
 
 
-def lds_kernel_name(info, chain1: bool = False) -> str:
+def lds_kernel_name(info, chain1: bool = False, team: bool = False) -> str:
     if chain1:
         return "cheb_chain1_kernel (the whole chain in one launch; per-step time = launch / K)"
     if not info:
-        return "cheb_step_kernel"
+        return "cheb_team4_kernel" if team else "cheb_step_kernel"
     return {1: "cheb_lds1_kernel", 2: "cheb_lds3_kernel + combine_lds2_kernel",
             4: "cheb_hub1_kernel"}.get(info["mode"], "lds mode %d" % info["mode"])
 
@@ -708,7 +708,7 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
             "traffic_source": (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction: "
                                f"an upper bound) + WRITE_SIZE per launch of this kernel on this workload"
                                if traffic is not None else None),
-            "kernel": lds_kernel_name(lds_info, one_launch_chain),
+            "kernel": lds_kernel_name(lds_info, one_launch_chain, "team:" in L.describe(F)),
             "byte_model": _byte_model(lds_info) if lds_info else
                           "SURVEY 8(d): 8 B/nnz + 4(N+1) + 20 N F over the launched rows",
             "algorithmic_bytes_per_launch": b_roof,

@@ -197,7 +197,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "chain must be -1 (auto), 0 or 1");
     L->tune.chain = (int32_t)value;
   } else if (!strcmp(key, "chain_wg")) {
-    if (value < 0 || value > 64) return fail(WG_ERR_INVALID, "chain_wg must be in [0 (auto), 64]");
+    if (value < 0 || value > 256) return fail(WG_ERR_INVALID, "chain_wg must be in [0 (auto), 256]");
     L->tune.chain_wg = (int32_t)value;
   } else if (!strcmp(key, "chain_fault")) {
     if (value < 0 || value > kChainMaxK) return fail(WG_ERR_INVALID, "chain_fault must be in [0, %d]", kChainMaxK);
@@ -207,10 +207,23 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.chain_xcd = value ? 1 : 0;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "gather4")) {
-    if (value != 0 && value != 1 && value != 21 && value != 22 && value != 31 && value != 41)
-      return fail(WG_ERR_INVALID, "gather4 must be 0 (off), 1 (default loop), 21, 22, 31 or 41");
+    if (value != 0 && value != 1 && value != 21 && value != 22 && value != 31 && value != 41 && value != 121)
+      return fail(WG_ERR_INVALID, "gather4 must be 0 (off), 1 (default loop), 21, 22, 31, 41 or 121");
     L->tune.gather4 = (int32_t)(value == 1 ? 21 : value);
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "team")) {
+    if (value < 0 || value > 10 || (value > 1 && value < 7))
+      return fail(WG_ERR_INVALID, "team must be 0 (off), 1 (default), 7, 8, 9 or 10");
+    L->tune.team = (int32_t)value;
+    return WG_OK;  // launch-time choice (the wave table is built with the plan on first use)
+  } else if (!strcmp(key, "team_pairs")) {
+    L->tune.team_pairs = value ? 1 : 0;
+  } else if (!strcmp(key, "team_grid")) {
+    if (value < 0 || value > 64) return fail(WG_ERR_INVALID, "team_grid must be in [0, 64]");
+    L->tune.team_grid = (int32_t)value;
+  } else if (!strcmp(key, "team_iter")) {
+    if (value < 8 || value > 4096) return fail(WG_ERR_INVALID, "team_iter must be in [8, 4096]");
+    L->tune.team_iter = (int32_t)value;
   } else if (!strcmp(key, "sell")) {
     L->tune.sell = value ? 1 : 0;
     return WG_OK;  // launch-time choice (the SELL arrays are built with the plan on first use)
@@ -280,6 +293,11 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
   snprintf(buf, sizeof(buf), "F=%lld VEC=%d LF=%d segments=%d blocks=%d active_rows=%lld closed_form_rows=%lld\n",
            (long long)F, vec, LF, p->tab.n, p->tab.total_blocks, (long long)L->n_active, (long long)L->n_closed);
   g_text = buf + p->text;
+  if (p->team.wd) {  // the independent-wave step kernel's table, once a step has built it (team.hip)
+    snprintf(buf, sizeof(buf), "team: waves=%d long_rows=%d part_slots=%d\n", p->team.n_waves, p->team.n_long,
+             p->team.n_slots);
+    g_text += buf;
+  }
   for (int i = 1; i >= 0; --i)  // the hybrid step's plan, once a chain has built it
     if (L->tiles[i]) g_text += L->tiles[i]->text;
   if (F == 1) {

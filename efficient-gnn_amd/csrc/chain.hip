@@ -52,7 +52,9 @@ struct ChainArgs {
   int32_t P;
   int32_t stride;             // workgroup b is worker b / stride when b % stride == 0 (XCD placement)
   int32_t ustride;            // floats per exchange buffer
-  const uint16_t* ids;        // [nnz_act] column ids (row order)
+  const uint16_t* ids;        // [nnz_act] column ids (row order): the worker's local column ids (P > 1)
+  const uint16_t* wcols;      // P > 1: each worker's gathered columns (ascending), concatenated
+  const int32_t* wcol_off;    // [P + 1] their offsets
   const int4* wdesc;          // [P] {row0, row1, e0, e1}
   const int32_t* wpass;       // [P][kChainWaves + 1] pass offsets of each worker's waves (into passes)
   const int2* passes;         // one wave pass: {first row, rows | log2 team size << 8}
@@ -72,21 +74,25 @@ struct ChainArgs {
   double c[kChainMaxK + 1];   // heat coefficients exp(-s k)
 };
 
-// LDS layout of one worker (byte offsets, 16-B aligned sections): u [, u2], dinv (double), X0,
-// previous u, row pointers, 16-bit ids, wave passes
+// LDS layout of one worker (byte offsets, 16-B aligned sections): u [, u2] (one worker: every
+// active row, twice; else the nu columns the worker gathers), dinv (double) and its reciprocal, X0,
+// previous u, current u of the own rows, row pointers, 16-bit ids, wave passes, the gathered
+// columns' global ids
 struct ChainLayout {
-  int64_t u2, dv, x0o, pu, lrp, id, pas, bytes;
-  __host__ __device__ ChainLayout(int64_t n_act, int64_t nr, int64_t ne, int64_t npass, bool single) {
+  int64_t u2, dv, x0o, pu, cu, lrp, id, pas, wc, bytes;
+  __host__ __device__ ChainLayout(int64_t nu, int64_t nr, int64_t ne, int64_t npass, bool single) {
     auto al = [](int64_t x) { return (x + 15) & ~(int64_t)15; };
-    const int64_t ub = al(4 * n_act);
+    const int64_t ub = al(4 * nu);
     u2 = ub;
     dv = single ? 2 * ub : ub;
     x0o = al(dv + 16 * nr);  // dinv and its reciprocal
     pu = al(x0o + 4 * nr);
-    lrp = al(pu + 4 * nr);
+    cu = al(pu + 4 * nr);
+    lrp = al(cu + 4 * nr);
     id = al(lrp + 4 * (nr + 1));
     pas = al(id + 2 * ne);
-    bytes = al(pas + 8 * npass);
+    wc = al(pas + 8 * npass);
+    bytes = al(wc + (single ? 0 : 2 * nu));
   }
 };
 
@@ -102,17 +108,21 @@ constexpr int kStageMax = 24;
 #ifndef WG_CHAIN_SLEEP  // s_sleep units (64 cycles) between polls of granules not yet published
 #define WG_CHAIN_SLEEP 1
 #endif
-__device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, int n, uint32_t tag, int tid,
-                                             int64_t wait_ticks) {
+__device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, const uint16_t* cols, int n, uint32_t tag,
+                                             int tid, int64_t wait_ticks) {
   uint32_t pending = 0;
+  int src[kStageMax];  // the granule of local column tid + q * threads
 #pragma unroll
-  for (int q = 0; q < kStageMax; ++q)
-    if (tid + q * kChainThreads < n) pending |= 1u << q;
+  for (int q = 0; q < kStageMax; ++q) {
+    const int i = tid + q * kChainThreads;
+    src[q] = i < n ? (int)cols[i] : 0;
+    if (i < n) pending |= 1u << q;
+  }
   const uint64_t t0 = wall_clock64();
   while (pending) {
     uint64_t v[kStageMax];
 #pragma unroll
-    for (int q = 0; q < kStageMax; ++q) v[q] = (pending >> q) & 1 ? ld_sc1_u64(g + tid + q * kChainThreads) : 0ull;
+    for (int q = 0; q < kStageMax; ++q) v[q] = (pending >> q) & 1 ? ld_sc1_u64(g + src[q]) : 0ull;
 #pragma unroll
     for (int q = 0; q < kStageMax; ++q) {
       if (((pending >> q) & 1) && (uint32_t)(v[q] >> 32) == tag) {
@@ -158,16 +168,20 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
   const int row0 = d.x, nr = d.y - d.x, e0 = d.z, ne = d.w - d.z;
   const int32_t* wp = a.wpass + w * (kChainWaves + 1);
   const int pass0 = wp[0], npass = wp[kChainWaves] - pass0;
-  const ChainLayout lay(a.n_act, nr, ne, npass, a.P == 1);
-  float* u = reinterpret_cast<float*>(smem);                         // [n_act] the gathered u
+  const int wc0 = a.P == 1 ? 0 : a.wcol_off[w];
+  const int nu = a.P == 1 ? a.n_act : a.wcol_off[w + 1] - wc0;       // columns this worker gathers
+  const ChainLayout lay(nu, nr, ne, npass, a.P == 1);
+  float* u = reinterpret_cast<float*>(smem);                         // [nu] the gathered u (local ids)
   float* u2 = reinterpret_cast<float*>(smem + lay.u2);               // [n_act] one worker: the next u
   double* dv = reinterpret_cast<double*>(smem + lay.dv);             // [nr] dinv, negative = isolated row
   double* rdv = dv + nr;                                             // [nr] 1 / dinv
   float* x0o = reinterpret_cast<float*>(smem + lay.x0o);             // [nr]
   float* pu = reinterpret_cast<float*>(smem + lay.pu);               // [nr] previous u of own rows
+  float* cu = reinterpret_cast<float*>(smem + lay.cu);               // [nr] current u of own rows
   int32_t* lrp = reinterpret_cast<int32_t*>(smem + lay.lrp);         // [nr + 1]
   uint16_t* id = reinterpret_cast<uint16_t*>(smem + lay.id);         // [ne]
   int2* pas = reinterpret_cast<int2*>(smem + lay.pas);               // [npass] the worker's wave passes
+  uint16_t* wc = reinterpret_cast<uint16_t*>(smem + lay.wc);         // [nu] P > 1: global id of local column
   const uint32_t ep = (uint32_t)a.bar[3] & 0x3ffffffu;             // this launch's epoch (tags ep * 64 + j)
   // A granule wait that gave up leaves stale u in this worker's LDS: from then on the worker
   // publishes NaN for its rows and writes NaN S / H, so every result that depends on the
@@ -181,12 +195,21 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
     dv[i] = a.iso[row0 + i] ? -di : di;
     rdv[i] = 1.0 / di;
     x0o[i] = a.x0[row0 + i];
+    cu[i] = a.u0[row0 + i];
     lrp[i] = a.rowptr[row0 + i] - e0;
   }
   if (tid == 0) lrp[nr] = ne;
   for (int i = tid; i < ne; i += kChainThreads) id[i] = a.ids[e0 + i];
   for (int i = tid; i < npass; i += kChainThreads) pas[i] = a.passes[pass0 + i];
-  for (int i = tid; i < a.n_act; i += kChainThreads) u[i] = a.u0[i];
+  if (a.P == 1) {
+    for (int i = tid; i < a.n_act; i += kChainThreads) u[i] = a.u0[i];
+  } else {
+    for (int i = tid; i < nu; i += kChainThreads) {
+      const int c = a.wcols[wc0 + i];
+      wc[i] = (uint16_t)c;
+      u[i] = a.u0[c];
+    }
+  }
   __syncthreads();
 #ifdef WG_CHAIN_TRACE  // timing build: worker 0 prints its phase timeline (s_memtime cycles)
   long long tr[2 * kChainMaxK + 4];
@@ -234,13 +257,14 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
           const double dsi = dv[li];
           const double di = fabs(dsi);
           const double rdi = rdv[li];  // 1 / dinv
-          const float ui = u[row];
+          const float ui = cu[li];     // this row's u of the previous phase (b_{k+1} * dinv)
           double lb = -di * s;
           if (dsi < 0.0) lb -= (double)ui * rdi;  // isolated row: L_hat_ii = -1 (ui / di = b_i)
           const double t = ck * (double)x0o[li] + cacc * lb - (prevs ? (double)pu[li] * rdi : 0.0);
           if (k > 0) {
             pu[li] = ui;  // b_{k+1} (as u): the next phase's b_{k+2}
             const float un = bad ? __int_as_float(0x7fc00000) : (float)(t * di);
+            cu[li] = un;
             if (a.P == 1) u2[row] = un;
             else if (!(j == a.fault_phase && w == 0))
               __hip_atomic_store(gnext + row, tag | __float_as_uint(un), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -263,7 +287,7 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
       float* t = u;
       u = u2;
       u2 = t;
-    } else if (!stage_tagged(u, gnext, a.n_act, (uint32_t)(tag >> 32), tid, a.wait_ticks)) {
+    } else if (!stage_tagged(u, gnext, wc, nu, (uint32_t)(tag >> 32), tid, a.wait_ticks)) {
       if (atomicExch(&s_bad, 1) == 0) {  // one lane per worker records the failed launch
         __hip_atomic_store(a.bar + 2, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.host_flag) __hip_atomic_store(a.host_flag, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -338,12 +362,18 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   std::vector<int4> wd;
   std::vector<int2> passes;
   std::vector<int32_t> wpass;
+  std::vector<uint16_t> wcols, lids;  // P > 1: each worker's gathered columns; the entries' local ids
+  std::vector<int32_t> wcol_off;
+  std::vector<int32_t> local(na, -1);
   size_t lds = 0;
   for (;; P = (P == 1 && L->tune.chain_wg <= 0) ? 64 : 2 * P) {
-    if (P > 64) return WG_ERR_UNSUPPORTED;
+    if (P > 256) return WG_ERR_UNSUPPORTED;
     wd.assign(P, int4{0, 0, 0, 0});
     passes.clear();
     wpass.assign((size_t)P * (kChainWaves + 1), 0);
+    wcols.clear();
+    wcol_off.assign(P + 1, 0);
+    lids.assign(ids.begin(), ids.end());
     lds = 0;
     int64_t r = 0;
     bool fits = true;
@@ -370,7 +400,20 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
         passes.insert(passes.end(), per[v].begin(), per[v].end());
       }
       wpass[(size_t)w * (kChainWaves + 1) + kChainWaves] = (int32_t)passes.size();
-      const ChainLayout lay(na, r - r0, rp[r] - rp[r0], (int64_t)wps.size(), P == 1);
+      int64_t nu = na;
+      if (P > 1) {  // the columns this worker's rows gather, ascending, and their local ids
+        std::vector<int32_t> cs(ids.begin() + rp[r0], ids.begin() + rp[r]);
+        std::sort(cs.begin(), cs.end());
+        cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+        for (size_t i = 0; i < cs.size(); ++i) {
+          local[cs[i]] = (int32_t)i;
+          wcols.push_back((uint16_t)cs[i]);
+        }
+        for (int64_t e = rp[r0]; e < rp[r]; ++e) lids[e] = (uint16_t)local[ids[e]];
+        wcol_off[w + 1] = (int32_t)wcols.size();
+        nu = (int64_t)cs.size();
+      }
+      const ChainLayout lay(nu, r - r0, rp[r] - rp[r0], (int64_t)wps.size(), P == 1);
       lds = std::max(lds, (size_t)lay.bytes);
       if (lay.bytes > kChainLds) fits = false;
     }
@@ -380,7 +423,10 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   p->n_act = (int32_t)na;
   p->lds_bytes = (int32_t)((lds + 15) / 16 * 16);
   p->ustride = (int32_t)((na + 63) / 64 * 64);
-  int rc = upload(&p->ids, ids);
+  if (wcols.empty()) wcols.push_back(0);
+  int rc = upload(&p->ids, P == 1 ? ids : lids);
+  if (!rc) rc = upload(&p->wcols, wcols);
+  if (!rc) rc = upload(&p->wcol_off, wcol_off);
   if (!rc) rc = upload(&p->wdesc, wd);
   if (!rc) rc = upload(&p->wpass, wpass);
   if (!rc) rc = upload(&p->passes, passes);
@@ -406,8 +452,8 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
 }  // namespace
 
 void ChainPlan::release() {
-  for (void* q : {(void*)ids, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar, (void*)gbuf, (void*)u0,
-                  (void*)x0})
+  for (void* q : {(void*)ids, (void*)wcols, (void*)wcol_off, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar,
+                  (void*)gbuf, (void*)u0, (void*)x0})
     (void)hipFree(q);
   if (host_flag) (void)hipHostFree(host_flag);
   *this = ChainPlan{};
@@ -472,6 +518,8 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.stride = L->tune.chain_xcd ? 8 : 1;
   a.ustride = p->ustride;
   a.ids = p->ids;
+  a.wcols = p->wcols;
+  a.wcol_off = p->wcol_off;
   a.wdesc = p->wdesc;
   a.wpass = p->wpass;
   a.passes = p->passes;

@@ -69,6 +69,17 @@ struct ChunkDesc {  // one workgroup's share of a split row
   int32_t pad;
 };
 
+// the wave table of the value-free VEC-4 step as independent waves (team.hip)
+struct TeamPlan {
+  int4* wd = nullptr;        // device [2 * n_waves]: per wave {SELL offset, turns, row, LN | rows << 8 | part << 16},
+                             // {part, parts, first slot, arrival counter}
+  int4* sell = nullptr;      // device: the waves' column ids in SELL order (accumulate_sell)
+  double* wpart = nullptr;   // device [n_slots][width]: long rows' float64 partials
+  int32_t* warr = nullptr;   // device [n_long]: monotonic arrival counters
+  int32_t n_waves = 0, n_slots = 0, n_long = 0, width = 0;
+  void release();
+};
+
 struct Plan {
   SegTable tab{};
   int64_t row0 = 0, row1 = 0;   // the rows planned
@@ -87,6 +98,7 @@ struct Plan {
   // kPadCol to the wave's longest sub-group, wmeta[w] = {first chunk, turns} per wave w
   int2* wmeta = nullptr;        // device [total_blocks * nw]
   int4* sell = nullptr;         // device
+  TeamPlan team;                // the same rows as independent waves (team.hip), lazily
   std::string text;
   void release();
 };
@@ -219,6 +231,11 @@ struct Tuning {
   int32_t gather4 = 21;      // value-free VEC-4 steps on the padded CSR (step.hip build_pcol / accumulate_u4):
                              // 0 = off, else 10 x chunks per turn + turns of ids in flight (21, 22, 31, 41)
   int32_t sell = 1;          // padded-CSR steps: team waves read their ids in SELL order (step.hip build_sell)
+  int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 / 8 / 9 / 10:
+                             // register-budget variants (team.hip launch_team4)
+  int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
+  int32_t team_pairs = 1;    // team.hip: rows of <= 4 entries two to a sub-group (pair waves)
+  int32_t team_grid = 0;     // team.hip: 0 = a wave per table entry; n = n workgroups per CU walking the table
   int32_t graph = 0;         // wg_wavelet_features: replay the chain as a hipGraph from its 3rd call with the same
                              // arguments (1 = on; -1 = small chains only, active nnz x width <= 2^22).  Off: the
                              // replay measured SLOWER than eager launches on this stack, +2.7 us per kernel node
@@ -231,7 +248,9 @@ struct Tuning {
 constexpr int kChainMaxK = 64;
 struct ChainPlan {
   int32_t P = 0, n_act = 0, lds_bytes = 0, ustride = 0;
-  uint16_t* ids = nullptr;    // device [nnz_active]: 16-bit column ids in row order
+  uint16_t* ids = nullptr;    // device [nnz_active]: 16-bit column ids in row order (P > 1: worker-local)
+  uint16_t* wcols = nullptr;  // device: each worker's gathered columns, concatenated (P > 1)
+  int32_t* wcol_off = nullptr;  // device [P + 1]
   int4* wdesc = nullptr;      // device [P]: {row0, row1, e0, e1}
   int32_t* wpass = nullptr;   // device [P][17]: each worker's waves' ranges of passes
   int2* passes = nullptr;     // device: one wave pass {first row, rows | log2 team size << 8}
@@ -360,6 +379,12 @@ int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, flo
 int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);
 int build_pcol(wg_laplacian_s* L);
+// team.hip: the wave table of rows [0, n) for LF-lane sub-groups, and its launch
+// (dcol: the operator's column ids, or the hybrid step's tail-first copy, drsplit its rows' tail ends)
+int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, bool pairs, const int32_t* dcol,
+                     const int32_t* drsplit, TeamPlan* tp);
+struct StepArgs;
+int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, int grid_per_cu, hipStream_t stream);
 // the value-free VEC-4 gathers on the padded CSR apply to an F-wide (internal width) signal
 bool gather4_applies(const wg_laplacian_s* L, int64_t F);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);

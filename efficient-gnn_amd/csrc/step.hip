@@ -79,7 +79,8 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     EpiIn<VEC> in;
 #ifdef WG_TIMING_PROBES
     if (a.probe_h2 == -3) {  // skeleton probe: no row work at all, one store per row
-      if (active && ns == 0) store_vec<VEC>(a.xk + row * a.ld + fs * VEC, acc);
+      float* dst = a.xk ? a.xk : a.S;  // the final step stores S (xk is null there)
+      if (active && ns == 0 && dst) store_vec<VEC>(dst + row * a.ld + fs * VEC, acc);
       return;
     }
 #endif
@@ -211,6 +212,12 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
       step_epilogue<VEC>(a, row, t, sum, in2, 0);
     }
   }
+}
+
+// the padded-CSR step held to 8 waves per SIMD (64 VGPRs; timing variant, gather4 = 121)
+template <int NW, int P4>
+__global__ __launch_bounds__(NW * 64, 8) void cheb_step_occ_kernel(StepArgs a, const Seg* __restrict__ segs, int nseg) {
+  unit_body<4, false, NW, false, P4>(a, segs, nseg, (int32_t)blockIdx.x, 0);
 }
 
 template <int VEC, bool BCAST, int NW, int P4 = 0>
@@ -459,6 +466,7 @@ void launch_main(const Plan& plan, const StepArgs& a, hipStream_t stream) {
     if (a.pcol) {  // a.vidx carries the padded-CSR loop variant (gather4 tuning value)
       const Seg* sg = plan.d_segs;
       switch (a.vidx) {
+        case 121: hipLaunchKernelGGL((cheb_step_occ_kernel<NW, 21>), grid, block, 0, stream, a, sg, plan.tab.n); break;
         case 31: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 31>), grid, block, 0, stream, a, sg, plan.tab.n); break;
         case 22: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 22>), grid, block, 0, stream, a, sg, plan.tab.n); break;
         case 41: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 41>), grid, block, 0, stream, a, sg, plan.tab.n); break;
@@ -522,6 +530,7 @@ int upload_segs(Plan& p) {
 }  // namespace
 
 void Plan::release() {
+  team.release();
   (void)hipFree(wmeta);
   (void)hipFree(sell);
   wmeta = nullptr;
@@ -821,7 +830,7 @@ int build_sell(wg_laplacian_s* L, Plan* p, int LF) {
         const size_t wi = (size_t)(sg.blk_begin + u) * NW + w;
         if (sell.size() + (size_t)(2 * G * (turns + 2)) >= ((size_t)1 << 27))  // 16-B chunks at 32-bit byte offsets
           return fail(WG_ERR_UNSUPPORTED, "build_sell: id array exceeds 2 GB (tuning key sell = 0)");
-        wm[wi] = int2{(int)sell.size(), (int)turns};
+        wm[wi] = int2{(int)sell.size(), (int)(2 * turns)};  // chunk count (accumulate_sell)
         const size_t base = sell.size();
         sell.resize(base + (size_t)2 * turns * G, pad4);
         for (int g = 0; g < G; ++g) {
@@ -900,9 +909,23 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.rsplit = hyb->tsplit;
         a.part = hyb->part + f0;
       }
-      // value-free steps at VEC 4 on the padded CSR (accumulate_u4): the plain step, all columns
-      // in one tile, gathered rows addressable by 24-bit ids
-      if (vec == 4 && a.uin && !hyb && F == fw && gather4_applies(L, F)) {
+      // value-free steps at VEC 4: every row as independent waves on SELL-ordered
+      // padded ids (team.hip; the hybrid step's tail too), or the workgroup kernel on the padded CSR
+      // (accumulate_u4 / accumulate_sell); all columns in one tile, rows addressable by 24-bit ids
+      const bool g4 = vec == 4 && a.uin && F == fw && gather4_applies(L, F);
+      if (g4 && L->tune.team) {
+        if (!plan->team.wd)
+          if (int rc2 = build_team_waves(L, plan->row1, LF, L->tune.team_iter, L->tune.team_pairs != 0,
+                                         hyb ? hyb->tcol : L->col, hyb ? hyb->tsplit : nullptr, &plan->team))
+            return rc2;
+        a.u_bytes = (uint32_t)(L->n_cols * F * 4);
+        a.probe = L->tune.probe;
+        a.probe_h2 = L->tune.probe_h2;
+        a.probe_fold = L->tune.probe_fold;
+        if (int rc2 = launch_team4(plan->team, a, L->tune.team, L->tune.team_grid, stream)) return rc2;
+        continue;
+      }
+      if (g4 && !hyb) {
         if (int rc2 = build_pcol(L)) return rc2;
         a.prp = L->prp;
         a.pcol = L->pcol;

@@ -495,7 +495,6 @@ __device__ __forceinline__ void accumulate_u4(const StepArgs& a, int32_t q, int3
   const uint32_t lo = (uint32_t)fs * 16u;
   const int32_t* __restrict__ pc = a.pcol;
   const int32_t T = CPT * step;  // entries between a sub-group's turns
-  const int4 pad = make_int4(kPadCol, kPadCol, kPadCol, kPadCol);
 #ifdef WG_TIMING_PROBES
   const int32_t idmask = a.probe_fold < 0 ? 1023 : -1;  // probe: ids from one 4-KB window
 #else
@@ -573,11 +572,36 @@ __device__ __forceinline__ void accumulate_u4(const StepArgs& a, int32_t q, int3
   }
 }
 
-// A team wave's sub-group g on the SELL-ordered ids (Plan::sell): turn t's two chunks of every
-// sub-group of the wave are contiguous (one coalesced 2 x G x 16-B id read per turn for the wave,
-// instead of G scattered 16-B reads), every sub-group runs the wave's turn count (pads are
-// kPadCol: dropped loads, no masking), the next turn's ids are in flight during this turn's
-// gathers.  Same chunks, same float32 tree and float64 order as accumulate_u4<2, 1> (bitwise equal).
+// A wave's sub-group g on SELL-ordered ids (Plan::sell, team.hip): chunk k (4 ids) of every
+// sub-group of the wave at off + k G + g, so a turn's id read is one coalesced G x 16-B block for
+// the wave instead of G scattered 16-B reads; every sub-group runs the wave's chunk count wm.y
+// (shorter ones padded with kPadCol chunks: dropped loads, no masking), two chunks per turn and a
+// single-chunk last turn when the count is odd; the next turn's ids are in flight during this
+// turn's gathers.  float32 tree per turn, float64 accumulation (as accumulate_u4).
+__device__ __forceinline__ void sum_turn(const u32x4_t* x, int n, double (&acc)[4]) {
+  f32x2 l2[8], h2[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (u < n) {
+      l2[u] = f32x2{__uint_as_float(x[u].x), __uint_as_float(x[u].y)};
+      h2[u] = f32x2{__uint_as_float(x[u].z), __uint_as_float(x[u].w)};
+    }
+  }
+#pragma unroll
+  for (int w = 1; w < 8; w *= 2)
+#pragma unroll
+    for (int u = 0; u + w < 8; u += 2 * w) {
+      if (u + w < n) {
+        l2[u] += l2[u + w];
+        h2[u] += h2[u + w];
+      }
+    }
+  acc[0] += (double)l2[0].x;
+  acc[1] += (double)l2[0].y;
+  acc[2] += (double)h2[0].x;
+  acc[3] += (double)h2[0].y;
+}
+
 __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int G, int g, int fs, double (&acc)[4]) {
   if (wm.y <= 0) return;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0,
@@ -590,35 +614,55 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
   const uint32_t cstep = (uint32_t)G * 16u;                // next chunk of the same sub-group
   // volatile (aux bit 31): the next turn's ids are not sunk to their use (accumulate_u4)
   auto ld = [&](uint32_t o) { return __builtin_amdgcn_raw_buffer_load_b128(ri, o, 0, (int)(1u << 31)); };
-  u32x4_t c0 = ld(off), c1 = ld(off + cstep);
-  for (int t = 0;;) {
+  auto gather = [&](uint32_t c) -> u32x4_t {
+#ifdef WG_TIMING_PROBES
+    if (a.probe_fold > 0 && c != (uint32_t)kPadCol) c &= (uint32_t)(a.probe_fold - 1);
+    if (a.probe_h2 == -1) return u32x4_t{c, 0u, 0u, 0u};
+#endif
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24(c, rb) + lo, 0, 0);
+  };
+  const int pairs = wm.y >> 1;
+  u32x4_t c0 = ld(off), c1 = ld(off + cstep);  // the array is padded past its last wave
+  for (int t = 0; t < pairs; ++t) {
     off += 2 * cstep;
-    const u32x4_t n0 = ld(off), n1 = ld(off + cstep);  // the array is padded past its last turn
+    const u32x4_t n0 = ld(off), n1 = ld(off + cstep);
     const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     u32x4_t x[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24(cc[u], rb) + lo, 0, 0);
-    f32x2 l2[8], h2[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      l2[u] = f32x2{__uint_as_float(x[u].x), __uint_as_float(x[u].y)};
-      h2[u] = f32x2{__uint_as_float(x[u].z), __uint_as_float(x[u].w)};
-    }
-#pragma unroll
-    for (int w = 1; w < 8; w *= 2)
-#pragma unroll
-      for (int u = 0; u + w < 8; u += 2 * w) {
-        l2[u] += l2[u + w];
-        h2[u] += h2[u + w];
-      }
-    acc[0] += (double)l2[0].x;
-    acc[1] += (double)l2[0].y;
-    acc[2] += (double)h2[0].x;
-    acc[3] += (double)h2[0].y;
-    if (++t >= wm.y) break;
+    for (int u = 0; u < 8; ++u) x[u] = gather(cc[u]);
+    sum_turn(x, 8, acc);
     c0 = n0;
     c1 = n1;
   }
+  if (wm.y & 1) {  // the last, single chunk
+    const uint32_t cc[4] = {c0.x, c0.y, c0.z, c0.w};
+    u32x4_t x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = gather(cc[u]);
+    sum_turn(x, 4, acc);
+  }
+}
+
+// A pair wave's sub-group g (team.hip): chunk 0 = row A's ids, chunk 1 = row B's (one each, rows of
+// <= 4 entries), one turn of 8 gathers, the two sums kept apart (each the single-chunk sum of
+// accumulate_sell: bitwise the same as a wave of one row per sub-group)
+__device__ __forceinline__ void accumulate_pair(const StepArgs& a, int32_t first, int G, int g, int fs,
+                                                double (&sa)[4], double (&sb)[4]) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0,
+                                                                      (int)a.u_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(const_cast<int4*>(a.sell), 0, 0x7fffffff,
+                                                                      0x00020000);
+  const uint32_t rb = (uint32_t)a.ld * 4u;
+  const uint32_t lo = (uint32_t)fs * 16u;
+  const uint32_t off = ((uint32_t)first + (uint32_t)g) * 16u;
+  const u32x4_t c0 = __builtin_amdgcn_raw_buffer_load_b128(ri, off, 0, 0);
+  const u32x4_t c1 = __builtin_amdgcn_raw_buffer_load_b128(ri, off + (uint32_t)G * 16u, 0, 0);
+  const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  u32x4_t x[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24(cc[u], rb) + lo, 0, 0);
+  sum_turn(x, 4, sa);
+  sum_turn(x + 4, 4, sb);
 }
 
 template <int VEC, bool BCAST, bool HOT>

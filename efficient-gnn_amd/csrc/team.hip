@@ -1,0 +1,299 @@
+// team.hip -- the value-free Chebyshev / Clenshaw step for VEC-4 signals as independent WAVES
+// (reference calibration/WATS.py:32-36 recurrence, :65-68 heat sum by Clenshaw, :71-72
+// normalisation fused into the last step).
+//
+// Why a second kernel.  cheb_step_kernel (step.hip) runs workgroup units of three kinds (team
+// rows, a workgroup per long row, split-row chunks reduced through LDS) in one kernel: its
+// register and scalar-register budget is the union of the three (106 SGPRs, 75 VGPRs: 6
+// workgroups of 4 waves per CU), and a long row holds four waves until the slowest finishes.
+// Here every wave is a unit of its own, described by one entry of a wave table built with the
+// plan (build_team_waves):
+//   * team waves: G / LN rows, LN sub-groups of LF lanes per row (LN | G = 64 / LF), the row's
+//     4-entry chunks dealt to its sub-groups (ns, ns + LN, ...), summed by shuffles;
+//   * part waves: one share of a long row (all G sub-groups on it); the wave writes its float64
+//     partial with write-through (sc1) stores, drains them, and adds to the row's arrival
+//     counter; the wave whose add completes the row sums every part's partial with sc1 loads in
+//     part order and runs the epilogue (MI355X_MICROARCH.md, hand-off table row 1, as step.hip's
+//     split rows, per wave instead of per workgroup).
+// Every wave reads its column ids in SELL order (accumulate_sell: one coalesced id read per turn,
+// pads are dropped loads), so the kernel has no LDS, no barrier and a lean register budget.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "internal.h"
+
+#include "step_dev.h"
+
+namespace wg {
+namespace {
+
+// wave descriptor (two int4 per wave):
+//   d0 = {first SELL chunk, chunks per sub-group, first row, LN | rows << 8 | part << 16 | pair << 17}
+//   d1 = {part index, parts of the row, first partial slot, arrival counter}   (part waves only)
+struct TeamArgs {
+  StepArgs a;
+  const int4* wd;
+  int32_t n_waves;
+  double* wpart;   // [slots][LF * 4] float64 partials of part waves
+  int32_t* warr;   // [long rows] monotonic arrival counters
+};
+
+// MINW: minimum waves per SIMD the registers are held to (6 = the natural 77 VGPRs); LATE: the
+// epilogue's X0 / previous-row operands loaded after the gathers instead of before (fewer live
+// registers in the loop)
+template <bool LATE>
+__device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
+  const StepArgs& a = t.a;
+  const int4 d0 = t.wd[2 * w];  // uniform address: a scalar load
+  const int lane = threadIdx.x & 63;
+  const int LF = a.LF;
+  const int G = 64 / LF;
+  const int sg = lane / LF;
+  const int fs = lane - sg * LF;
+  const int LN = d0.w & 0xff;
+  const int tpw = (d0.w >> 8) & 0xff;
+  const bool part = (d0.w >> 16) & 1;
+  if ((d0.w >> 17) & 1) {  // a pair wave: sub-group g owns rows d0.z + g and d0.z + G + g, one chunk each
+    const int64_t ra = (int64_t)d0.z + sg, rb = ra + G;
+    const bool aa = sg < G && sg < tpw, ab = sg < G && sg + G < tpw;
+    EpiIn<4> ia, ib;
+    double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
+    if (aa) {
+      epi_prefetch<4>(a, ra, fs, ia);
+      if (ab) epi_prefetch<4>(a, rb, fs, ib);
+      accumulate_pair(a, d0.x, G, sg, fs, sa, sb);
+    }
+    if (aa) {
+      part_add<4>(a, ra, fs, sa);  // the hybrid step's dense blocks (phase 4; no-op otherwise)
+      step_epilogue<4>(a, ra, fs, sa, ia, sg * LF);
+    }
+    if (ab) {
+      part_add<4>(a, rb, fs, sb);
+      step_epilogue<4>(a, rb, fs, sb, ib, sg * LF);
+    }
+    return;
+  }
+  const int team = sg / LN;
+  const int ns = sg - team * LN;
+  const int64_t row = (int64_t)d0.z + team;
+  const bool active = sg < G && team < tpw;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  EpiIn<4> in;
+  if (active) {
+    if (!LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
+    accumulate_sell(a, int2{d0.x, d0.y}, G, sg, fs, acc);
+    if (LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
+  }
+  reduce_subgroups<4>(acc, LN, LF, team * LN * LF, fs);  // every lane (shuffles)
+  if (!part) {
+    if (active && ns == 0) {
+      part_add<4>(a, row, fs, acc);
+      step_epilogue<4>(a, row, fs, acc, in, team * LN * LF);
+    }
+    return;
+  }
+  // a share of a long row: float64 partial (sc1), drained, then one arrival per wave
+  const int4 d1 = t.wd[2 * w + 1];
+  const int width = LF * 4;
+  if (lane < LF) {
+    double* p = t.wpart + (int64_t)(d1.z + d1.x) * width + lane * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) __hip_atomic_store(p + j, acc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int last = 0;
+  if (lane == 0) {
+    const int old = __hip_atomic_fetch_add(t.warr + d1.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = ((old + 1) % d1.y) == 0;  // monotonic counter: every parts-th arrival completes a step
+  }
+  last = __shfl(last, 0, 64);
+  if (!last || lane >= LF) return;
+  EpiIn<4> in2;
+  epi_prefetch<4>(a, row, lane, in2);
+  double sum[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < d1.y; ++q) {  // part order: deterministic
+    const double* p = t.wpart + (int64_t)(d1.z + q) * width + lane * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum[j] += __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  part_add<4>(a, row, lane, sum);
+  step_epilogue<4>(a, row, lane, sum, in2, 0);
+}
+
+// STRIDE: a grid of a few workgroups per CU whose waves walk the table with a grid stride
+// (no per-entry wave dispatch) instead of one wave per entry
+template <int MINW, bool LATE, bool STRIDE>
+__global__ __launch_bounds__(256, MINW) void cheb_team4_kernel(TeamArgs t) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w0 = (int)blockIdx.x * 4 + wave;
+  if constexpr (STRIDE) {
+    for (int w = w0; w < t.n_waves; w += (int)gridDim.x * 4) team_wave<LATE>(t, w);
+  } else {
+    if (w0 < t.n_waves) team_wave<LATE>(t, w0);
+  }
+}
+
+}  // namespace
+
+void TeamPlan::release() {
+  for (void* q : {(void*)wd, (void*)sell, (void*)wpart, (void*)warr}) (void)hipFree(q);
+  *this = TeamPlan{};
+}
+
+// The wave table and SELL ids of the rows [0, n) of L's operator (internal order, rows by
+// descending length) for LF-lane sub-groups: a row of nch 4-entry chunks gets LN sub-groups, the
+// smallest divisor of G with ceil(nch / LN) <= tch chunks each (tch = iter / 4, even); consecutive
+// rows with the same LN share a wave (G / LN rows); a row longer than G * tch chunks is dealt to
+// ceil(nch / (G * tch)) part waves; with `pairs`, rows of <= 4 entries (one chunk) go 2 G to a
+// wave, two rows per sub-group (half the waves of the commonest rows).  Every sub-group of a
+// wave runs the wave's chunk count (two chunks per turn, a single one last when it is odd),
+// shorter ones padded with kPadCol chunks.
+int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, bool pairs, const int32_t* dcol,
+                     const int32_t* drsplit, TeamPlan* tp) {
+  const int G = 64 / LF;
+  const int64_t tch = std::max<int64_t>(2, (iter / 4 + 1) / 2 * 2);
+  std::vector<int32_t> rs(n + 1);  // row starts; the entries of row r are [rs[r], re[r])
+  WG_HIP_TRY(hipMemcpy(rs.data(), L->rowptr, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToHost));
+  std::vector<int32_t> col(std::max<int32_t>(rs[n], 1));
+  if (rs[n]) WG_HIP_TRY(hipMemcpy(col.data(), dcol, sizeof(int32_t) * rs[n], hipMemcpyDeviceToHost));
+  std::vector<int32_t> re(rs.begin() + 1, rs.end());  // drsplit: the hybrid step's tail ends
+  if (drsplit && n) WG_HIP_TRY(hipMemcpy(re.data(), drsplit, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  auto rlen = [&](int64_t r) -> int64_t { return re[r] - rs[r]; };
+  std::vector<int> divs;
+  for (int d = 1; d <= G; ++d)
+    if (G % d == 0) divs.push_back(d);
+  std::vector<int4> wd;
+  std::vector<int4> sell;
+  const int4 pad4{kPadCol, kPadCol, kPadCol, kPadCol};
+  int32_t slots = 0, longs = 0;
+  auto chunk = [&](int64_t r, int64_t ch) {  // the 4 ids of chunk ch of row r
+    int32_t id[4];
+    for (int i = 0; i < 4; ++i) {
+      const int64_t e = (int64_t)rs[r] + ch * 4 + i;
+      id[i] = e < re[r] ? col[e] : kPadCol;
+    }
+    return int4{id[0], id[1], id[2], id[3]};
+  };
+  auto fits = [&]() {
+    return sell.size() < ((size_t)1 << 27);  // 16-B chunks at 32-bit byte offsets (accumulate_sell)
+  };
+  int64_t r = 0;
+  while (r < n) {
+    const int64_t nch0 = (rlen(r) + 3) / 4;
+    if (nch0 > (int64_t)G * tch) {  // a long row: part waves, all G sub-groups on one share each
+      const int64_t per = (int64_t)G * tch;
+      const int32_t parts = (int32_t)((nch0 + per - 1) / per);
+      for (int32_t q = 0; q < parts; ++q) {
+        const int64_t c0 = q * per, c1 = std::min<int64_t>(nch0, c0 + per);
+        const int64_t nchs = (c1 - c0 + G - 1) / G;  // chunks per sub-group
+        wd.push_back(int4{(int32_t)sell.size(), (int32_t)nchs, (int32_t)r, G | (1 << 8) | (1 << 16)});
+        wd.push_back(int4{q, parts, slots, longs});
+        const size_t base = sell.size();
+        sell.resize(base + (size_t)nchs * G, pad4);
+        for (int64_t c = c0; c < c1; ++c) sell[base + (size_t)(c - c0)] = chunk(r, c);  // chunk k: k / G, k % G
+        if (!fits()) return fail(WG_ERR_UNSUPPORTED, "team waves: id array exceeds 2 GB");
+      }
+      slots += parts;
+      ++longs;
+      ++r;
+      continue;
+    }
+    if (pairs && nch0 == 1) {  // rows of <= 4 entries: 2 G per wave, two rows per sub-group
+      int rows = 0;
+      while (rows < 2 * G && r + rows < n && rlen(r + rows) <= 4) ++rows;
+      wd.push_back(int4{(int32_t)sell.size(), 2, (int32_t)r, 1 | (rows << 8) | (1 << 17)});
+      wd.push_back(int4{0, 0, 0, 0});
+      const size_t base = sell.size();
+      sell.resize(base + (size_t)2 * G, pad4);
+      for (int i = 0; i < rows; ++i) sell[base + (size_t)i] = chunk(r + i, 0);  // k = i / G, g = i % G
+      if (!fits()) return fail(WG_ERR_UNSUPPORTED, "team waves: id array exceeds 2 GB");
+      r += rows;
+      continue;
+    }
+    int LN = G;
+    for (int d : divs)
+      if ((nch0 + d - 1) / d <= tch) {
+        LN = d;
+        break;
+      }
+    const int tpw = G / LN;
+    int rows = 0;
+    while (rows < tpw && r + rows < n) {  // consecutive rows with the same LN
+      const int64_t nch = (rlen(r + rows) + 3) / 4;
+      if (nch > (int64_t)G * tch) break;
+      int ln = G;
+      for (int d : divs)
+        if ((nch + d - 1) / d <= tch) {
+          ln = d;
+          break;
+        }
+      if (ln != LN) break;
+      ++rows;
+    }
+    int64_t nchs = 0;  // chunks per sub-group: the wave's most (sub-group 0 of its longest row)
+    for (int i = 0; i < rows; ++i) {
+      const int64_t nch = (rlen(r + i) + 3) / 4;
+      nchs = std::max<int64_t>(nchs, (nch + LN - 1) / LN);
+    }
+    wd.push_back(int4{(int32_t)sell.size(), (int32_t)nchs, (int32_t)r, LN | (rows << 8)});
+    wd.push_back(int4{0, 0, 0, 0});
+    const size_t base = sell.size();
+    sell.resize(base + (size_t)nchs * G, pad4);
+    for (int i = 0; i < rows; ++i) {
+      const int64_t nch = (rlen(r + i) + 3) / 4;
+      for (int ns = 0; ns < LN; ++ns)
+        for (int64_t k = 0; ns + k * LN < nch; ++k)
+          sell[base + (size_t)k * G + (size_t)(i * LN + ns)] = chunk(r + i, ns + k * LN);
+    }
+    if (!fits()) return fail(WG_ERR_UNSUPPORTED, "team waves: id array exceeds 2 GB");
+    r += rows;
+  }
+  sell.resize(sell.size() + (size_t)4 * G, pad4);  // the next-turn id reads past the last wave
+  tp->n_waves = (int32_t)(wd.size() / 2);
+  tp->n_slots = slots;
+  tp->n_long = longs;
+  tp->width = LF * 4;
+  int rc = dmalloc(&tp->wd, std::max<size_t>(wd.size(), 2));
+  if (!rc) rc = dmalloc(&tp->sell, sell.size());
+  if (!rc) rc = dmalloc(&tp->wpart, (size_t)std::max(slots, 1) * tp->width);
+  if (!rc) rc = dmalloc(&tp->warr, (size_t)std::max(longs, 1));
+  if (rc) return rc;
+  if (!wd.empty()) WG_HIP_TRY(hipMemcpy(tp->wd, wd.data(), sizeof(int4) * wd.size(), hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipMemcpy(tp->sell, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice));
+  WG_HIP_TRY(hipMemset(tp->warr, 0, sizeof(int32_t) * std::max(longs, 1)));
+  return WG_OK;
+}
+
+int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, int grid_per_cu, hipStream_t stream) {
+  if (tp.n_waves <= 0) return WG_OK;
+  TeamArgs t{};
+  t.a = a;
+  t.wd = tp.wd;
+  t.n_waves = tp.n_waves;
+  t.wpart = tp.wpart;
+  t.warr = tp.warr;
+  t.a.sell = tp.sell;
+  const int64_t full = ceil_div(tp.n_waves, 4);
+  const dim3 block(256);
+  if (grid_per_cu > 0) {
+    int dev = 0;
+    WG_HIP_TRY(hipGetDevice(&dev));
+    const dim3 grid((unsigned)std::min<int64_t>(full, (int64_t)grid_per_cu * n_cus(dev)));
+    hipLaunchKernelGGL((cheb_team4_kernel<6, false, true>), grid, block, 0, stream, t);
+    WG_LAUNCH_CHECK();
+    return WG_OK;
+  }
+  const dim3 grid((unsigned)full);
+  switch (variant) {
+    case 7: hipLaunchKernelGGL((cheb_team4_kernel<7, false, false>), grid, block, 0, stream, t); break;
+    case 8: hipLaunchKernelGGL((cheb_team4_kernel<8, false, false>), grid, block, 0, stream, t); break;
+    case 9: hipLaunchKernelGGL((cheb_team4_kernel<8, true, false>), grid, block, 0, stream, t); break;
+    case 10: hipLaunchKernelGGL((cheb_team4_kernel<6, true, false>), grid, block, 0, stream, t); break;
+    default: hipLaunchKernelGGL((cheb_team4_kernel<6, false, false>), grid, block, 0, stream, t);
+  }
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+
+}  // namespace wg

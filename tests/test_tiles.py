@@ -48,7 +48,9 @@ def test_tiles_vs_oracle_and_gather(F, k):
     blocks, one or two 16-row groups per wave, or waves owning one 16-column block
     for four row groups (tile_rg = 4); the 32x32x16 MFMA shape (tile_mfma = 32,
     widths 48 / 64; narrower widths keep the 16x16x32 kernel); the first step
-    gathers u_0 = X0 * dinv value-free (K = 1: the only step)."""
+    gathers u_0 = X0 * dinv value-free (K = 1: the only step); the tail entries on
+    the independent-wave kernel (csrc/team.hip; team_iter 8: long tails as part
+    waves) and on the workgroup kernel (team = 0)."""
     g = rmat_graph(4000, 120000, seed=F + k)
     A = g.to_scipy()
     X = np.random.default_rng(F * 31 + k).standard_normal((g.n, F)).astype(np.float32)
@@ -58,7 +60,9 @@ def test_tiles_vs_oracle_and_gather(F, k):
     for knobs in (dict(tile_th=64, tile_max=128, tile_rows=128, tile_rg=2), dict(tile_th=8, tile_max=3, tile_rows=64),
                   dict(tile_th=1, tile_max=1, tile_rows=128, tile_rg=1), dict(tile_th=16, tile_max=5, tile_rows=128, tile_rg=4),
                   dict(tile_th=1, tile_max=1, tile_rows=128, tile_mfma=32),
-                  dict(tile_th=16, tile_max=5, tile_rows=128, tile_mfma=32)):
+                  dict(tile_th=16, tile_max=5, tile_rows=128, tile_mfma=32),
+                  dict(tile_th=16, tile_max=5, tile_rows=128, team_iter=8),
+                  dict(tile_th=8, tile_max=3, tile_rows=64, team=0, team_iter=96)):
         H1, S1 = _run(L, X, k, tiles=1, **knobs)
         assert "tiles:" in L.describe(F), f"hybrid step not planned: {L.describe(F)}"
         assert_parity(_np(S1), ref["S"], what=f"F={F} K={k} {knobs} S")

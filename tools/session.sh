@@ -57,7 +57,7 @@ for step in "$@"; do
             python3 bench.py --steps 2 --warmup 1 $HEADLINE > "$OUT/pmc_$tag.log" 2>&1
         stop_if_fatal $? "pmc $tag"
       done
-      python3 tools/pmc_traffic.py --kernel "${PMC_KERNEL:-cheb_step_kernel<4, true}" "$OUT"/pmc_* \
+      python3 tools/pmc_traffic.py --kernel "${PMC_KERNEL:-cheb_team4_kernel}" "$OUT"/pmc_* \
           --out "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
       rm -rf "$OUT"/pmc_FETCH_SIZE "$OUT"/pmc_WRITE_SIZE "$OUT"/pmc_TCC_HIT_sum ;;
     sweep:*)

@@ -74,7 +74,9 @@ def main():
     X = torch.randn(L.n, F, device="cuda") if F > 1 else L.log1p_degree()
     n_act = L.n - int(L.info["n_closed_form"])
     bstep = 8 * L.nnz + 4 * (n_act + 1) + 20 * n_act * F
-    grid = [(kv.split("=")[0], [int(v) for v in kv.split("=")[1].split(",")]) for kv in a.grid.split(";") if kv]
+    # knobs separated by ';' or '/' (the latter survives a shell command line unquoted)
+    grid = [(kv.split("=")[0], [int(v) for v in kv.split("=")[1].split(",")])
+            for kv in a.grid.replace("/", ";").split(";") if kv]
     names = [k for k, _ in grid]
     # Clock ramp: without ~1 s of load first, the first grid entry reads 2-3 us slow
     # on arxiv F=40 (profiles/r01/s48_ab.log round 0, s51_iter_sweep.log).
