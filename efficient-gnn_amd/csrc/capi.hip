@@ -212,15 +212,11 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.gather4 = (int32_t)(value == 1 ? 21 : value);
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "team")) {
-    if (value < 0 || value > 10 || (value > 1 && value < 7))
-      return fail(WG_ERR_INVALID, "team must be 0 (off), 1 (default), 7, 8, 9 or 10");
+    if (value < 0 || value > 13 || (value > 1 && value < 7))
+      return fail(WG_ERR_INVALID, "team must be 0 (off), 1 (default) or 7 .. 13");
     L->tune.team = (int32_t)value;
     return WG_OK;  // launch-time choice (the wave table is built with the plan on first use)
-  } else if (!strcmp(key, "team_pairs")) {
-    L->tune.team_pairs = value ? 1 : 0;
-  } else if (!strcmp(key, "team_grid")) {
-    if (value < 0 || value > 64) return fail(WG_ERR_INVALID, "team_grid must be in [0, 64]");
-    L->tune.team_grid = (int32_t)value;
+
   } else if (!strcmp(key, "team_iter")) {
     if (value < 8 || value > 4096) return fail(WG_ERR_INVALID, "team_iter must be in [8, 4096]");
     L->tune.team_iter = (int32_t)value;

@@ -231,11 +231,9 @@ struct Tuning {
   int32_t gather4 = 21;      // value-free VEC-4 steps on the padded CSR (step.hip build_pcol / accumulate_u4):
                              // 0 = off, else 10 x chunks per turn + turns of ids in flight (21, 22, 31, 41)
   int32_t sell = 1;          // padded-CSR steps: team waves read their ids in SELL order (step.hip build_sell)
-  int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 / 8 / 9 / 10:
-                             // register-budget variants (team.hip launch_team4)
+  int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 .. 13:
+                             // register-budget / turn-size variants (team.hip launch_team4; all time the same)
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
-  int32_t team_pairs = 1;    // team.hip: rows of <= 4 entries two to a sub-group (pair waves)
-  int32_t team_grid = 0;     // team.hip: 0 = a wave per table entry; n = n workgroups per CU walking the table
   int32_t graph = 0;         // wg_wavelet_features: replay the chain as a hipGraph from its 3rd call with the same
                              // arguments (1 = on; -1 = small chains only, active nnz x width <= 2^22).  Off: the
                              // replay measured SLOWER than eager launches on this stack, +2.7 us per kernel node
@@ -381,10 +379,10 @@ int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src
 int build_pcol(wg_laplacian_s* L);
 // team.hip: the wave table of rows [0, n) for LF-lane sub-groups, and its launch
 // (dcol: the operator's column ids, or the hybrid step's tail-first copy, drsplit its rows' tail ends)
-int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, bool pairs, const int32_t* dcol,
+int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32_t* dcol,
                      const int32_t* drsplit, TeamPlan* tp);
 struct StepArgs;
-int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, int grid_per_cu, hipStream_t stream);
+int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream);
 // the value-free VEC-4 gathers on the padded CSR apply to an F-wide (internal width) signal
 bool gather4_applies(const wg_laplacian_s* L, int64_t F);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);

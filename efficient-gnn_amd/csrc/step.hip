@@ -915,14 +915,14 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       const bool g4 = vec == 4 && a.uin && F == fw && gather4_applies(L, F);
       if (g4 && L->tune.team) {
         if (!plan->team.wd)
-          if (int rc2 = build_team_waves(L, plan->row1, LF, L->tune.team_iter, L->tune.team_pairs != 0,
-                                         hyb ? hyb->tcol : L->col, hyb ? hyb->tsplit : nullptr, &plan->team))
+          if (int rc2 = build_team_waves(L, plan->row1, LF, L->tune.team_iter, hyb ? hyb->tcol : L->col,
+                                         hyb ? hyb->tsplit : nullptr, &plan->team))
             return rc2;
         a.u_bytes = (uint32_t)(L->n_cols * F * 4);
         a.probe = L->tune.probe;
         a.probe_h2 = L->tune.probe_h2;
         a.probe_fold = L->tune.probe_fold;
-        if (int rc2 = launch_team4(plan->team, a, L->tune.team, L->tune.team_grid, stream)) return rc2;
+        if (int rc2 = launch_team4(plan->team, a, L->tune.team, stream)) return rc2;
         continue;
       }
       if (g4 && !hyb) {

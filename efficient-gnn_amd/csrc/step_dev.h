@@ -602,6 +602,9 @@ __device__ __forceinline__ void sum_turn(const u32x4_t* x, int n, double (&acc)[
   acc[3] += (double)h2[0].y;
 }
 
+// CPT: chunks per turn (2: a turn of 8 gathers, a single chunk last when the count is odd; 1:
+// turns of 4 gathers and fewer live registers)
+template <int CPT = 2>
 __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int G, int g, int fs, double (&acc)[4]) {
   if (wm.y <= 0) return;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0,
@@ -621,6 +624,20 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
 #endif
     return __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24(c, rb) + lo, 0, 0);
   };
+  if constexpr (CPT == 1) {
+    u32x4_t c0 = ld(off);  // the array is padded past its last wave
+    for (int t = 0; t < wm.y; ++t) {
+      off += cstep;
+      const u32x4_t n0 = ld(off);
+      const uint32_t cc[4] = {c0.x, c0.y, c0.z, c0.w};
+      u32x4_t x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = gather(cc[u]);
+      sum_turn(x, 4, acc);
+      c0 = n0;
+    }
+    return;
+  }
   const int pairs = wm.y >> 1;
   u32x4_t c0 = ld(off), c1 = ld(off + cstep);  // the array is padded past its last wave
   for (int t = 0; t < pairs; ++t) {
@@ -630,6 +647,15 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
     u32x4_t x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) x[u] = gather(cc[u]);
+#ifdef WG_TIMING_PROBES
+    if (a.probe_h2 == -6) {  // one more id-load instruction per turn (its cost through the address unit)
+      const u32x4_t e = ld(off + 2 * cstep);
+      asm volatile("" ::"v"(e.x));
+    } else if (a.probe_h2 == -7) {  // one more gather instruction per turn (same line: an L1 hit)
+      const u32x4_t e = gather(cc[7]);
+      asm volatile("" ::"v"(e.x));
+    }
+#endif
     sum_turn(x, 8, acc);
     c0 = n0;
     c1 = n1;
@@ -641,28 +667,6 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
     for (int u = 0; u < 4; ++u) x[u] = gather(cc[u]);
     sum_turn(x, 4, acc);
   }
-}
-
-// A pair wave's sub-group g (team.hip): chunk 0 = row A's ids, chunk 1 = row B's (one each, rows of
-// <= 4 entries), one turn of 8 gathers, the two sums kept apart (each the single-chunk sum of
-// accumulate_sell: bitwise the same as a wave of one row per sub-group)
-__device__ __forceinline__ void accumulate_pair(const StepArgs& a, int32_t first, int G, int g, int fs,
-                                                double (&sa)[4], double (&sb)[4]) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0,
-                                                                      (int)a.u_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(const_cast<int4*>(a.sell), 0, 0x7fffffff,
-                                                                      0x00020000);
-  const uint32_t rb = (uint32_t)a.ld * 4u;
-  const uint32_t lo = (uint32_t)fs * 16u;
-  const uint32_t off = ((uint32_t)first + (uint32_t)g) * 16u;
-  const u32x4_t c0 = __builtin_amdgcn_raw_buffer_load_b128(ri, off, 0, 0);
-  const u32x4_t c1 = __builtin_amdgcn_raw_buffer_load_b128(ri, off + (uint32_t)G * 16u, 0, 0);
-  const uint32_t cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  u32x4_t x[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) x[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24(cc[u], rb) + lo, 0, 0);
-  sum_turn(x, 4, sa);
-  sum_turn(x + 4, 4, sb);
 }
 
 template <int VEC, bool BCAST, bool HOT>

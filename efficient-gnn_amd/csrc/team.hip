@@ -29,7 +29,7 @@ namespace wg {
 namespace {
 
 // wave descriptor (two int4 per wave):
-//   d0 = {first SELL chunk, chunks per sub-group, first row, LN | rows << 8 | part << 16 | pair << 17}
+//   d0 = {first SELL chunk, chunks per sub-group, first row, LN | rows << 8 | part << 16}
 //   d1 = {part index, parts of the row, first partial slot, arrival counter}   (part waves only)
 struct TeamArgs {
   StepArgs a;
@@ -42,10 +42,13 @@ struct TeamArgs {
 // MINW: minimum waves per SIMD the registers are held to (6 = the natural 77 VGPRs); LATE: the
 // epilogue's X0 / previous-row operands loaded after the gathers instead of before (fewer live
 // registers in the loop)
-template <bool LATE>
+template <bool LATE, int CPT>
 __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
   const StepArgs& a = t.a;
-  const int4 d0 = t.wd[2 * w];  // uniform address: a scalar load
+#ifdef WG_TIMING_PROBES
+  if (a.probe_h2 == -4) return;  // launch + wave dispatch only
+#endif
+  int4 d0 = t.wd[2 * w];  // uniform address: a scalar load
   const int lane = threadIdx.x & 63;
   const int LF = a.LF;
   const int G = 64 / LF;
@@ -54,84 +57,67 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
   const int LN = d0.w & 0xff;
   const int tpw = (d0.w >> 8) & 0xff;
   const bool part = (d0.w >> 16) & 1;
-  if ((d0.w >> 17) & 1) {  // a pair wave: sub-group g owns rows d0.z + g and d0.z + G + g, one chunk each
-    const int64_t ra = (int64_t)d0.z + sg, rb = ra + G;
-    const bool aa = sg < G && sg < tpw, ab = sg < G && sg + G < tpw;
-    EpiIn<4> ia, ib;
-    double sa[4] = {0.0, 0.0, 0.0, 0.0}, sb[4] = {0.0, 0.0, 0.0, 0.0};
-    if (aa) {
-      epi_prefetch<4>(a, ra, fs, ia);
-      if (ab) epi_prefetch<4>(a, rb, fs, ib);
-      accumulate_pair(a, d0.x, G, sg, fs, sa, sb);
-    }
-    if (aa) {
-      part_add<4>(a, ra, fs, sa);  // the hybrid step's dense blocks (phase 4; no-op otherwise)
-      step_epilogue<4>(a, ra, fs, sa, ia, sg * LF);
-    }
-    if (ab) {
-      part_add<4>(a, rb, fs, sb);
-      step_epilogue<4>(a, rb, fs, sb, ib, sg * LF);
-    }
-    return;
-  }
   const int team = sg / LN;
   const int ns = sg - team * LN;
   const int64_t row = (int64_t)d0.z + team;
   const bool active = sg < G && team < tpw;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   EpiIn<4> in;
+#ifdef WG_TIMING_PROBES
+  if (a.probe_h2 == -3) {  // no ids, gathers or epilogue operands: one 16-B store per row
+    if (active && ns == 0 && a.xk)
+      *reinterpret_cast<float4*>(a.xk + row * a.ld + fs * 4) = float4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  if (a.probe_h2 == -2) d0.y = 0;  // no ids, no gathers
+#endif
   if (active) {
     if (!LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
-    accumulate_sell(a, int2{d0.x, d0.y}, G, sg, fs, acc);
+    accumulate_sell<CPT>(a, int2{d0.x, d0.y}, G, sg, fs, acc);
     if (LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
   }
   reduce_subgroups<4>(acc, LN, LF, team * LN * LF, fs);  // every lane (shuffles)
-  if (!part) {
-    if (active && ns == 0) {
-      part_add<4>(a, row, fs, acc);
-      step_epilogue<4>(a, row, fs, acc, in, team * LN * LF);
+  bool emit = active && ns == 0;
+  int lane0 = team * LN * LF;
+  if (part) {  // a share of a long row: float64 partial (sc1), drained, then one arrival per wave
+    const int4 d1 = t.wd[2 * w + 1];
+    const int width = LF * 4;
+    if (lane < LF) {
+      double* p = t.wpart + (int64_t)(d1.z + d1.x) * width + lane * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) __hip_atomic_store(p + j, acc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return;
-  }
-  // a share of a long row: float64 partial (sc1), drained, then one arrival per wave
-  const int4 d1 = t.wd[2 * w + 1];
-  const int width = LF * 4;
-  if (lane < LF) {
-    double* p = t.wpart + (int64_t)(d1.z + d1.x) * width + lane * 4;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) {
+      const int old = __hip_atomic_fetch_add(t.warr + d1.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = ((old + 1) % d1.y) == 0;  // monotonic counter: every parts-th arrival completes a step
+    }
+    last = __shfl(last, 0, 64);
+    if (!last || lane >= LF) return;
+    // the last arriver: lanes 0 .. LF-1 (sub-group 0: fs == lane) sum every part's partial in
+    // part order (deterministic) and share the team rows' epilogue below (one inlined copy)
+    epi_prefetch<4>(a, row, lane, in);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) __hip_atomic_store(p + j, acc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int last = 0;
-  if (lane == 0) {
-    const int old = __hip_atomic_fetch_add(t.warr + d1.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = ((old + 1) % d1.y) == 0;  // monotonic counter: every parts-th arrival completes a step
-  }
-  last = __shfl(last, 0, 64);
-  if (!last || lane >= LF) return;
-  EpiIn<4> in2;
-  epi_prefetch<4>(a, row, lane, in2);
-  double sum[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int q = 0; q < d1.y; ++q) {  // part order: deterministic
-    const double* p = t.wpart + (int64_t)(d1.z + q) * width + lane * 4;
+    for (int j = 0; j < 4; ++j) acc[j] = 0.0;
+    for (int q = 0; q < d1.y; ++q) {
+      const double* p = t.wpart + (int64_t)(d1.z + q) * width + lane * 4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sum[j] += __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int j = 0; j < 4; ++j) acc[j] += __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    emit = true;
+    lane0 = 0;
   }
-  part_add<4>(a, row, lane, sum);
-  step_epilogue<4>(a, row, lane, sum, in2, 0);
+  if (emit) {
+    part_add<4>(a, row, fs, acc);
+    step_epilogue<4>(a, row, fs, acc, in, lane0);
+  }
 }
 
-// STRIDE: a grid of a few workgroups per CU whose waves walk the table with a grid stride
-// (no per-entry wave dispatch) instead of one wave per entry
-template <int MINW, bool LATE, bool STRIDE>
+template <int MINW, bool LATE, int CPT = 2>
 __global__ __launch_bounds__(256, MINW) void cheb_team4_kernel(TeamArgs t) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int w0 = (int)blockIdx.x * 4 + wave;
-  if constexpr (STRIDE) {
-    for (int w = w0; w < t.n_waves; w += (int)gridDim.x * 4) team_wave<LATE>(t, w);
-  } else {
-    if (w0 < t.n_waves) team_wave<LATE>(t, w0);
-  }
+  const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w < t.n_waves) team_wave<LATE, CPT>(t, w);
 }
 
 }  // namespace
@@ -145,11 +131,9 @@ void TeamPlan::release() {
 // descending length) for LF-lane sub-groups: a row of nch 4-entry chunks gets LN sub-groups, the
 // smallest divisor of G with ceil(nch / LN) <= tch chunks each (tch = iter / 4, even); consecutive
 // rows with the same LN share a wave (G / LN rows); a row longer than G * tch chunks is dealt to
-// ceil(nch / (G * tch)) part waves; with `pairs`, rows of <= 4 entries (one chunk) go 2 G to a
-// wave, two rows per sub-group (half the waves of the commonest rows).  Every sub-group of a
-// wave runs the wave's chunk count (two chunks per turn, a single one last when it is odd),
+// ceil(nch / (G * tch)) part waves.  Every sub-group of a wave runs the wave's chunk count (two chunks per turn, a single one last when it is odd),
 // shorter ones padded with kPadCol chunks.
-int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, bool pairs, const int32_t* dcol,
+int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32_t* dcol,
                      const int32_t* drsplit, TeamPlan* tp) {
   const int G = 64 / LF;
   const int64_t tch = std::max<int64_t>(2, (iter / 4 + 1) / 2 * 2);
@@ -197,18 +181,6 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, bool pairs,
       slots += parts;
       ++longs;
       ++r;
-      continue;
-    }
-    if (pairs && nch0 == 1) {  // rows of <= 4 entries: 2 G per wave, two rows per sub-group
-      int rows = 0;
-      while (rows < 2 * G && r + rows < n && rlen(r + rows) <= 4) ++rows;
-      wd.push_back(int4{(int32_t)sell.size(), 2, (int32_t)r, 1 | (rows << 8) | (1 << 17)});
-      wd.push_back(int4{0, 0, 0, 0});
-      const size_t base = sell.size();
-      sell.resize(base + (size_t)2 * G, pad4);
-      for (int i = 0; i < rows; ++i) sell[base + (size_t)i] = chunk(r + i, 0);  // k = i / G, g = i % G
-      if (!fits()) return fail(WG_ERR_UNSUPPORTED, "team waves: id array exceeds 2 GB");
-      r += rows;
       continue;
     }
     int LN = G;
@@ -265,7 +237,7 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, bool pairs,
   return WG_OK;
 }
 
-int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, int grid_per_cu, hipStream_t stream) {
+int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream) {
   if (tp.n_waves <= 0) return WG_OK;
   TeamArgs t{};
   t.a = a;
@@ -274,23 +246,16 @@ int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, int grid_pe
   t.wpart = tp.wpart;
   t.warr = tp.warr;
   t.a.sell = tp.sell;
-  const int64_t full = ceil_div(tp.n_waves, 4);
-  const dim3 block(256);
-  if (grid_per_cu > 0) {
-    int dev = 0;
-    WG_HIP_TRY(hipGetDevice(&dev));
-    const dim3 grid((unsigned)std::min<int64_t>(full, (int64_t)grid_per_cu * n_cus(dev)));
-    hipLaunchKernelGGL((cheb_team4_kernel<6, false, true>), grid, block, 0, stream, t);
-    WG_LAUNCH_CHECK();
-    return WG_OK;
-  }
-  const dim3 grid((unsigned)full);
+  const dim3 grid((unsigned)ceil_div(tp.n_waves, 4)), block(256);
   switch (variant) {
-    case 7: hipLaunchKernelGGL((cheb_team4_kernel<7, false, false>), grid, block, 0, stream, t); break;
-    case 8: hipLaunchKernelGGL((cheb_team4_kernel<8, false, false>), grid, block, 0, stream, t); break;
-    case 9: hipLaunchKernelGGL((cheb_team4_kernel<8, true, false>), grid, block, 0, stream, t); break;
-    case 10: hipLaunchKernelGGL((cheb_team4_kernel<6, true, false>), grid, block, 0, stream, t); break;
-    default: hipLaunchKernelGGL((cheb_team4_kernel<6, false, false>), grid, block, 0, stream, t);
+    case 7: hipLaunchKernelGGL((cheb_team4_kernel<7, false>), grid, block, 0, stream, t); break;
+    case 8: hipLaunchKernelGGL((cheb_team4_kernel<8, false>), grid, block, 0, stream, t); break;
+    case 9: hipLaunchKernelGGL((cheb_team4_kernel<8, true>), grid, block, 0, stream, t); break;
+    case 10: hipLaunchKernelGGL((cheb_team4_kernel<6, true>), grid, block, 0, stream, t); break;
+    case 11: hipLaunchKernelGGL((cheb_team4_kernel<6, false, 1>), grid, block, 0, stream, t); break;
+    case 12: hipLaunchKernelGGL((cheb_team4_kernel<8, false, 1>), grid, block, 0, stream, t); break;
+    case 13: hipLaunchKernelGGL((cheb_team4_kernel<8, true, 1>), grid, block, 0, stream, t); break;
+    default: hipLaunchKernelGGL((cheb_team4_kernel<6, false>), grid, block, 0, stream, t);
   }
   WG_LAUNCH_CHECK();
   return WG_OK;

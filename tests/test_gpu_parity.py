@@ -215,11 +215,11 @@ def test_padded_csr_gathers(F):
     """The value-free VEC-4 step on the padded CSR (rows padded to 4-entry chunks of
     dropped pad ids) against the oracle, on the arxiv-size graph and the same graph
     with no closed-form rows: the independent-wave kernel (team.hip; team_iter 32 /
-    96 / 512: long rows as part waves combined by arrival counters), the workgroup
+    96 / 512: long rows as part waves combined by arrival counters; its late-operand
+    and single-chunk-turn variants 9 / 13), the workgroup
     kernel with SELL-ordered team ids and with the per-row loop (bitwise equal: same
-    chunks, same sums), the old gather loop (gather4 = 0); the wave table walked by a
-    grid of 1 or 2 workgroups per CU (team_grid; bitwise equal to a wave per entry);
-    repeated calls bitwise equal."""
+    chunks, same sums), the old gather loop (gather4 = 0); repeated calls bitwise
+    equal."""
     g = named_graph("ogbn-arxiv")
     for gg in (g, connect_isolated(g, seed=7)):
         A = gg.to_scipy()
@@ -227,8 +227,8 @@ def test_padded_csr_gathers(F):
         ref = O.graph_wavelet_features(A, k=16, s=0.8, X0=X, return_all=True)
         L = NormalizedLaplacian.from_graph(gg)
         out = {}
-        for knobs in ({}, {"team_grid": 2}, {"team_grid": 1, "team_iter": 32}, {"team_pairs": 0}, {"team_iter": 32},
-                      {"team_iter": 512}, {"team": 0}, {"team": 0, "sell": 0},
+        for knobs in ({}, {"team_iter": 32}, {"team_iter": 512}, {"team": 9}, {"team": 13, "team_iter": 32},
+                      {"team": 0}, {"team": 0, "sell": 0},
                       {"team": 0, "gather4": 41, "sell": 0}, {"gather4": 0}):
             L.tune(**knobs)
             H, S = wats_hip.graph_wavelet_features(L, k=16, X0=torch.from_numpy(X), return_S=True)
@@ -237,10 +237,8 @@ def test_padded_csr_gathers(F):
             out[str(knobs)] = (_np(S), _np(H))
             assert_parity(out[str(knobs)][0], ref["S"], what=f"padded CSR F={F} {knobs} S")
             assert_parity(out[str(knobs)][1], ref["H"], what=f"padded CSR F={F} {knobs} H")
-            L.tune(gather4=1, sell=1, team=1, team_iter=96, team_pairs=1, team_grid=0)
+            L.tune(gather4=1, sell=1, team=1, team_iter=96)
         assert np.array_equal(out["{'team': 0}"][0], out["{'team': 0, 'sell': 0}"][0])
-        assert np.array_equal(out["{}"][0], out["{'team_grid': 2}"][0]), "the table walk changed the sums"
-        assert np.array_equal(out["{'team_iter': 32}"][0], out["{'team_grid': 1, 'team_iter': 32}"][0])
         L.close()
 
 

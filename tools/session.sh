@@ -10,6 +10,7 @@
 #                  (no companions / extras): its kernel summary reproduces the line's roofline
 #   pmc            FETCH_SIZE / WRITE_SIZE / L2 hit passes of the headline alone -> traffic.json
 #   sweep:<args>   python tools/sweep.py <args> (spaces as '+'), WATS_HIP_LIB from $LIB if set
+#   rehearse:<N>   tools/rehearse.sh: the N-rank bench with every rank on device 0 (IPC exchange)
 #   py:<script>    python <script> (spaces as '+')
 # Output: gpurun_out/$SESSION/.
 set -u
@@ -64,6 +65,9 @@ for step in "$@"; do
       args=$(echo "${step#sweep:}" | tr '+' ' ')
       WATS_HIP_LIB=${LIB:-} timeout -k 10 600 python -u tools/sweep.py $args > "$OUT/sweep$n.log" 2>&1
       stop_if_fatal $? "sweep$n" ;;
+    rehearse:*)
+      N=${step#rehearse:} SESSION=${SESSION:-session}/rehearse bash tools/rehearse.sh
+      stop_if_fatal $? "$step" ;;
     py:*)
       args=$(echo "${step#py:}" | tr '+' ' ')
       timeout -k 10 600 python -u $args > "$OUT/py$n.log" 2>&1
