@@ -671,7 +671,7 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
     traffic, traffic_src = None, None
     tj = args.traffic_json
     if tj == "auto":
-        tj = os.path.join(REPO, "profiles", "r03", "s35_traffic.json") \
+        tj = os.path.join(REPO, "profiles", "r04", "s25_traffic.json") \
             if (config == "ogbn-arxiv" and F == 40 and K == 16) else None
     if tj and tj != "none" and os.path.exists(tj):
         traffic = json.load(open(tj)).get("bytes_per_launch")

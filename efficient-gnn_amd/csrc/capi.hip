@@ -438,7 +438,10 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
   // writes S and H in the caller's order (no separate finalize pass)
   const bool fuse_fin = !lp && L->tune.fuse_finalize && Fp == F && K >= 1 && S && H &&
                         step_single_tile(L, F, {b0, b1, sint, S, H});
-  int rc = fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, stream)
+  // the first value-free Clenshaw step gathers u_0 = X0 * dinv: written by the same pass
+  const bool u0_fused = fuse_fin && u0 && !lp && L->tune.clenshaw && K >= 1;
+  int rc = fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, u0_fused ? L->ws + 3 * stride : nullptr,
+                                               stream)
                     : launch_permute_pad(L, F, Fp, X0, b0, stream);
   if (rc) return rc;
   if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * Fp, hipMemcpyDeviceToDevice, stream));
@@ -474,7 +477,7 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     // (L_hat b = -dinv_i sum_j u_j); X0 itself stays unscaled (the first step reads the values)
     const int useu = (L->unit && L->tune.uscale && L->tune.hot == 0) ? 1 : 0;
     float* ub = u0 ? L->ws + 3 * stride : nullptr;  // u_0 = X0 * dinv (active rows)
-    if (u0 && (rc = launch_scale_rows(L, L->n_active, Fp, b0, ub, stream))) return rc;
+    if (u0 && !u0_fused && (rc = launch_scale_rows(L, L->n_active, Fp, b0, ub, stream))) return rc;
     for (int32_t k = K - 1; k >= 1; --k) {
       float* out = bk2 ? bk2 : bufs[nb++];
       const double ck = c[k] - (bk2 == nullptr && k + 2 == K ? c[K] : 0.0);  // implicit b_{k+2} = c_K X0

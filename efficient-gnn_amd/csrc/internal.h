@@ -372,7 +372,7 @@ int padded_features(const wg_laplacian_s* L, int64_t F);
 bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const void*> ptrs);
 // permute-in that also writes the closed-form rows' S and H in the caller's order
 int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
-                             float* H, hipStream_t stream);
+                             float* H, float* u, hipStream_t stream);  // u: also u_0 = X0 * dinv (or nullptr)
 // caller rows (stride F) -> internal rows (stride Fp), pad columns zeroed
 int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);

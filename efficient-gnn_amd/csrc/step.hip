@@ -384,7 +384,8 @@ __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, in
                                                                    const float* __restrict__ src,
                                                                    float* __restrict__ dst, int64_t closed_from,
                                                                    double coef, float* __restrict__ S,
-                                                                   float* __restrict__ H) {
+                                                                   float* __restrict__ H, const double* __restrict__ dinv,
+                                                                   float* __restrict__ u) {
   const int lane = threadIdx.x & 63;
   const int G = 64 / LF;
   const int sg = lane / LF;
@@ -404,7 +405,16 @@ __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, in
       sv[j] = closed ? coef * (double)x[j] : (double)x[j];
       part += fabs(sv[j]);
     }
-    if (!closed) store_vec<VEC>(dst + row * F + fs * VEC, sv);
+    if (!closed) {
+      store_vec<VEC>(dst + row * F + fs * VEC, sv);
+      if (u) {  // u_0 = X0 * dinv for the first value-free step (scale_rows_kernel's rounding)
+        const double di = dinv[row];
+        double uv[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) uv[j] = (double)x[j] * di;
+        store_vec<VEC>(u + row * F + fs * VEC, uv);
+      }
+    }
   }
   // closed rows are the internal tail: most waves hold none and skip the row sums
   if (!__ballot(active && closed)) return;
@@ -1067,7 +1077,7 @@ bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const 
 }
 
 int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
-                             float* H, hipStream_t stream) {
+                             float* H, float* u, hipStream_t stream) {
   const int64_t n = L->n_rows;
   if (n == 0) return WG_OK;
   const int vec = pick_vec(F, {src, dst, S, H});
@@ -1077,13 +1087,13 @@ int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, flo
   const dim3 grid((unsigned)ceil_div(n, 4 * G));
   if (vec == 4)
     hipLaunchKernelGGL(permute_in_closed_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
-                       L->n_active, coef, S, H);
+                       L->n_active, coef, S, H, L->dinv, u);
   else if (vec == 2)
     hipLaunchKernelGGL(permute_in_closed_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
-                       L->n_active, coef, S, H);
+                       L->n_active, coef, S, H, L->dinv, u);
   else
     hipLaunchKernelGGL(permute_in_closed_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
-                       L->n_active, coef, S, H);
+                       L->n_active, coef, S, H, L->dinv, u);
   WG_LAUNCH_CHECK();
   return WG_OK;
 }
