@@ -217,6 +217,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.team = (int32_t)value;
     return WG_OK;  // launch-time choice (the wave table is built with the plan on first use)
 
+  } else if (!strcmp(key, "team_order")) {
+    if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
+    L->tune.team_order = (int32_t)value;
   } else if (!strcmp(key, "team_iter")) {
     if (value < 8 || value > 4096) return fail(WG_ERR_INVALID, "team_iter must be in [8, 4096]");
     L->tune.team_iter = (int32_t)value;

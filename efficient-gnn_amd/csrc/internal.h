@@ -234,6 +234,8 @@ struct Tuning {
   int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 .. 13:
                              // register-budget / turn-size variants (team.hip launch_team4; all time the same)
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
+  int32_t team_order = -1;   // team.hip: wave dispatch order (0 longest rows first, 1 reversed, 2 .. 7 mixed;
+                             // -1 auto: 2 for plain steps, 0 for the hybrid step's tail)
   int32_t graph = 0;         // wg_wavelet_features: replay the chain as a hipGraph from its 3rd call with the same
                              // arguments (1 = on; -1 = small chains only, active nnz x width <= 2^22).  Off: the
                              // replay measured SLOWER than eager launches on this stack, +2.7 us per kernel node
@@ -380,7 +382,7 @@ int build_pcol(wg_laplacian_s* L);
 // team.hip: the wave table of rows [0, n) for LF-lane sub-groups, and its launch
 // (dcol: the operator's column ids, or the hybrid step's tail-first copy, drsplit its rows' tail ends)
 int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32_t* dcol,
-                     const int32_t* drsplit, TeamPlan* tp);
+                     const int32_t* drsplit, int order, TeamPlan* tp);
 struct StepArgs;
 int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream);
 // the value-free VEC-4 gathers on the padded CSR apply to an F-wide (internal width) signal

@@ -926,7 +926,8 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       if (g4 && L->tune.team) {
         if (!plan->team.wd)
           if (int rc2 = build_team_waves(L, plan->row1, LF, L->tune.team_iter, hyb ? hyb->tcol : L->col,
-                                         hyb ? hyb->tsplit : nullptr, &plan->team))
+                                         hyb ? hyb->tsplit : nullptr,
+                                         L->tune.team_order >= 0 ? L->tune.team_order : (hyb ? 0 : 2), &plan->team))
             return rc2;
         a.u_bytes = (uint32_t)(L->n_cols * F * 4);
         a.probe = L->tune.probe;

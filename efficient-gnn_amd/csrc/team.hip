@@ -134,7 +134,7 @@ void TeamPlan::release() {
 // ceil(nch / (G * tch)) part waves.  Every sub-group of a wave runs the wave's chunk count (two chunks per turn, a single one last when it is odd),
 // shorter ones padded with kPadCol chunks.
 int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32_t* dcol,
-                     const int32_t* drsplit, TeamPlan* tp) {
+                     const int32_t* drsplit, int order, TeamPlan* tp) {
   const int G = 64 / LF;
   const int64_t tch = std::max<int64_t>(2, (iter / 4 + 1) / 2 * 2);
   std::vector<int32_t> rs(n + 1);  // row starts; the entries of row r are [rs[r], re[r])
@@ -222,6 +222,35 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
     r += rows;
   }
   sell.resize(sell.size() + (size_t)4 * G, pad4);  // the next-turn id reads past the last wave
+  if (order) {  // dispatch order of the waves (the table is built longest rows first)
+    const size_t nw = wd.size() / 2;
+    std::vector<int4> o;
+    o.reserve(wd.size());
+    // 1: reversed (shortest rows first); 2 ..: fa waves from the longest end, then fb from the
+    // shortest, repeated.  2 (one and one) mixes long and short rows in every workgroup: arxiv
+    // F = 40 33.9 vs 34.7 us; whole workgroups alternating (7) put every long row on every other
+    // XCD (round-robin placement): 51.9 (r04 s28)
+    static const int kFa[8] = {0, 0, 1, 2, 4, 1, 1, 4}, kFb[8] = {0, 0, 1, 1, 1, 2, 4, 4};
+    size_t lo = 0, hi = nw;
+    while (lo < hi) {
+      if (order == 1) {
+        --hi;
+        o.push_back(wd[2 * hi]);
+        o.push_back(wd[2 * hi + 1]);
+        continue;
+      }
+      for (int q = 0; q < kFa[order] && lo < hi; ++q, ++lo) {
+        o.push_back(wd[2 * lo]);
+        o.push_back(wd[2 * lo + 1]);
+      }
+      for (int q = 0; q < kFb[order] && lo < hi; ++q) {
+        --hi;
+        o.push_back(wd[2 * hi]);
+        o.push_back(wd[2 * hi + 1]);
+      }
+    }
+    wd.swap(o);
+  }
   tp->n_waves = (int32_t)(wd.size() / 2);
   tp->n_slots = slots;
   tp->n_long = longs;

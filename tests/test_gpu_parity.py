@@ -216,7 +216,8 @@ def test_padded_csr_gathers(F):
     dropped pad ids) against the oracle, on the arxiv-size graph and the same graph
     with no closed-form rows: the independent-wave kernel (team.hip; team_iter 32 /
     96 / 512: long rows as part waves combined by arrival counters; its late-operand
-    and single-chunk-turn variants 9 / 13), the workgroup
+    and single-chunk-turn variants 9 / 13; waves dispatched in other orders, bitwise
+    equal), the workgroup
     kernel with SELL-ordered team ids and with the per-row loop (bitwise equal: same
     chunks, same sums), the old gather loop (gather4 = 0); repeated calls bitwise
     equal."""
@@ -228,6 +229,7 @@ def test_padded_csr_gathers(F):
         L = NormalizedLaplacian.from_graph(gg)
         out = {}
         for knobs in ({}, {"team_iter": 32}, {"team_iter": 512}, {"team": 9}, {"team": 13, "team_iter": 32},
+                      {"team_order": 0}, {"team_order": 1, "team_iter": 32}, {"team_order": 6},
                       {"team": 0}, {"team": 0, "sell": 0},
                       {"team": 0, "gather4": 41, "sell": 0}, {"gather4": 0}):
             L.tune(**knobs)
@@ -237,8 +239,10 @@ def test_padded_csr_gathers(F):
             out[str(knobs)] = (_np(S), _np(H))
             assert_parity(out[str(knobs)][0], ref["S"], what=f"padded CSR F={F} {knobs} S")
             assert_parity(out[str(knobs)][1], ref["H"], what=f"padded CSR F={F} {knobs} H")
-            L.tune(gather4=1, sell=1, team=1, team_iter=96)
+            L.tune(gather4=1, sell=1, team=1, team_iter=96, team_order=-1)
         assert np.array_equal(out["{'team': 0}"][0], out["{'team': 0, 'sell': 0}"][0])
+        assert np.array_equal(out["{}"][0], out["{'team_order': 0}"][0]), "the wave order changed the sums"
+        assert np.array_equal(out["{}"][0], out["{'team_order': 6}"][0])
         L.close()
 
 
