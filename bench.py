@@ -285,6 +285,12 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         g.manual_seed(1 + rank)
         X = torch.randn(r1 - r0, F, generator=g, device=device)
     out = (torch.empty(r1 - r0, F, device=device), torch.empty(r1 - r0, F, device=device))
+    if exchange in ("rccl", "ipc") and sw._dist is not None:
+        # the signal already in the chain's input buffer (as graph_wavelet_features reads the
+        # caller's X0 in place): no per-chain copy into it
+        xb = sw._buf("X", r1 - r0, X.shape[1] if X.dim() == 2 else 1)
+        xb.copy_(X.reshape(xb.shape))
+        X = xb
     _log(f"sharded {config} ({exchange}): shard ready ({r1 - r0} rows, {sw.plan.n_halo} halo rows); warmup")
     run = (lambda: sw.wavelet_features(X, k=K, s=s_heat, out=out)) if exchange in ("rccl", "ipc") else \
         (lambda: sw.wavelet_features(X, k=K, s=s_heat))

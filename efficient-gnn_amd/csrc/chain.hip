@@ -515,7 +515,8 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.n_act = p->n_act;
   a.K = K;
   a.P = p->P;
-  a.stride = L->tune.chain_xcd ? 8 : 1;
+  // one XCD holds 32 workers (one per CU): more would wait for residency that never comes
+  a.stride = (L->tune.chain_xcd && p->P <= 32) ? 8 : 1;
   a.ustride = p->ustride;
   a.ids = p->ids;
   a.wcols = p->wcols;

@@ -414,7 +414,19 @@ struct wg_dist_s {
     float* sendbuf = take(snd);
     int rc = WG_OK;
     if (sig) rc = ipc_wait_only(st);
-    if (!rc) rc = launch_permute_pad(L, F, Fp, X0, A[0], st);
+    // unweighted (u = b * dinv exchanged) Clenshaw chains at an unpadded width: one pass writes X0
+    // (internal order), u_0 = X0 * dinv into slot 0, the closed-form rows' S / H straight to the
+    // caller's rows and zeros to their u rows in both slots; the last step writes S / H of the
+    // active rows to the caller's rows (no finalize pass) -- as wg_wavelet_features
+    const int useu_f = (L->unit && L->values_null && L->tune.uscale && L->tune.hot == 0) ? 1 : 0;
+    const bool fused = !lp && L->tune.clenshaw && K >= 1 && useu_f && Fp == F && L->tune.fuse_finalize && S && H &&
+                       step_single_tile(L, F, {A[0], A[1], S, H});
+    float* x0f = fused ? take(own) : nullptr;
+    double coef_f = 0.0;  // closed-form rows: S = X0 * sum_k (-1)^k c_k (as wg_wavelet_features)
+    for (int32_t k = 0; k <= K; ++k) coef_f += ((k & 1) ? -1.0 : 1.0) * std::exp(-s * (double)k);
+    if (!rc)
+      rc = fused ? launch_permute_in_closed(L, F, X0, x0f, coef_f, S, H, A[0], st, A[1])
+                 : launch_permute_pad(L, F, Fp, X0, A[0], st);
     if (!rc && K == 0)
       rc = hipMemcpyAsync(sint, A[0], sizeof(float) * n_own * Fp, hipMemcpyDeviceToDevice, st) == hipSuccess
                ? WG_OK
@@ -423,8 +435,9 @@ struct wg_dist_s {
       // b_K = c_K X0 implicit; b_k = c_k X0 + 2 L_hat b_{k+1} - b_{k+2} written over b_{k+2} (own rows)
       // in the slot the forward chain would write; S = c_0 X0 + L_hat b_1 - b_2 (capi.hip).
       // Phase j = 1..K exchanges slot (j-1)&1, exactly as the forward chain's step j.
-      float* x0 = take(own);
-      if (!rc && hipMemcpyAsync(x0, A[0], sizeof(float) * n_own * Fp, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      float* x0 = fused ? x0f : take(own);
+      if (!rc && !fused &&
+          hipMemcpyAsync(x0, A[0], sizeof(float) * n_own * Fp, hipMemcpyDeviceToDevice, st) != hipSuccess)
         rc = fail(WG_ERR_HIP, "wg_dist: copy X0");
       std::vector<double> c(K + 1);
       for (int32_t k = 0; k <= K; ++k) c[k] = std::exp(-s * (double)k);
@@ -439,11 +452,11 @@ struct wg_dist_s {
       // halo rows a rank receives in phase 1 must be in the format it gathers (a
       // shard that declined its plan must not send unscaled rows to one that took it).
       const bool u0 = useu && K >= 1;
-      if (!rc && u0) rc = launch_scale_rows(L, n_own, Fp, x0, A[0], st);
+      if (!rc && u0 && !fused) rc = launch_scale_rows(L, n_own, Fp, x0, A[0], st);
       // the closed-form own rows [n_active, n_own) are never written by the steps (active rows only)
       // nor gathered, but a hybrid step's dense tile stages whole 32-row column tiles: keep them
       // zero in the other slot (finite u_0 in A[0]) so that 0 x stale never enters an MFMA sum
-      if (!rc && L->n_active < n_own &&
+      if (!rc && !fused && L->n_active < n_own &&
           hipMemsetAsync(A[1] + L->n_active * Fp, 0, sizeof(float) * (n_own - L->n_active) * Fp, st) != hipSuccess)
         rc = fail(WG_ERR_HIP, "wg_dist: zero the closed-form rows");
       for (int32_t j = 1; j <= K && !rc; ++j) {
@@ -459,16 +472,18 @@ struct wg_dist_s {
         rc = exchange(cur, sendbuf, Fp, st, (j - 1) & 1);
         // only the active rows: purely isolated own rows (no entries, w = 0; relabelled to the end
         // of the shard by the prologue) are never gathered by any rank and have T_k = (-1)^k X0, so
-        // their S is written in closed form by the finalize below (WATS.py:55, -1 diagonal)
+        // their S is written in closed form by the fused permute-in or the finalize below (WATS.py:55,
+        // -1 diagonal)
         if (!rc)
           rc = launch_step(L, 2, Fp, cur, prev_stored ? A[j & 1] : nullptr, k == 0 ? nullptr : A[j & 1],
-                           k == 0 ? sint : nullptr, nullptr, 1.0, 0.0, st, /*active_only=*/true, nullptr, &cl);
+                           k == 0 ? sint : nullptr, (k == 0 && fused) ? H : nullptr, 1.0, 0.0, st,
+                           /*active_only=*/true, (k == 0 && fused) ? S : nullptr, &cl);
       }
-      if (!rc) {
+      if (!rc && sig) rc = ipc_signal(st);  // phase K
+      if (!rc && !fused) {
         double coef = 0.0;  // closed-form rows: S = X0 * sum_k (-1)^k c_k (as wg_wavelet_features)
         for (int32_t k = 0; k <= K; ++k) coef += ((k & 1) ? -1.0 : 1.0) * c[k];
-        if (sig) rc = ipc_signal(st);  // phase K
-        if (!rc) rc = launch_finalize(L, F, sint, x0, coef, S, H, st, Fp);
+        rc = launch_finalize(L, F, sint, x0, coef, S, H, st, Fp);
       }
       return rc;
     } else {

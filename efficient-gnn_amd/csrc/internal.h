@@ -225,7 +225,7 @@ struct Tuning {
                              // 0 = auto: one when its ids and two u buffers fit LDS (no exchange), else 64
                              // (PubMed-size K=16: 8 / 16 / 32 / 64 workers 187 / 139 / 119 / 113 us per chain,
                              // profiles/r03/s13_chain1_worker_sweep.log)
-  int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works)
+  int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works; P <= 32)
   int32_t chain_fault = 0;   // chain.hip fault injection (tests of the timeout path): worker 0 does not publish
                              // phase chain_fault; the launch's S / H come out NaN and the next call fails
   int32_t gather4 = 21;      // value-free VEC-4 steps on the padded CSR (step.hip build_pcol / accumulate_u4):
@@ -373,8 +373,10 @@ int padded_features(const wg_laplacian_s* L, int64_t F);
 // launch_step would run F columns as one tile (the condition for a fused H / finalize)
 bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const void*> ptrs);
 // permute-in that also writes the closed-form rows' S and H in the caller's order
+// u: also u_0 = X0 * dinv of the active rows (or nullptr); zero (a row shard's second exchange
+// slot): the closed rows' u rows zeroed in u and in zero
 int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
-                             float* H, float* u, hipStream_t stream);  // u: also u_0 = X0 * dinv (or nullptr)
+                             float* H, float* u, hipStream_t stream, float* zero = nullptr);
 // caller rows (stride F) -> internal rows (stride Fp), pad columns zeroed
 int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);

@@ -397,8 +397,12 @@ int build_operator(wg_laplacian_s* L, const int64_t* indptr, const int32_t* indi
   hipLaunchKernelGGL(iota_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, ids);
   WG_LAUNCH_CHECK();
   if (L->reordered) {
-    // closed-form rows only on a whole-graph handle (a shard's rows may be halo rows elsewhere)
-    const int allow_closed = (w_cols == nullptr && !raw) ? 1 : 0;
+    // closed-form rows: purely isolated rows (w_i == 0, no entries in row or column i).  On a row
+    // shard w is the GLOBAL column degree (w_cols, wats_hip.dist's all-reduce): on an unweighted
+    // graph w_i == 0 means no shard's row has an entry in column i, so such an own row is never
+    // a halo row elsewhere and can be finished in closed form too; with
+    // values a zero sum need not mean no entries, so weighted shards keep every row
+    const int allow_closed = (!raw && (w_cols == nullptr || values == nullptr)) ? 1 : 0;
     hipLaunchKernelGGL(sort_key_kernel, dim3(nb_rows), dim3(256), 0, stream, n_rows, len, colcnt, iso_col, allow_closed,
                        key);
     WG_LAUNCH_CHECK();

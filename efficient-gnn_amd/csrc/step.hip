@@ -385,7 +385,8 @@ __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, in
                                                                    float* __restrict__ dst, int64_t closed_from,
                                                                    double coef, float* __restrict__ S,
                                                                    float* __restrict__ H, const double* __restrict__ dinv,
-                                                                   float* __restrict__ u) {
+                                                                   float* __restrict__ u, int64_t u_rows,
+                                                                   float* __restrict__ zero) {
   const int lane = threadIdx.x & 63;
   const int G = 64 / LF;
   const int sg = lane / LF;
@@ -427,6 +428,11 @@ __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, in
   for (int j = 0; j < VEC; ++j) h[j] = sv[j] / den;
   store_vec<VEC>(S + r * F + fs * VEC, sv);
   store_vec<VEC>(H + r * F + fs * VEC, h);
+  // a row shard's exchange slots (dist.hip): the closed rows' u rows zero in both slots (the
+  // hybrid step's dense tiles stage whole 32-row column tiles: 0 x stale must not enter a sum)
+  const double z[VEC] = {};
+  if (u && row < u_rows) store_vec<VEC>(u + row * F + fs * VEC, z);
+  if (zero) store_vec<VEC>(zero + row * F + fs * VEC, z);
 }
 
 // caller rows (stride F) -> internal rows (stride Fp > F), the Fp - F pad columns zeroed
@@ -1078,23 +1084,23 @@ bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const 
 }
 
 int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
-                             float* H, float* u, hipStream_t stream) {
+                             float* H, float* u, hipStream_t stream, float* zero) {
   const int64_t n = L->n_rows;
   if (n == 0) return WG_OK;
-  const int vec = pick_vec(F, {src, dst, S, H});
+  const int vec = pick_vec(F, {src, dst, S, H, u, zero});
   if (F > 64 * vec) return fail(WG_ERR_INVALID, "permute_in_closed: F too wide");
   const int LF = (int)(F / vec);
   const int G = 64 / LF;
   const dim3 grid((unsigned)ceil_div(n, 4 * G));
   if (vec == 4)
     hipLaunchKernelGGL(permute_in_closed_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
-                       L->n_active, coef, S, H, L->dinv, u);
+                       L->n_active, coef, S, H, L->dinv, u, zero ? n : 0, zero);
   else if (vec == 2)
     hipLaunchKernelGGL(permute_in_closed_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
-                       L->n_active, coef, S, H, L->dinv, u);
+                       L->n_active, coef, S, H, L->dinv, u, zero ? n : 0, zero);
   else
     hipLaunchKernelGGL(permute_in_closed_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
-                       L->n_active, coef, S, H, L->dinv, u);
+                       L->n_active, coef, S, H, L->dinv, u, zero ? n : 0, zero);
   WG_LAUNCH_CHECK();
   return WG_OK;
 }

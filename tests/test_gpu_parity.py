@@ -741,6 +741,7 @@ def test_chain_under_torch_graph_capture():
 @pytest.mark.parametrize("n,nnz,K,knobs", [(19717, 88648, 16, {}), (2708, 10556, 8, {}), (2708, 10556, 3, {"chain_wg": 1}),
                                            (19717, 88648, 1, {}), (19717, 88648, 2, {"chain_wg": 3}),
                                            (19717, 88648, 32, {"chain_wg": 16, "chain_xcd": 1}),
+                                           (19717, 88648, 16, {"chain_xcd": 1}),
                                            (6000, 150000, 16, {"chain_wg": 5})])
 def test_chain1_vs_oracle(n, nnz, K, knobs):
     """F = 1 small graphs run the whole chain in one launch (P workers, a
