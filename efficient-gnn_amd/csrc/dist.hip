@@ -602,7 +602,7 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   const GraphKey key{X0, S, H, F, K, s, D->L->tune_gen};
   if (!(key == D->key)) {
     if (D->exec) {
-      WG_HIP_TRY(hipStreamSynchronize(D->cap));
+      WG_HIP_TRY(hipDeviceSynchronize());  // its last replay ran on some caller stream
       (void)hipGraphExecDestroy(D->exec);
       D->exec = nullptr;
     }
@@ -613,9 +613,9 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   // these arguments (it builds the kernel plans and the workspace).  Either way the chain
   // runs on the handle's own non-blocking stream (cap), joined to the caller's: on the legacy
   // null stream the step kernels would wait for every blocking stream's work.
-  WG_HIP_TRY(hipEventRecord(D->fork, st));
-  WG_HIP_TRY(hipStreamWaitEvent(D->cap, D->fork, 0));
   if (!D->use_graph || D->L->prof || D->warm == 0) {
+    WG_HIP_TRY(hipEventRecord(D->fork, st));
+    WG_HIP_TRY(hipStreamWaitEvent(D->cap, D->fork, 0));
     const int rc = D->chain(X0, F, K, s, S, H, D->cap);
     if (!rc) ++D->warm;
     WG_HIP_TRY(hipEventRecord(D->join, D->cap));
@@ -624,6 +624,8 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   }
   if (!D->exec) {
     hipGraph_t g = nullptr;
+    WG_HIP_TRY(hipEventRecord(D->fork, st));  // capture on the handle's stream (the caller's may be the null one)
+    WG_HIP_TRY(hipStreamWaitEvent(D->cap, D->fork, 0));
     WG_HIP_TRY(hipStreamBeginCapture(D->cap, hipStreamCaptureModeRelaxed));
     const int rc = D->chain(X0, F, K, s, S, H, D->cap);
     const hipError_t ec = hipStreamEndCapture(D->cap, &g);
@@ -639,9 +641,9 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
       return fail(WG_ERR_HIP, "wg_dist: graph instantiate: %s", hipGetErrorString(ei));
     }
   }
-  WG_HIP_TRY(hipGraphLaunch(D->exec, D->cap));
-  WG_HIP_TRY(hipEventRecord(D->join, D->cap));
-  WG_HIP_TRY(hipStreamWaitEvent(st, D->join, 0));
+  // the replay goes straight into the caller's stream: a fork / join through the handle's stream
+  // per call left ~25-30 us of idle GPU between back-to-back chains (r04 s35 kernel trace)
+  WG_HIP_TRY(hipGraphLaunch(D->exec, st));
   return WG_OK;
 }
 
