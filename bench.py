@@ -355,7 +355,8 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     kernel = lds_kernel_name(lds_info) + " (rank 0 shard)"
     tiles_plan = [ln for ln in sw.L.describe(F).splitlines() if ln.startswith("tiles:")]
     if tiles_plan:   # the hybrid step: dense blocks on MFMA + the tail on the step kernel
-        kernel = "hybrid step: cheb_tiles_kernel + cheb_step_kernel over the tail (rank 0 shard)"
+        kernel = ("hybrid step: cheb_tiles_kernel + tiles_combine_kernel + the tail on the step kernel "
+                  "(cheb_team4_kernel; rank 0 shard)")
     avg_ms = prof["step_ms"]
     sw.close()
     del sw

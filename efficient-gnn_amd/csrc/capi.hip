@@ -217,6 +217,10 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.team = (int32_t)value;
     return WG_OK;  // launch-time choice (the wave table is built with the plan on first use)
 
+  } else if (!strcmp(key, "team_tail")) {
+    if (value < 0) return fail(WG_ERR_INVALID, "team_tail must be >= 0");
+    L->tune.team_tail = value;
+    return WG_OK;  // launch-time choice (each plan keeps its own wave table)
   } else if (!strcmp(key, "team_order")) {
     if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
     L->tune.team_order = (int32_t)value;

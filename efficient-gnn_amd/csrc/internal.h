@@ -234,6 +234,7 @@ struct Tuning {
   int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 .. 13:
                              // register-budget / turn-size variants (team.hip launch_team4; all time the same)
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
+  int64_t team_tail = 8 << 20;  // the hybrid step's tail on the team kernel up to this many entries
   int32_t team_order = -1;   // team.hip: wave dispatch order (0 longest rows first, 1 reversed, 2 .. 7 mixed;
                              // -1 auto: 2 for plain steps, 0 for the hybrid step's tail)
   int32_t graph = 0;         // wg_wavelet_features: replay the chain as a hipGraph from its 3rd call with the same

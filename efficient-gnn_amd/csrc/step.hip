@@ -929,7 +929,11 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       // padded ids (team.hip; the hybrid step's tail too), or the workgroup kernel on the padded CSR
       // (accumulate_u4 / accumulate_sell); all columns in one tile, rows addressable by 24-bit ids
       const bool g4 = vec == 4 && a.uin && F == fw && gather4_applies(L, F);
-      if (g4 && L->tune.team) {
+      // the hybrid step's tail on independent waves up to team_tail entries: larger tails keep the
+      // workgroup kernel and its tiered plan (Reddit-size F = 41, width 48: 1 / 2 / 4 / 8-way shards
+      // 798 / 411 / 224 / 133 us per step with the team tail vs 719 / 367 / 233 / 145; r04 s38)
+      const bool team_here = L->tune.team && (!hyb || L->nnz - hyb->dense_nnz <= L->tune.team_tail);
+      if (g4 && team_here) {
         if (!plan->team.wd)
           if (int rc2 = build_team_waves(L, plan->row1, LF, L->tune.team_iter, hyb ? hyb->tcol : L->col,
                                          hyb ? hyb->tsplit : nullptr,
