@@ -88,7 +88,8 @@ def parse():
                     help="seconds the extras may take before the line is printed without the unfinished ones")
     ap.add_argument("--exchange", default="ipc,rccl",
                     help="comma-separated sharded halo exchanges: native chain with grouped ncclSend/ncclRecv "
-                         "(rccl) or the one-sided IPC pull (ipc), or torch all_to_all_single per step (nccl); the "
+                         "(rccl), the one-sided IPC pull (ipc), packed blocks copied by peer DMA (sdma), or torch "
+                         "all_to_all_single per step (nccl); the "
                          "first is the headline's (N > 1) and the extras'; the others are timed for the first "
                          "sharded config only, as 'sharded_<config>_<exchange>'")
     ap.add_argument("--pick-exchange", type=int, default=1,
@@ -285,14 +286,14 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         g.manual_seed(1 + rank)
         X = torch.randn(r1 - r0, F, generator=g, device=device)
     out = (torch.empty(r1 - r0, F, device=device), torch.empty(r1 - r0, F, device=device))
-    if exchange in ("rccl", "ipc") and sw._dist is not None:
+    if exchange in ("rccl", "ipc", "sdma") and sw._dist is not None:
         # the signal already in the chain's input buffer (as graph_wavelet_features reads the
         # caller's X0 in place): no per-chain copy into it
         xb = sw._buf("X", r1 - r0, X.shape[1] if X.dim() == 2 else 1)
         xb.copy_(X.reshape(xb.shape))
         X = xb
     _log(f"sharded {config} ({exchange}): shard ready ({r1 - r0} rows, {sw.plan.n_halo} halo rows); warmup")
-    run = (lambda: sw.wavelet_features(X, k=K, s=s_heat, out=out)) if exchange in ("rccl", "ipc") else \
+    run = (lambda: sw.wavelet_features(X, k=K, s=s_heat, out=out)) if exchange in ("rccl", "ipc", "sdma") else \
         (lambda: sw.wavelet_features(X, k=K, s=s_heat))
     for i in range(max(2, warmup)):   # the native chain is captured into a hipGraph on its 2nd call
         run()
@@ -380,6 +381,9 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                                + {"rccl": "(native: grouped ncclSend/ncclRecv, chain replayed as a hipGraph)",
                                   "ipc": "(native: one-sided pull from IPC-mapped peer memory, flag-ordered "
                                          "phases, chain replayed as a hipGraph)",
+                                  "sdma": "(native: owners pack, receivers copy the packed blocks from "
+                                          "IPC-mapped peer memory by hipMemcpyAsync on a copy stream, "
+                                          "flag-ordered phases, chain replayed as a hipGraph)",
                                   "nccl": "(torch all_to_all_single, RCCL)",
                                   "host": "(torch all_to_all_single on host copies, gloo)"}[exchange]
                                + f"; K={K} F={F}",

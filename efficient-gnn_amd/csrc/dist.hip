@@ -241,6 +241,16 @@ struct wg_dist_s {
   std::vector<void*> peer_region;     // IPC-mapped, nullptr for self
   int64_t** peer_flags = nullptr;     // device array [world]
   IpcPull pull{};
+  // exchange mode "sdma" (wg_dist_ipc_sdma, after wg_dist_ipc_connect): each rank packs the rows
+  // its peers asked for into one of two send buffers of its region; the receiver copies each
+  // owner's packed block into its halo rows with hipMemcpyAsync on a copy stream (DMA engines
+  // on a multi-GPU node: no CU time for the transfer), behind the same phase flags
+  bool sdma = false;
+  hipStream_t copy = nullptr;
+  hipEvent_t cev[2] = {nullptr, nullptr};
+  int64_t send_base = 0, send_floats = 0;  // mine: [send 0][send 1] at region + send_base
+  std::vector<const float*> peer_send;     // peer q's send buffer 0 (mapped); buffer 1 at + peer_send_floats[q]
+  std::vector<int64_t> peer_send_floats, peer_send_off;  // and the row where q packed my block
 
   ~wg_dist_s() {
     if (exec) (void)hipGraphExecDestroy(exec);
@@ -251,6 +261,9 @@ struct wg_dist_s {
                     (void*)peer_flags})
       (void)hipFree(q);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : cev)
+      if (e) (void)hipEventDestroy(e);
+    if (copy) (void)hipStreamDestroy(copy);
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
     if (cap) (void)hipStreamDestroy(cap);
@@ -308,6 +321,32 @@ struct wg_dist_s {
 
   int transfer(float* ext, float* sendbuf, int64_t F, hipStream_t st, int slot) {
     if (ipc && world == 1) return WG_OK;  // no peers: nothing to wait for or pull
+    if (ipc && sdma) {
+      if (int rc = mark(st, true)) return rc;
+      // owner: this phase's rows for every peer, packed in the peers' halo order, then the
+      // phase signalled (ipc_signal_kernel writes back every XCD's L2 before the flags)
+      float* sb = region + send_base + slot * send_floats;
+      if (n_send > 0) {
+        launch_pack(n_send, F, send_rows, ext, sb, st);
+        WG_LAUNCH_CHECK();
+      }
+      if (int rc = ipc_signal(st)) return rc;
+      // receiver, on the copy stream: wait for every peer's signal of this phase, then one copy
+      // per owner of its packed block into this rank's halo rows; the step waits for the copies
+      WG_HIP_TRY(hipEventRecord(cev[0], st));
+      WG_HIP_TRY(hipStreamWaitEvent(copy, cev[0], 0));
+      hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, copy, pull, 0);
+      WG_LAUNCH_CHECK();
+      for (int q = 0; q < world; ++q) {
+        if (q == rank || recv_cnt[q] == 0) continue;
+        const float* from = peer_send[q] + slot * peer_send_floats[q] + peer_send_off[q] * F;
+        WG_HIP_TRY(hipMemcpyAsync(ext + (n_own + recv_off[q]) * F, from, sizeof(float) * recv_cnt[q] * F,
+                                  hipMemcpyDeviceToDevice, copy));
+      }
+      WG_HIP_TRY(hipEventRecord(cev[1], copy));
+      WG_HIP_TRY(hipStreamWaitEvent(st, cev[1], 0));
+      return mark(st, false);
+    }
     if (ipc) {
       if (int rc = mark(st, true)) return rc;
       // one spinning workgroup signals and waits (ranks sharing a GPU in tests must not
@@ -658,7 +697,10 @@ int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
   if (lp) ulen = lp->u_floats();
   D->F_max = F_max;
   D->slot_floats = (std::max<int64_t>(D->n_cols * padded_features(D->L, F_max), ulen) + 63) / 64 * 64;
-  const size_t bytes = sizeof(float) * 2 * D->slot_floats + sizeof(int64_t) * D->world;
+  // [slot 0][slot 1][flags: world int64][send 0][send 1] (the send buffers: exchange mode "sdma")
+  D->send_base = (2 * D->slot_floats + 2 * (int64_t)D->world + 63) / 64 * 64;
+  D->send_floats = (std::max<int64_t>(D->n_send, 1) * padded_features(D->L, F_max) + 63) / 64 * 64;
+  const size_t bytes = sizeof(float) * (D->send_base + 2 * D->send_floats);
   if (int rc = dmalloc(reinterpret_cast<char**>(&D->region), bytes)) return rc;
   if (int rc = dmalloc(&D->count, 1)) return rc;
   if (int rc = dmalloc(&D->err, 1)) return rc;
@@ -679,6 +721,8 @@ int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob) {
   std::memset(out, 0, 128);
   std::memcpy(out, &h, sizeof(h));
   std::memcpy(out + 64, &D->slot_floats, sizeof(int64_t));
+  std::memcpy(out + 72, &D->send_base, sizeof(int64_t));
+  std::memcpy(out + 80, &D->send_floats, sizeof(int64_t));
   WG_HIP_TRY(hipDeviceSynchronize());
   return WG_OK;
 }
@@ -689,6 +733,8 @@ int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src)
   if (D->ipc || !D->peer_region.empty()) return fail(WG_ERR_INVALID, "wg_dist_ipc_connect: already connected");
   const char* b = static_cast<const char*>(blobs);
   D->peer_region.assign(D->world, nullptr);
+  D->peer_send.assign(D->world, nullptr);
+  D->peer_send_floats.assign(D->world, 0);
   std::vector<int64_t*> pf(D->world, nullptr);
   IpcPull p{};
   for (int q = 0; q < D->world; ++q) {
@@ -696,6 +742,9 @@ int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src)
     int64_t sf = 0;
     std::memcpy(&h, b + 128 * q, sizeof(h));
     std::memcpy(&sf, b + 128 * q + 64, sizeof(int64_t));
+    int64_t sbase = 0, sfl = 0;
+    std::memcpy(&sbase, b + 128 * q + 72, sizeof(int64_t));
+    std::memcpy(&sfl, b + 128 * q + 80, sizeof(int64_t));
     float* base = D->region;
     if (q != D->rank) {
       void* mp = nullptr;
@@ -705,6 +754,8 @@ int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src)
     }
     p.slot_base[q] = base;
     p.slot_floats[q] = sf;
+    D->peer_send[q] = base + sbase;
+    D->peer_send_floats[q] = sfl;
     pf[q] = reinterpret_cast<int64_t*>(base + 2 * sf);
   }
   if (int rc = dmalloc(&D->peer_flags, (size_t)D->world)) return rc;
@@ -729,6 +780,28 @@ int wg_dist_ipc_connect(wg_dist_t D, const void* blobs, const int32_t* halo_src)
   return WG_OK;
 }
 
+int wg_dist_ipc_sdma(wg_dist_t D, const int64_t* peer_send_off) {
+  if (!D || !peer_send_off) return fail(WG_ERR_INVALID, "wg_dist_ipc_sdma: NULL argument");
+  if (!D->ipc) return fail(WG_ERR_INVALID, "wg_dist_ipc_sdma: call wg_dist_ipc_connect first");
+  for (int q = 0; q < D->world; ++q)
+    if (q != D->rank && D->recv_cnt[q] > 0 &&
+        (peer_send_off[q] < 0 ||
+         (peer_send_off[q] + D->recv_cnt[q]) * padded_features(D->L, D->F_max) > D->peer_send_floats[q]))
+      return fail(WG_ERR_INVALID, "wg_dist_ipc_sdma: rank %d's block for this rank lies outside its send buffer", q);
+  WG_HIP_TRY(hipDeviceSynchronize());
+  if (!D->copy) WG_HIP_TRY(hipStreamCreateWithFlags(&D->copy, hipStreamNonBlocking));
+  for (hipEvent_t& e : D->cev)
+    if (!e) WG_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  D->peer_send_off.assign(peer_send_off, peer_send_off + D->world);
+  D->sdma = true;
+  if (D->exec) {  // a chain captured with the pull exchange is not replayed
+    (void)hipGraphExecDestroy(D->exec);
+    D->exec = nullptr;
+  }
+  D->warm = 0;
+  return WG_OK;
+}
+
 int wg_dist_status(wg_dist_t D, int32_t* timed_out) {
   if (!D || !timed_out) return fail(WG_ERR_INVALID, "wg_dist_status: NULL argument");
   *timed_out = 0;
@@ -745,7 +818,7 @@ int wg_dist_info(wg_dist_t D, int64_t* out) {
   out[2] = D->n_halo;
   out[3] = D->n_send;
   out[4] = D->world;
-  out[5] = D->ipc ? 1 : (D->comm ? 2 : 0);
+  out[5] = D->ipc ? (D->sdma ? 3 : 1) : (D->comm ? 2 : 0);
   out[6] = D->exec ? 1 : 0;
   out[7] = 1;  // halo tiers
   return WG_OK;

@@ -87,6 +87,7 @@ SIGNATURES = {
     "wg_dist_profile_collect": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64)]),
     "wg_dist_ipc_local": (ctypes.c_int, [c_vp, c_i64, c_vp]),
     "wg_dist_ipc_connect": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "wg_dist_ipc_sdma": (ctypes.c_int, [c_vp, c_vp]),
     "wg_dist_status": (ctypes.c_int, [c_vp, ctypes.POINTER(c_i32)]),
     "wg_chain_status": (ctypes.c_int, [c_vp, ctypes.POINTER(c_i32)]),
 }

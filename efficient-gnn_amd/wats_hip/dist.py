@@ -243,6 +243,10 @@ class ShardedWavelet:
     ``exchange="ipc"``: the same native chain with a one-sided exchange: the
     ranks' vectors mapped into each other by IPC, halo rows pulled straight
     from the owners' memory, phases ordered by flags (``wg_dist_ipc_*``).
+    ``exchange="sdma"``: the same mapping, but each owner packs the rows its
+    peers asked for and the receivers copy the packed blocks with peer DMA
+    (``hipMemcpyAsync`` on a copy stream, ``wg_dist_ipc_sdma``): no CU time
+    for the transfer itself.
     ``exchange="nccl"``: the same exchange from Python, one
     ``torch.distributed.all_to_all_single`` per step (RCCL/xGMI).
     ``exchange="host"``: that collective on host copies (gloo) -- lets several
@@ -297,14 +301,14 @@ class ShardedWavelet:
         self._dist = None
         if exchange == "rccl":
             self._dist = self._create_native()
-        elif exchange == "ipc":
+        elif exchange in ("ipc", "sdma"):
             # the shared region is sized for max_features columns (large IPC
             # mappings are slow to set up: keep it to what the chain uses); a
             # call with more columns rebuilds it (collective, like the call)
             self._ipc_F = int(max_features)
             self._dist = self._create_ipc(self._ipc_F)
         elif exchange not in ("nccl", "host"):
-            raise ValueError(f"exchange must be 'rccl', 'ipc', 'nccl' or 'host', not {exchange!r}")
+            raise ValueError(f"exchange must be 'rccl', 'ipc', 'sdma', 'nccl' or 'host', not {exchange!r}")
         _trace("exchange ready")
 
     def _create_native(self):
@@ -372,6 +376,21 @@ class ShardedWavelet:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
             if not int(ok.item()) and err is None:
                 err = RuntimeError("wats_hip: IPC exchange setup failed on another rank")
+        if err is None and self.exchange == "sdma":
+            # where each owner packed my block in its send buffer: its send offset for me
+            offs_q = (exchange_int_lists([[int(offs[q])] for q in range(p.world)], self.group) if p.world > 1
+                      else [np.array([0])])
+            pso = np.ascontiguousarray([int(x[0]) for x in offs_q], dtype=np.int64)
+            with torch.cuda.device(self.device):
+                try:
+                    check(lib.wg_dist_ipc_sdma(h, pso.ctypes.data), "dist_ipc_sdma")
+                except Exception as exc:  # noqa: BLE001 -- made collective below
+                    err = exc
+            if p.world > 1:
+                ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=_device_for(self.group))
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
+                if not int(ok.item()) and err is None:
+                    err = RuntimeError("wats_hip: SDMA exchange setup failed on another rank")
         if err is not None:
             lib.wg_dist_destroy(h)
             raise err
@@ -454,7 +473,7 @@ class ShardedWavelet:
         keys = ("overlap", "n_own", "n_halo", "n_send", "world", "exchange", "captured", "tiers")
         d = dict(zip(keys, [int(v) for v in out]))
         del d["overlap"], d["tiers"]
-        d["exchange"] = {1: "ipc", 2: "rccl"}.get(d["exchange"], "none")
+        d["exchange"] = {1: "ipc", 2: "rccl", 3: "sdma"}.get(d["exchange"], "none")
         return d
 
     # -------------------------------------------------------------- chain
@@ -526,7 +545,7 @@ class ShardedWavelet:
         F_in = X0_local.shape[-1] if X0_local.dim() == 2 else 1
         X = X0_local.to(self.device, torch.float32).reshape(p.n_own, F_in).contiguous()   # (0, F) on an empty shard
         F = X.shape[1]
-        if self.exchange == "ipc" and F > self._ipc_F:
+        if self.exchange in ("ipc", "sdma") and F > self._ipc_F:
             self.close()
             self._ipc_F = F
             self._dist = self._create_ipc(F)

@@ -334,6 +334,16 @@ int wg_dist_profile_collect(wg_dist_t D, double* exchange_ms_host, int64_t* coun
 int wg_dist_ipc_local(wg_dist_t D, int64_t F_max, void* blob_out /* 128 bytes, host */);
 int wg_dist_ipc_connect(wg_dist_t D, const void* blobs_host /* world x 128 bytes */,
                         const int32_t* halo_src);
+/* Exchange mode "sdma" (after wg_dist_ipc_connect): every phase the owner packs the rows each
+ * peer asked for into one of two send buffers in its IPC region (in the peer's halo order) and
+ * signals the phase; the receiver waits for the signals on a copy stream and copies each
+ * owner's block into its halo rows with hipMemcpyAsync (peer DMA: the transfer takes no CU time
+ * on a multi-GPU node), the step waiting on the copies.  peer_send_off[q] = the row of rank q's
+ * send buffer where q packed this rank's block (q's send offset for this rank; collective setup,
+ * wats_hip.dist).  Replaces the pull exchange of the same handle.
+ * (reference: the halo exchange of the row-sharded Chebyshev step, WATS.py:35-36 sharded per
+ * SURVEY.md 8(e); no reference interface -- the reference has no multi-GPU path) */
+int wg_dist_ipc_sdma(wg_dist_t D, const int64_t* peer_send_off /* world, host */);
 int wg_dist_status(wg_dist_t D, int32_t* timed_out_host);
 
 /* -------------------------------------------------------------------------

@@ -157,14 +157,14 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiles=
         q_path = "u" if (F == 1 and sw.u_len() > 0) else "t"
         rng = np.random.default_rng(0)
         X = rng.standard_normal((g.n, F)).astype(np.float32)
-        runs = 3 if exchange == "ipc" else 1   # ipc: eager, captured, replayed
+        runs = 3 if exchange in ("ipc", "sdma") else 1   # native: eager, captured, replayed
         outs = [sw.wavelet_features(torch.from_numpy(X[r0:r1]), k=K, s=0.8) for _ in range(runs)]
         H, S = outs[0]
         same = all(torch.equal(o[1], S) and torch.equal(o[0], H) for o in outs)
-        if exchange == "ipc":
+        if exchange in ("ipc", "sdma"):
             if tiles:
                 assert ("tiles:" in sw.L.describe(F + (-F) % 16)) == hybrid, sw.L.describe(F)
-            assert sw.info()["exchange"] == "ipc"
+            assert sw.info()["exchange"] == exchange
             sw.check_exchange()
             sw.close()
         q.put((rank, S.cpu().numpy(), H.cpu().numpy(), q_path, same))
@@ -184,11 +184,16 @@ def _gpu_worker(rank, world, port, kind, K, F, q, lds=2, exchange="host", tiles=
     (2, "weighted", 4, 2, "ipc", 0), (3, "weighted", 1, 2, "ipc", 0), (2, "rmat", 1, 4, "ipc", 0), (2, "rmat", 1, 4, "host", 0),
     (4, "rmat", 1, 2, "ipc", 0), (3, "rmat", 8, 2, "host", 0), (8, "rmat", 40, 2, "ipc", 0), (8, "rmat", 1, 2, "ipc", 0),
     (8, "weighted", 4, 2, "ipc", 0), (2, "rmat", 48, 2, "ipc", 1), (3, "rmat", 41, 2, "ipc", 1),
-    (4, "rmat", 48, 2, "ipc", 1), (3, "rmat", 48, 2, "ipc", 2), (2, "rmat", 41, 2, "ipc", 2)])
+    (4, "rmat", 48, 2, "ipc", 1), (3, "rmat", 48, 2, "ipc", 2), (2, "rmat", 41, 2, "ipc", 2),
+    (2, "rmat", 1, 2, "sdma", 0), (3, "rmat", 40, 2, "sdma", 0), (4, "weighted", 4, 2, "sdma", 0),
+    (8, "rmat", 40, 2, "sdma", 0), (8, "rmat", 1, 2, "sdma", 0), (4, "rmat", 48, 2, "sdma", 1),
+    (3, "rmat", 41, 2, "sdma", 2)])
 def test_sharded_chain_gpu_multi_rank(world, kind, F, lds, exchange, tiles):
     """Several ranks on one GPU: the Python exchange over gloo host copies, or
     the native chain with the one-sided IPC exchange (ranks pull from each
-    other's memory; same-device IPC stands in for xGMI peers).  tiles = 1: the
+    other's memory; same-device IPC stands in for xGMI peers), or with the
+    packed-block copies (sdma: hipMemcpyAsync from the owners' IPC-mapped send
+    buffers on a copy stream, behind the same phase flags).  tiles = 1: the
     hybrid step on every shard (dense blocks over [own | halo] columns); tiles = 2:
     on every shard but rank 1's (the ranks disagree on the plan)."""
     if not torch.cuda.is_available():
@@ -412,7 +417,7 @@ def test_native_chain_recaptures_after_tune():
     sw.close()
 
 
-def _empty_shard_worker(rank, world, port, bounds, F, q):
+def _empty_shard_worker(rank, world, port, bounds, F, q, exchange="ipc"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -424,7 +429,7 @@ def _empty_shard_worker(rank, world, port, bounds, F, q):
         r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
         lo, hi = g.indptr[r0], g.indptr[r1]
         sw = ShardedWavelet(g.indptr[r0:r1 + 1] - lo, g.indices[lo:hi], None, g.n, np.asarray(bounds),
-                            exchange="ipc", device="cuda:0", max_features=F)
+                            exchange=exchange, device="cuda:0", max_features=F)
         X = np.random.default_rng(0).standard_normal((g.n, F)).astype(np.float32)
         outs = [sw.wavelet_features(torch.from_numpy(X[r0:r1]), k=5, s=0.8) for _ in range(3)]
         sw.check_exchange()
@@ -435,8 +440,8 @@ def _empty_shard_worker(rank, world, port, bounds, F, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F", [1, 4])
-def test_ipc_chain_with_an_empty_shard(F):
+@pytest.mark.parametrize("F,exchange", [(1, "ipc"), (4, "ipc"), (4, "sdma")])
+def test_ipc_chain_with_an_empty_shard(F, exchange):
     """a rank that owns no rows runs the native chain too (it must
     take part in every exchange phase); before, it took the Python path and
     its peers hung.  Bounds [0, 600, 600, 1100, n]: rank 1 is empty."""
@@ -447,7 +452,7 @@ def test_ipc_chain_with_an_empty_shard(F):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_empty_shard_worker, args=(r, 4, port, bounds, F, q)) for r in range(4)]
+    procs = [ctx.Process(target=_empty_shard_worker, args=(r, 4, port, bounds, F, q, exchange)) for r in range(4)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=170) for _ in range(4)], key=lambda t: t[0])
