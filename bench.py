@@ -86,7 +86,7 @@ def parse():
                     help="N > 1: seconds the row-sharded headline may take before an error line is printed")
     ap.add_argument("--sharded-timeout", type=float, default=420.0,
                     help="seconds the extras may take before the line is printed without the unfinished ones")
-    ap.add_argument("--exchange", default="ipc,rccl",
+    ap.add_argument("--exchange", default="ipc,rccl,sdma",
                     help="comma-separated sharded halo exchanges: native chain with grouped ncclSend/ncclRecv "
                          "(rccl), the one-sided IPC pull (ipc), packed blocks copied by peer DMA (sdma), or torch "
                          "all_to_all_single per step (nccl); the "
