@@ -203,6 +203,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < 0 || value > kChainMaxK) return fail(WG_ERR_INVALID, "chain_fault must be in [0, %d]", kChainMaxK);
     L->tune.chain_fault = (int32_t)value;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "chain_direct")) {
+    L->tune.chain_direct = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "chain_xcd")) {
     L->tune.chain_xcd = value ? 1 : 0;
     return WG_OK;  // launch-time choice

@@ -55,6 +55,10 @@ struct ChainArgs {
   const uint16_t* ids;        // [nnz_act] column ids (row order): the worker's local column ids (P > 1)
   const uint16_t* wcols;      // P > 1: each worker's gathered columns (ascending), concatenated
   const int32_t* wcol_off;    // [P + 1] their offsets
+  const uint16_t* gids;       // [nnz_act] global column ids (direct mode)
+  const uint16_t* bcols;      // direct mode: each worker's back-edge columns (build_chain_plan), concatenated
+  const int32_t* bcol_off;    // [P + 1]
+  int32_t direct;             // tuning key "chain_direct": gathers read the granules (no LDS staging)
   const int4* wdesc;          // [P] {row0, row1, e0, e1}
   const int32_t* wpass;       // [P][kChainWaves + 1] pass offsets of each worker's waves (into passes)
   const int2* passes;         // one wave pass: {first row, rows | log2 team size << 8}
@@ -138,6 +142,51 @@ __device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, const 
   return true;
 }
 
+// a granule wait that gave up: the launch's epoch recorded (once per worker) for the next API call
+__device__ __forceinline__ void chain_fail(const ChainArgs& a, int* s_bad, uint32_t ep) {
+  if (atomicExch(s_bad, 1) == 0) {
+    __hip_atomic_store(a.bar + 2, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.host_flag) __hip_atomic_store(a.host_flag, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// direct mode: u of columns c[0 .. n) for phase j -- u_0 (written before the launch) in phase 1,
+// else the previous phase's granules, all loads in flight at once, re-polled until every tag is
+// `want`; false past the deadline (the values are then NaN)
+__device__ __forceinline__ bool fetch_u(const ChainArgs& a, const uint64_t* gprev, int j, uint32_t want,
+                                        const int (&c)[4], int n, float (&x)[4], uint64_t deadline) {
+  if (j == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < n) x[i] = a.u0[c[i]];
+    return true;
+  }
+  uint64_t v[4];
+  uint32_t pending = (1u << n) - 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < n) v[i] = ld_sc1_u64(gprev + c[i]);
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (((pending >> i) & 1) && (uint32_t)(v[i] >> 32) == want) {
+        x[i] = __uint_as_float((uint32_t)v[i]);
+        pending &= ~(1u << i);
+      }
+    if (!pending) return true;
+    if (wall_clock64() > deadline) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((pending >> i) & 1) x[i] = __int_as_float(0x7fc00000);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((pending >> i) & 1) v[i] = ld_sc1_u64(gprev + c[i]);
+  }
+}
+
 // internal X0 of the active rows, u_0 = X0 * dinv into exchange buffer 0, and the
 // closed-form rows' S = coef * X0, H = S / (|S| + 1e-8) straight to the caller's rows
 __global__ void chain_prologue_kernel(int64_t n, int64_t n_act, const int32_t* __restrict__ perm,
@@ -199,9 +248,12 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
     lrp[i] = a.rowptr[row0 + i] - e0;
   }
   if (tid == 0) lrp[nr] = ne;
-  for (int i = tid; i < ne; i += kChainThreads) id[i] = a.ids[e0 + i];
+  const uint16_t* idsrc = a.direct ? a.gids : a.ids;
+  for (int i = tid; i < ne; i += kChainThreads) id[i] = idsrc[e0 + i];
   for (int i = tid; i < npass; i += kChainThreads) pas[i] = a.passes[pass0 + i];
-  if (a.P == 1) {
+  if (a.direct) {
+    // no LDS copy of u: the gathers read u_0 and then the granules themselves
+  } else if (a.P == 1) {
     for (int i = tid; i < a.n_act; i += kChainThreads) u[i] = a.u0[i];
   } else {
     for (int i = tid; i < nu; i += kChainThreads) {
@@ -226,7 +278,25 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
     const double ck = a.c[k] - (j == 2 ? a.c[K] : 0.0);
     const bool prevs = j >= 3;
     const uint64_t tag = (uint64_t)((ep << 6) | (uint32_t)j) << 32;
-    uint64_t* gnext = a.gbuf + (size_t)(j & 1) * a.ustride;
+    // staging: two granule buffers by phase; direct: four (a worker publishing phase j overwrites
+    // phase j - 4, read by its readers in phase j - 3: every reader is also a producer of this
+    // worker (symmetric graphs) or a back edge it polls, and its phase j - 2 granules, seen before
+    // this worker's barrier of phase j - 1, prove it passed its own barrier after phase j - 3)
+    uint64_t* gnext = a.gbuf + (size_t)(j & (a.direct ? 3 : 1)) * a.ustride;
+    const uint64_t* gprev = a.gbuf + (size_t)((j - 1) & 3) * a.ustride;
+    const uint32_t want = (ep << 6) | (uint32_t)(j - 1);
+    const uint64_t deadline = wall_clock64() + (uint64_t)a.wait_ticks;
+    if (a.direct && j >= 2) {  // back edges: one granule of every worker that reads this one's rows
+      const int b0 = a.bcol_off[w], b1 = a.bcol_off[w + 1];
+      for (int i = b0 + tid; i < b1; i += kChainThreads)
+        while ((uint32_t)(ld_sc1_u64(gprev + a.bcols[i]) >> 32) != want) {
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() > deadline) {
+            chain_fail(a, &s_bad, ep);
+            break;
+          }
+        }
+    }
     for (int pi = pb; pi < pe; ++pi) {
       const int2 P = pas[pi];
       const int lts = P.y >> 8;
@@ -238,7 +308,26 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
         const bool act = team < (P.y & 0xff);
         const int li = row - row0;
         double s = 0.0;
-        if (act) {  // four independent LDS chains per lane (the phase is latency-bound)
+        if (act && a.direct) {  // the same four chains, each term a granule (or u_0) from memory
+          const int b = lrp[li], e = lrp[li + 1];
+          double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+          int q = b + tl;
+          float x[4];
+          for (; q + 3 * TS < e; q += 4 * TS) {
+            const int c4[4] = {id[q], id[q + TS], id[q + 2 * TS], id[q + 3 * TS]};
+            if (!fetch_u(a, gprev, j, want, c4, 4, x, deadline)) chain_fail(a, &s_bad, ep);
+            s += (double)x[0];
+            s1 += (double)x[1];
+            s2 += (double)x[2];
+            s3 += (double)x[3];
+          }
+          for (; q < e; q += TS) {
+            const int c1[4] = {id[q], 0, 0, 0};
+            if (!fetch_u(a, gprev, j, want, c1, 1, x, deadline)) chain_fail(a, &s_bad, ep);
+            s += (double)x[0];
+          }
+          s = (s + s1) + (s2 + s3);
+        } else if (act) {  // four independent LDS chains per lane (the phase is latency-bound)
           const int b = lrp[li], e = lrp[li + 1];
           double s1 = 0.0, s2 = 0.0, s3 = 0.0;
           int q = b + tl;
@@ -283,7 +372,9 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
 #endif
     if (k == 0) break;
     __syncthreads();  // every gather of this phase is done with u
-    if (a.P == 1) {
+    if (a.direct) {
+      // nothing to stage: the next phase's gathers read this phase's granules
+    } else if (a.P == 1) {
       float* t = u;
       u = u2;
       u2 = t;
@@ -364,6 +455,8 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   std::vector<int32_t> wpass;
   std::vector<uint16_t> wcols, lids;  // P > 1: each worker's gathered columns; the entries' local ids
   std::vector<int32_t> wcol_off;
+  std::vector<uint16_t> bcols;        // P > 1: each worker's back-edge columns (direct mode polls them)
+  std::vector<int32_t> bcol_off;
   std::vector<int32_t> local(na, -1);
   size_t lds = 0;
   for (;; P = (P == 1 && L->tune.chain_wg <= 0) ? 64 : 2 * P) {
@@ -373,15 +466,33 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
     wpass.assign((size_t)P * (kChainWaves + 1), 0);
     wcols.clear();
     wcol_off.assign(P + 1, 0);
+    bcols.clear();
+    bcol_off.assign(P + 1, 0);
     lids.assign(ids.begin(), ids.end());
     lds = 0;
     int64_t r = 0;
     bool fits = true;
-    for (int w = 0; w < P && fits; ++w) {
+    // every worker's rows first: a worker's staging list needs its consumers
+    std::vector<int32_t> owner(na, 0);
+    for (int w = 0; w < P; ++w) {
       const int64_t goal = total * (w + 1) / P;
       const int64_t r0 = r;
       while (r < na && (w == P - 1 || rp[r] + kRowCost * r < goal)) ++r;
       wd[w] = int4{(int)r0, (int)r, rp[r0], rp[r]};
+      for (int64_t i = r0; i < r; ++i) owner[i] = w;
+    }
+    // refs[c * P + w]: worker w gathers a row of worker c.  A worker overwrites the granule
+    // buffer of phase j with phase j + 2 once it has staged phase j + 1 from the workers it
+    // reads; a worker c that reads w must have finished reading w's phase j by then, which it
+    // has once it published phase j + 1 -- so w also stages one granule of every worker that
+    // reads it but that it does not read (directed graphs; symmetric ones have none)
+    std::vector<char> refs((size_t)P * P, 0);
+    if (P > 1)
+      for (int w = 0; w < P; ++w)
+        for (int64_t e = wd[w].z; e < wd[w].w; ++e) refs[(size_t)owner[ids[e]] * P + w] = 1;
+    for (int w = 0; w < P && fits; ++w) {
+      const int64_t r0 = wd[w].x;
+      r = wd[w].y;
       std::vector<int2> wps;
       std::vector<int64_t> cost;
       make_passes(rp, r0, r, wps, cost);
@@ -403,6 +514,12 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
       int64_t nu = na;
       if (P > 1) {  // the columns this worker's rows gather, ascending, and their local ids
         std::vector<int32_t> cs(ids.begin() + rp[r0], ids.begin() + rp[r]);
+        for (int c = 0; c < P; ++c)  // back edges: a granule of each reader this worker does not read
+          if (c != w && refs[(size_t)w * P + c] && !refs[(size_t)c * P + w] && wd[c].y > wd[c].x) {
+            cs.push_back(wd[c].x);
+            bcols.push_back((uint16_t)wd[c].x);
+          }
+        bcol_off[w + 1] = (int32_t)bcols.size();
         std::sort(cs.begin(), cs.end());
         cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
         for (size_t i = 0; i < cs.size(); ++i) {
@@ -424,14 +541,18 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   p->lds_bytes = (int32_t)((lds + 15) / 16 * 16);
   p->ustride = (int32_t)((na + 63) / 64 * 64);
   if (wcols.empty()) wcols.push_back(0);
+  if (bcols.empty()) bcols.push_back(0);
   int rc = upload(&p->ids, P == 1 ? ids : lids);
   if (!rc) rc = upload(&p->wcols, wcols);
+  if (!rc) rc = upload(&p->gids, ids);
+  if (!rc) rc = upload(&p->bcols, bcols);
+  if (!rc) rc = upload(&p->bcol_off, bcol_off);
   if (!rc) rc = upload(&p->wcol_off, wcol_off);
   if (!rc) rc = upload(&p->wdesc, wd);
   if (!rc) rc = upload(&p->wpass, wpass);
   if (!rc) rc = upload(&p->passes, passes);
   if (!rc) rc = dmalloc(&p->bar, 4);
-  if (!rc) rc = dmalloc(&p->gbuf, (size_t)2 * p->ustride);
+  if (!rc) rc = dmalloc(&p->gbuf, (size_t)4 * p->ustride);
   if (!rc) rc = dmalloc(&p->u0, (size_t)std::max<int64_t>(na, 1));
   if (!rc) rc = dmalloc(&p->x0, (size_t)std::max<int64_t>(na, 1));
   if (rc) return rc;
@@ -440,7 +561,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   WG_HIP_TRY(hipHostGetDevicePointer((void**)&p->d_host_flag, p->host_flag, 0));
   p->seen = 0;
   WG_HIP_TRY(hipMemset(p->bar, 0, 4 * sizeof(int32_t)));
-  WG_HIP_TRY(hipMemset(p->gbuf, 0, 2 * p->ustride * sizeof(uint64_t)));  // tag 0: never a live phase's
+  WG_HIP_TRY(hipMemset(p->gbuf, 0, 4 * p->ustride * sizeof(uint64_t)));  // tag 0: never a live phase's
   char buf[192];
   snprintf(buf, sizeof(buf), "chain1: one launch per chain, %d workers x %d threads, %lld active rows, %lld nonzeros, "
            "%d wave passes, LDS %d B per worker\n", P, kChainThreads, (long long)na, (long long)nnz,
@@ -452,7 +573,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
 }  // namespace
 
 void ChainPlan::release() {
-  for (void* q : {(void*)ids, (void*)wcols, (void*)wcol_off, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar,
+  for (void* q : {(void*)ids, (void*)wcols, (void*)wcol_off, (void*)gids, (void*)bcols, (void*)bcol_off, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar,
                   (void*)gbuf, (void*)u0, (void*)x0})
     (void)hipFree(q);
   if (host_flag) (void)hipHostFree(host_flag);
@@ -521,6 +642,10 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.ids = p->ids;
   a.wcols = p->wcols;
   a.wcol_off = p->wcol_off;
+  a.gids = p->gids;
+  a.bcols = p->bcols;
+  a.bcol_off = p->bcol_off;
+  a.direct = (L->tune.chain_direct && p->P > 1) ? 1 : 0;
   a.wdesc = p->wdesc;
   a.wpass = p->wpass;
   a.passes = p->passes;

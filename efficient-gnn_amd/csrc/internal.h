@@ -225,6 +225,7 @@ struct Tuning {
                              // 0 = auto: one when its ids and two u buffers fit LDS (no exchange), else 64
                              // (PubMed-size K=16: 8 / 16 / 32 / 64 workers 187 / 139 / 119 / 113 us per chain,
                              // profiles/r03/s13_chain1_worker_sweep.log)
+  int32_t chain_direct = 0;  // chain.hip: gathers read the granules straight from memory (no LDS staging of u)
   int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works; P <= 32)
   int32_t chain_fault = 0;   // chain.hip fault injection (tests of the timeout path): worker 0 does not publish
                              // phase chain_fault; the launch's S / H come out NaN and the next call fails
@@ -251,6 +252,9 @@ struct ChainPlan {
   int32_t P = 0, n_act = 0, lds_bytes = 0, ustride = 0;
   uint16_t* ids = nullptr;    // device [nnz_active]: 16-bit column ids in row order (P > 1: worker-local)
   uint16_t* wcols = nullptr;  // device: each worker's gathered columns, concatenated (P > 1)
+  uint16_t* gids = nullptr;   // device [nnz_active]: global 16-bit column ids (direct mode)
+  uint16_t* bcols = nullptr;  // device: each worker's back-edge columns, concatenated (P > 1)
+  int32_t* bcol_off = nullptr;  // device [P + 1]
   int32_t* wcol_off = nullptr;  // device [P + 1]
   int4* wdesc = nullptr;      // device [P]: {row0, row1, e0, e1}
   int32_t* wpass = nullptr;   // device [P][17]: each worker's waves' ranges of passes

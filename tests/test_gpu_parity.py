@@ -742,6 +742,8 @@ def test_chain_under_torch_graph_capture():
                                            (19717, 88648, 1, {}), (19717, 88648, 2, {"chain_wg": 3}),
                                            (19717, 88648, 32, {"chain_wg": 16, "chain_xcd": 1}),
                                            (19717, 88648, 16, {"chain_xcd": 1}),
+                                           (19717, 88648, 16, {"chain_direct": 1}), (19717, 88648, 2, {"chain_direct": 1}),
+                                           (19717, 88648, 32, {"chain_wg": 16, "chain_direct": 1}),
                                            (6000, 150000, 16, {"chain_wg": 5})])
 def test_chain1_vs_oracle(n, nnz, K, knobs):
     """F = 1 small graphs run the whole chain in one launch (P workers, a
@@ -770,6 +772,33 @@ def test_chain1_vs_oracle(n, nnz, K, knobs):
     L.tune(chain=0)   # the multi-launch path gives the same result to rounding
     _, S0 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=Xt, return_S=True)
     assert_parity(S1.cpu().numpy(), S0.cpu().numpy().astype(np.float64), what="chain1 vs multi-launch")
+    L.close()
+
+
+@pytest.mark.parametrize("wg", [4, 16, 64])
+def test_chain1_directed_multi_worker(wg):
+    """A directed graph through the one-launch chain with several workers: a worker
+    that reads another need not be read by it, so each worker also waits on one
+    granule of every worker that reads it (csrc/chain.hip build_chain_plan), or
+    a fast worker could overwrite a granule buffer its reader has not finished
+    (the reader would then wait for a tag that never comes)."""
+    g = random_graph(12000, 0.0012, seed=wg, directed=True, weighted=False, self_loop_frac=0.05,
+                     isolated_frac=0.05)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(chain_wg=wg)
+    X = np.random.default_rng(wg).standard_normal((g.n, 1)).astype(np.float32)
+    ref = O.graph_wavelet_features(g.to_scipy(), k=16, s=0.8, X0=X, return_all=True)
+    out = {}
+    for direct in (0, 1):   # staged u, or gathers straight from the granules (same sums, bitwise)
+        L.tune(chain_direct=direct)
+        for _ in range(3):
+            H, S = wats_hip.graph_wavelet_features(L, k=16, s=0.8, X0=torch.from_numpy(X), return_S=True)
+            torch.cuda.synchronize()
+            assert "chain1:" in L.describe(1), L.describe(1)
+            assert not L.chain_status(), "a chain wait timed out"
+            assert_parity(_np(S), ref["S"], what=f"chain1 directed P={wg} direct={direct} S")
+        out[direct] = _np(S)
+    assert np.array_equal(out[0], out[1]), "direct gathers changed the sums"
     L.close()
 
 
