@@ -225,7 +225,7 @@ struct Tuning {
                              // 0 = auto: one when its ids and two u buffers fit LDS (no exchange), else 64
                              // (PubMed-size K=16: 8 / 16 / 32 / 64 workers 187 / 139 / 119 / 113 us per chain,
                              // profiles/r03/s13_chain1_worker_sweep.log)
-  int32_t chain_direct = 0;  // chain.hip: gathers read the granules straight from memory (no LDS staging of u)
+  int32_t chain_direct = 1;  // chain.hip: gathers read the granules straight from memory (no LDS staging of u)
   int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works; P <= 32)
   int32_t chain_fault = 0;   // chain.hip fault injection (tests of the timeout path): worker 0 does not publish
                              // phase chain_fault; the launch's S / H come out NaN and the next call fails
