@@ -925,6 +925,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.rsplit = hyb->tsplit;
         a.part = hyb->part + f0;
       }
+      a.nt = L->tune.nt >= 0 ? L->tune.nt : 8;  // store policy (below), for the team kernel too
       // value-free steps at VEC 4: every row as independent waves on SELL-ordered
       // padded ids (team.hip; the hybrid step's tail too), or the workgroup kernel on the padded CSR
       // (accumulate_u4 / accumulate_sell); all columns in one tile, rows addressable by 24-bit ids
