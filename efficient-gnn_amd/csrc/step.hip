@@ -378,7 +378,9 @@ __global__ __launch_bounds__(kBlock) void permute_kernel(int64_t n, int64_t F, i
 // purely isolated rows >= closed_from never enter the chain, so their
 // S = coef * X0 and H = S / (|S|_1 + 1e-8) are written to the caller's row
 // directly (the finalize_kernel arithmetic, same order of the row sum).
-template <int VEC>
+// RG row groups per wave, their row ids and X0 rows loaded before any is used (the pass is
+// latency-bound: one group per wave left each wave a dependent perm -> X0 -> store chain)
+template <int VEC, int RG>
 __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, int64_t F, int LF,
                                                                    const int32_t* __restrict__ perm,
                                                                    const float* __restrict__ src,
@@ -391,48 +393,60 @@ __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, in
   const int G = 64 / LF;
   const int sg = lane / LF;
   const int fs = lane - sg * LF;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + sg;
-  const bool active = sg < G && row < n;
-  const bool closed = row >= closed_from;
-  int64_t r = 0;
-  float x[VEC];
-  double sv[VEC];
-  double part = 0.0;
-  if (active) {
-    r = perm[row];
-    load_vec<VEC>(src + r * F + fs * VEC, x);
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  int64_t rows[RG], rs[RG];
+  bool act[RG];
+  float x[RG][VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      sv[j] = closed ? coef * (double)x[j] : (double)x[j];
-      part += fabs(sv[j]);
-    }
-    if (!closed) {
-      store_vec<VEC>(dst + row * F + fs * VEC, sv);
-      if (u) {  // u_0 = X0 * dinv for the first value-free step (scale_rows_kernel's rounding)
-        const double di = dinv[row];
-        double uv[VEC];
+  for (int g = 0; g < RG; ++g) {
+    rows[g] = (wave * RG + g) * G + sg;
+    act[g] = sg < G && rows[g] < n;
+    rs[g] = act[g] ? perm[rows[g]] : 0;
+  }
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) uv[j] = (double)x[j] * di;
-        store_vec<VEC>(u + row * F + fs * VEC, uv);
+  for (int g = 0; g < RG; ++g)
+    if (act[g]) load_vec<VEC>(src + rs[g] * F + fs * VEC, x[g]);
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int64_t row = rows[g], r = rs[g];
+    const bool active = act[g];
+    const bool closed = row >= closed_from;
+    double sv[VEC];
+    double part = 0.0;
+    if (active) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        sv[j] = closed ? coef * (double)x[g][j] : (double)x[g][j];
+        part += fabs(sv[j]);
+      }
+      if (!closed) {
+        store_vec<VEC>(dst + row * F + fs * VEC, sv);
+        if (u) {  // u_0 = X0 * dinv for the first value-free step (scale_rows_kernel's rounding)
+          const double di = dinv[row];
+          double uv[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) uv[j] = (double)x[g][j] * di;
+          store_vec<VEC>(u + row * F + fs * VEC, uv);
+        }
       }
     }
-  }
-  // closed rows are the internal tail: most waves hold none and skip the row sums
-  if (!__ballot(active && closed)) return;
-  double tot = 0.0;
-  for (int q = 0; q < LF; ++q) tot += __shfl(part, sg * LF + q, 64);
-  if (!active || !closed) return;
-  const double den = tot + 1e-8;
-  double h[VEC];
+    // closed rows are the internal tail: most groups hold none and skip the row sums
+    if (!__ballot(active && closed)) continue;
+    double tot = 0.0;
+    for (int q = 0; q < LF; ++q) tot += __shfl(part, sg * LF + q, 64);
+    if (!active || !closed) continue;
+    const double den = tot + 1e-8;
+    double h[VEC];
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) h[j] = sv[j] / den;
-  store_vec<VEC>(S + r * F + fs * VEC, sv);
-  store_vec<VEC>(H + r * F + fs * VEC, h);
-  // a row shard's exchange slots (dist.hip): the closed rows' u rows zero in both slots (the
-  // hybrid step's dense tiles stage whole 32-row column tiles: 0 x stale must not enter a sum)
-  const double z[VEC] = {};
-  if (u && row < u_rows) store_vec<VEC>(u + row * F + fs * VEC, z);
-  if (zero) store_vec<VEC>(zero + row * F + fs * VEC, z);
+    for (int j = 0; j < VEC; ++j) h[j] = sv[j] / den;
+    store_vec<VEC>(S + r * F + fs * VEC, sv);
+    store_vec<VEC>(H + r * F + fs * VEC, h);
+    // a row shard's exchange slots (dist.hip): the closed rows' u rows zero in both slots (the
+    // hybrid step's dense tiles stage whole 32-row column tiles: 0 x stale must not enter a sum)
+    const double z[VEC] = {};
+    if (u && row < u_rows) store_vec<VEC>(u + row * F + fs * VEC, z);
+    if (zero) store_vec<VEC>(zero + row * F + fs * VEC, z);
+  }
 }
 
 // caller rows (stride F) -> internal rows (stride Fp > F), the Fp - F pad columns zeroed
@@ -1096,15 +1110,16 @@ int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, flo
   if (F > 64 * vec) return fail(WG_ERR_INVALID, "permute_in_closed: F too wide");
   const int LF = (int)(F / vec);
   const int G = 64 / LF;
-  const dim3 grid((unsigned)ceil_div(n, 4 * G));
+  constexpr int kRG = 4;
+  const dim3 grid((unsigned)ceil_div(n, 4 * G * kRG));
   if (vec == 4)
-    hipLaunchKernelGGL(permute_in_closed_kernel<4>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
+    hipLaunchKernelGGL((permute_in_closed_kernel<4, kRG>), grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
                        L->n_active, coef, S, H, L->dinv, u, zero ? n : 0, zero);
   else if (vec == 2)
-    hipLaunchKernelGGL(permute_in_closed_kernel<2>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
+    hipLaunchKernelGGL((permute_in_closed_kernel<2, kRG>), grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
                        L->n_active, coef, S, H, L->dinv, u, zero ? n : 0, zero);
   else
-    hipLaunchKernelGGL(permute_in_closed_kernel<1>, grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
+    hipLaunchKernelGGL((permute_in_closed_kernel<1, kRG>), grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src, dst,
                        L->n_active, coef, S, H, L->dinv, u, zero ? n : 0, zero);
   WG_LAUNCH_CHECK();
   return WG_OK;
