@@ -372,9 +372,11 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
 #endif
     if (k == 0) break;
     __syncthreads();  // every gather of this phase is done with u
-    if (a.direct) {
-      // nothing to stage: the next phase's gathers read this phase's granules
-    } else if (a.P == 1) {
+    if (a.direct) {  // nothing to stage: the next phase's gathers read this phase's granules
+      bad = s_bad != 0;
+      continue;
+    }
+    if (a.P == 1) {
       float* t = u;
       u = u2;
       u2 = t;
