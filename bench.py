@@ -16,8 +16,15 @@ Headline workload by GPU count (BASELINE.json configs):
   N > 1  configs[3]: the Reddit-size graph (232,965 nodes / 114.6M nonzeros),
          K=16, F=41 (the 41-class logit-shaped RHS of SURVEY 8(d)), ONE graph
          row-sharded over the N ranks (nnz-balanced row blocks, [own | halo]
-         columns) with a halo exchange per Chebyshev step (RCCL grouped
-         send/recv by default) -- strong scaling.  The same Reddit run at one
+         columns) with a halo exchange per Chebyshev step -- strong scaling.
+         Exchange (--exchange ipc,rccl,sdma, --pick-exchange 1): the headline
+         is timed with the one-sided IPC pull AND with RCCL grouped
+         ncclSend/ncclRecv (north_star's all-to-all-v, each peer's rows straight
+         into the halo), and the line is the FASTER of the two whose check
+         passed (both attached; an RCCL error or hang falls back to IPC on every
+         rank); the peer-DMA exchange (sdma) is timed beside them.  So the N > 1
+         line may well be the IPC pull, not RCCL: whichever measured faster on
+         that node.  The same Reddit run at one
          rank is the N = 1 line's `sharded` object, so the Reddit curve is
          complete across the driver's 1/2/4/8 lines.
 value = total edges*K processed by all ranks / max-over-ranks wall time, where
@@ -350,7 +357,10 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
     nnz_lhat = _allreduce(float(sw.L.nnz), dist.ReduceOp.SUM, device) if world > 1 else float(sw.L.nnz)
     p = sw.plan
-    b_8d = algorithmic_bytes(p.n_own, sw.L.nnz, F)
+    # SURVEY 8(d) over the rows the step launches: a shard's purely isolated own rows are closed-form
+    # and never launched, as in the unsharded line
+    n_launch = p.n_own - int(sw.L.info["n_closed_form"])
+    b_8d = algorithmic_bytes(n_launch, sw.L.nnz, F)
     lds_info = sw.L.lds_plan_info(active_only=False) if (F == 1 and sw.u_len() > 0) else None
     b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
     kernel = lds_kernel_name(lds_info) + " (rank 0 shard)"
@@ -400,8 +410,7 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
                      "byte_model": _byte_model(lds_info),
                      "lds_plan": lds_info,
                      "tiles_plan": tiles_plan[0] if tiles_plan else None,
-                     "nominal_8d_bytes": b_8d,
-                     "nominal_8d_frac": (b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if avg_ms else None},
+                     "rows_per_launch": n_launch, "closed_form_rows": p.n_own - n_launch},
         "check": chk,
     }
 
@@ -547,8 +556,7 @@ def f1_companion(lib, L, K, s_heat, steps, device, unit=False):
             "byte_model": _byte_model(info),
             "algorithmic_bytes_per_launch": b_roof, "frac": b_roof / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "kernel_byte_model": _byte_model(info) if info else "Clenshaw heat sum (DESIGN.md 4.1)",
-            "kernel_bytes_frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            "kernel_bytes_frac": b_step / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def prologue_timing(g, L, device, reps: int = 5) -> dict:
@@ -736,7 +744,6 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
                          "rows are closed-form and never launched); kernel_bytes_frac: the bytes this "
                          "kernel's algorithm needs (Clenshaw: no S stream; unweighted: no CSR values); "
                          "all_rows_frac: SURVEY 8(d)'s B_step with N = all nodes",
-            "nominal_8d_frac": b_8d / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "avg_launch_us": avg_ms * 1e3,
             "max_launch_us": prof["max_ms"] * 1e3,
             "launches": prof["launches"],

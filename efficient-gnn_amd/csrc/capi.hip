@@ -197,7 +197,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < -1 || value > 1) return fail(WG_ERR_INVALID, "chain must be -1 (auto), 0 or 1");
     L->tune.chain = (int32_t)value;
   } else if (!strcmp(key, "chain_wg")) {
-    if (value < 0 || value > 256) return fail(WG_ERR_INVALID, "chain_wg must be in [0 (auto), 256]");
+    if (value < 0 || value > 1024) return fail(WG_ERR_INVALID, "chain_wg must be in [0 (auto), 1024]");
     L->tune.chain_wg = (int32_t)value;
   } else if (!strcmp(key, "chain_fault")) {
     if (value < 0 || value > kChainMaxK) return fail(WG_ERR_INVALID, "chain_fault must be in [0, %d]", kChainMaxK);
@@ -294,13 +294,26 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
   const int LF = (int)(std::min<int64_t>(F, 64 * vec) / vec);
   Plan* p = nullptr;
   if (get_plan(L, LF, vec, true, &p)) return "";
-  char buf[128];
+  char buf[192];
   snprintf(buf, sizeof(buf), "F=%lld VEC=%d LF=%d segments=%d blocks=%d active_rows=%lld closed_form_rows=%lld\n",
            (long long)F, vec, LF, p->tab.n, p->tab.total_blocks, (long long)L->n_active, (long long)L->n_closed);
   g_text = buf + p->text;
+  // split-row arrival counters left non-zero (each row's completing arrival resets its counter,
+  // so a finished launch leaves none: tests read this after a device sync)
+  auto pending = [](const uint32_t* d, int32_t n) -> int {
+    if (!d || n <= 0) return 0;
+    std::vector<uint32_t> h(n);
+    if (hipMemcpy(h.data(), d, sizeof(uint32_t) * n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return (int)std::count_if(h.begin(), h.end(), [](uint32_t v) { return v != 0; });
+  };
   if (p->team.wd) {  // the independent-wave step kernel's table, once a step has built it (team.hip)
-    snprintf(buf, sizeof(buf), "team: waves=%d long_rows=%d part_slots=%d\n", p->team.n_waves, p->team.n_long,
-             p->team.n_slots);
+    snprintf(buf, sizeof(buf), "team: waves=%d long_rows=%d part_slots=%d max_parts=%d npot_rows=%d pending_arrivals=%d\n",
+             p->team.n_waves, p->team.n_long, p->team.n_slots, p->team.max_parts, p->team.npot_rows,
+             pending(p->team.warr, p->team.n_long));
+    g_text += buf;
+  }
+  if (p->arrivals && p->n_split > 0) {
+    snprintf(buf, sizeof(buf), "split rows: %d pending_arrivals=%d\n", p->n_split, pending(p->arrivals, p->n_split));
     g_text += buf;
   }
   for (int i = 1; i >= 0; --i)  // the hybrid step's plan, once a chain has built it
@@ -309,6 +322,11 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
     Lds1Plan* lp = nullptr;
     if (!get_lds1_plan(L, true, &lp) && lp) g_text += lp->text;
     if (L->chain1) g_text += L->chain1->text;  // once a chain has built it
+    if (L->chain1_timeouts || L->chain1_off) {
+      snprintf(buf, sizeof(buf), "chain1 timeouts=%d%s\n", L->chain1_timeouts,
+               L->chain1_off ? " (off: multi-launch path)" : "");
+      g_text += buf;
+    }
   }
   return g_text.c_str();
 }

@@ -465,7 +465,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   // 64; staged: 64 workers 79.5, 128 77.9; r04 s43), doubled until a worker fits LDS
   const int p_auto = L->tune.chain_direct ? 128 : 64;
   for (;; P = (P == 1 && L->tune.chain_wg <= 0) ? p_auto : 2 * P) {
-    if (P > 256) return WG_ERR_UNSUPPORTED;
+    if (P > 1024) return WG_ERR_UNSUPPORTED;  // (and never more than can be resident: below)
     wd.assign(P, int4{0, 0, 0, 0});
     passes.clear();
     wpass.assign((size_t)P * (kChainWaves + 1), 0);
@@ -541,6 +541,19 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
     }
     if (fits) break;
   }
+  // every worker spins on other workers' granules, so all P (x the XCD stride) workgroups must be
+  // resident at once: never more than one per CU, and no more than the occupancy query admits for
+  // this LDS size (a plain launch does not check; a shared GPU is caught by the wait timeout)
+  {
+    int dev = 0, per_cu = 0;
+    WG_HIP_TRY(hipGetDevice(&dev));
+    if (int rc = ensure_dyn_lds((const void*)cheb_chain1_kernel, kChainLds)) return rc;
+    WG_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)cheb_chain1_kernel, kChainThreads,
+                                                            (lds + 15) / 16 * 16));
+    const int64_t stride = (L->tune.chain_xcd && P <= 32) ? 8 : 1;
+    const int64_t resident = (int64_t)n_cus(dev) * std::min(per_cu, 1);
+    if ((int64_t)P * stride > resident) return WG_ERR_UNSUPPORTED;
+  }
   p->P = P;
   p->n_act = (int32_t)na;
   p->lds_bytes = (int32_t)((lds + 15) / 16 * 16);
@@ -561,6 +574,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   if (!rc) rc = dmalloc(&p->u0, (size_t)std::max<int64_t>(na, 1));
   if (!rc) rc = dmalloc(&p->x0, (size_t)std::max<int64_t>(na, 1));
   if (rc) return rc;
+  WG_HIP_TRY(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
   WG_HIP_TRY(hipHostMalloc((void**)&p->host_flag, sizeof(int32_t), hipHostMallocMapped));
   *p->host_flag = 0;
   WG_HIP_TRY(hipHostGetDevicePointer((void**)&p->d_host_flag, p->host_flag, 0));
@@ -582,6 +596,7 @@ void ChainPlan::release() {
                   (void*)gbuf, (void*)u0, (void*)x0})
     (void)hipFree(q);
   if (host_flag) (void)hipHostFree(host_flag);
+  if (done) (void)hipEventDestroy(done);
   *this = ChainPlan{};
 }
 
@@ -592,6 +607,7 @@ void release_chain1(wg_laplacian_s* L) {
     L->chain1 = nullptr;
   }
   L->chain1_failed = false;
+  L->chain1_off = false;  // a tune gives the one-launch chain another chance
 }
 
 int get_chain1_plan(wg_laplacian_s* L, int64_t F, int32_t K, ChainPlan** out) {
@@ -603,7 +619,7 @@ int get_chain1_plan(wg_laplacian_s* L, int64_t F, int32_t K, ChainPlan** out) {
       na > 24576 || L->tune.chain == 0 || (L->tune.chain < 0 && L->nnz > ((int64_t)1 << 18)) ||
       L->tune.uscale == 0)
     return WG_OK;
-  if (L->chain1_failed) return WG_OK;
+  if (L->chain1_failed || L->chain1_off) return WG_OK;
   if (!L->chain1) {
     auto* p = new ChainPlan();
     const int rc = build_chain_plan(L, p);
@@ -672,6 +688,9 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   hipLaunchKernelGGL(cheb_chain1_kernel, dim3((unsigned)(p->P * a.stride)), dim3(kChainThreads), (size_t)p->lds_bytes,
                      stream, a);
   WG_LAUNCH_CHECK();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  WG_HIP_TRY(hipStreamIsCapturing(stream, &cs));
+  if (cs == hipStreamCaptureStatusNone) WG_HIP_TRY(hipEventRecord(p->done, stream));
   return prof_mark(L, stream, false);
 }
 
@@ -683,6 +702,8 @@ int chain1_check(wg_laplacian_s* L) {
   const int32_t failed = __atomic_load_n(p->host_flag, __ATOMIC_ACQUIRE);
   if (failed == p->seen) return WG_OK;
   p->seen = failed;
+  L->chain1_off = true;  // later calls take the multi-launch path
+  ++L->chain1_timeouts;
   return fail(WG_ERR_TIMEOUT,
               "wg_wavelet_features: a previous one-launch chain (csrc/chain.hip) gave up waiting for a worker; its "
               "S / H were written as NaN (was the GPU shared with another kernel?)");
@@ -691,10 +712,14 @@ int chain1_check(wg_laplacian_s* L) {
 int chain1_status(wg_laplacian_s* L, int32_t* timed_out) {
   *timed_out = 0;
   if (!L->chain1) return WG_OK;
-  WG_HIP_TRY(hipDeviceSynchronize());
   ChainPlan* p = L->chain1;
+  WG_HIP_TRY(hipEventSynchronize(p->done));  // the handle's last one-launch chain only (no device sync)
   const int32_t failed = __atomic_load_n(p->host_flag, __ATOMIC_ACQUIRE);
   *timed_out = failed != p->seen ? 1 : 0;  // since the last report (here or by wg_wavelet_features)
+  if (*timed_out) {  // later calls take the multi-launch path
+    L->chain1_off = true;
+    ++L->chain1_timeouts;
+  }
   p->seen = failed;
   return WG_OK;
 }

@@ -165,7 +165,7 @@ __global__ void ipc_wait_kernel(IpcPull p, int) { ipc_wait(p); }
 // rest on the scope of the runtime's end-of-kernel release (which this code cannot read, eager or
 // replayed from a hipGraph), kIpcSignalBlocks workgroups (one or more on every XCD: workgroups are
 // dealt round-robin) each write back their XCD's L2 (__threadfence_system = buffer_wbl2 sc0 sc1 +
-// its wait), count their XCD in a mask and arrive on a monotonic counter; the last to arrive
+// its wait), count their XCD in a mask and arrive on a counter; the last to arrive resets it,
 // checks that n_xcc distinct XCDs released (else err |= 2: the ordering is not guaranteed) and
 // stores the flags with system-scope release stores.
 constexpr int kIpcSignalBlocks = 64;
@@ -177,7 +177,8 @@ __global__ void ipc_signal_kernel(int64_t* count, int32_t world, int32_t rank, i
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   __hip_atomic_fetch_or(arrive + 1, 1u << (xcc & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  if ((old + 1) % kIpcSignalBlocks != 0) return;
+  if (old + 1u != (uint32_t)kIpcSignalBlocks) return;
+  __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next phase starts from 0
   const uint32_t mask = __hip_atomic_exchange(arrive + 1, 0u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
   if (__popc(mask) < n_xcc) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __threadfence_system();
@@ -222,6 +223,12 @@ struct wg_dist_s {
   bool use_graph = true;
   hipStream_t cap = nullptr;  // capture / replay stream (the caller's may be the null stream)
   hipEvent_t fork = nullptr, join = nullptr;
+  // the stream the handle's last chain was enqueued on (a replay goes into the caller's stream, an
+  // eager chain onto cap): a chain enqueued on another stream first waits for it (handoff), since
+  // both share the workspace, the exchange slots and the phase counts.  The caller keeps that
+  // stream alive while the handle is in use.
+  hipStream_t last_on = nullptr;
+  hipEvent_t handoff = nullptr;
   hipGraphExec_t exec = nullptr;
   GraphKey key{};
   int warm = 0;  // eager calls made with the current key (the first builds plans / workspace)
@@ -234,7 +241,7 @@ struct wg_dist_s {
   float* region = nullptr;            // [slot 0][slot 1][flags: world int64]
   int64_t* count = nullptr;           // phases completed (device)
   int32_t* err = nullptr;             // 1: a wait timed out; 2: a signal's release missed an XCD (device)
-  uint32_t* arrive = nullptr;         // ipc_signal_kernel: [0] arrivals (monotonic), [1] XCD mask
+  uint32_t* arrive = nullptr;         // ipc_signal_kernel: [0] arrivals (0 between phases), [1] XCD mask
   int32_t n_xcc = 1;                  // XCDs of this device
   int32_t* halo_owner = nullptr;
   int32_t* halo_src = nullptr;
@@ -266,6 +273,7 @@ struct wg_dist_s {
     if (copy) (void)hipStreamDestroy(copy);
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
+    if (handoff) (void)hipEventDestroy(handoff);
     if (cap) (void)hipStreamDestroy(cap);
     (void)hipFree(send_rows);
     (void)hipFree(ws);
@@ -596,7 +604,8 @@ int wg_dist_create(wg_laplacian_t L, const void* unique_id, int32_t rank, int32_
   }
   if (!rc && (hipStreamCreateWithFlags(&D->cap, hipStreamNonBlocking) != hipSuccess ||
               hipEventCreateWithFlags(&D->fork, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess))
+              hipEventCreateWithFlags(&D->join, hipEventDisableTiming) != hipSuccess ||
+              hipEventCreateWithFlags(&D->handoff, hipEventDisableTiming) != hipSuccess))
     rc = fail(WG_ERR_HIP, "wg_dist_create: stream/event");
   if (!rc && unique_id) {  // NULL: no RCCL communicator (one-sided IPC exchange, wg_dist_ipc_*)
     ncclUniqueId id;
@@ -644,15 +653,27 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
       WG_HIP_TRY(hipDeviceSynchronize());  // its last replay ran on some caller stream
       (void)hipGraphExecDestroy(D->exec);
       D->exec = nullptr;
+      D->last_on = nullptr;
     }
     D->key = key;
     D->warm = 0;
   }
+  // order this chain after the handle's previous one when that ran on another stream (no event
+  // per call on the usual path: the marker is recorded only when the stream changes)
+  auto after_last = [&](hipStream_t target) -> int {
+    if (D->last_on && D->last_on != target) {
+      WG_HIP_TRY(hipEventRecord(D->handoff, D->last_on));
+      WG_HIP_TRY(hipStreamWaitEvent(target, D->handoff, 0));
+    }
+    D->last_on = target;
+    return WG_OK;
+  };
   // eager: profiling (per-step events), graphs disabled, or the first call with
   // these arguments (it builds the kernel plans and the workspace).  Either way the chain
   // runs on the handle's own non-blocking stream (cap), joined to the caller's: on the legacy
   // null stream the step kernels would wait for every blocking stream's work.
   if (!D->use_graph || D->L->prof || D->warm == 0) {
+    if (int rc = after_last(D->cap)) return rc;
     WG_HIP_TRY(hipEventRecord(D->fork, st));
     WG_HIP_TRY(hipStreamWaitEvent(D->cap, D->fork, 0));
     const int rc = D->chain(X0, F, K, s, S, H, D->cap);
@@ -682,6 +703,7 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   }
   // the replay goes straight into the caller's stream: a fork / join through the handle's stream
   // per call left ~25-30 us of idle GPU between back-to-back chains (r04 s35 kernel trace)
+  if (int rc = after_last(st)) return rc;
   WG_HIP_TRY(hipGraphLaunch(D->exec, st));
   return WG_OK;
 }

@@ -75,8 +75,9 @@ struct TeamPlan {
                              // {part, parts, first slot, arrival counter}
   int4* sell = nullptr;      // device: the waves' column ids in SELL order (accumulate_sell)
   double* wpart = nullptr;   // device [n_slots][width]: long rows' float64 partials
-  int32_t* warr = nullptr;   // device [n_long]: monotonic arrival counters
+  uint32_t* warr = nullptr;  // device [n_long]: arrival counters, reset by each row's last arrival
   int32_t n_waves = 0, n_slots = 0, n_long = 0, width = 0;
+  int32_t max_parts = 0, npot_rows = 0;  // long rows: most parts; rows whose part count is not a power of 2
   void release();
 };
 
@@ -92,7 +93,7 @@ struct Plan {
   ChunkDesc* chunks = nullptr;  // device [n_chunks]
   double* partial = nullptr;    // device [n_chunks][width]
   int2* rowchunks = nullptr;    // device [n_split] {first chunk, chunk count}
-  int32_t* arrivals = nullptr;  // device [n_split] monotonic arrival counters (in-kernel combine)
+  uint32_t* arrivals = nullptr; // device [n_split] arrival counters, reset by each row's last arrival
   // value-free VEC-4 team waves (step.hip build_sell): each wave's column ids in SELL-G order --
   // turn t, chunk c (4 ids), sub-group g at sell[wmeta[w].x + (2 t + c) G + g] -- padded with
   // kPadCol to the wave's longest sub-group, wmeta[w] = {first chunk, turns} per wave w
@@ -263,6 +264,7 @@ struct ChainPlan {
   int32_t* host_flag = nullptr;    // host-mapped (pinned): epoch of the last timed-out launch
   int32_t* d_host_flag = nullptr;  // its device address
   int32_t seen = 0;                // the host_flag value already reported
+  hipEvent_t done = nullptr;       // recorded after every launch: chain1_status waits for it alone
   uint64_t* gbuf = nullptr;   // device [2][ustride]: tagged u granules {float bits, tag << 32}
   float* u0 = nullptr;        // device [n_act]: u_0 = X0 * dinv
   float* x0 = nullptr;        // device [n_act]: X0 in internal order
@@ -334,7 +336,9 @@ struct wg_laplacian_s {
   int64_t warm_gen = -1;
   wg::ChainGraph chain;  // small chains replayed as a hipGraph (tuning key "graph")
   wg::ChainPlan* chain1 = nullptr;  // the one-launch F = 1 chain (chain.hip), lazily
-  bool chain1_failed = false;
+  bool chain1_failed = false;       // no plan (too large for resident workers / LDS): multi-launch path
+  bool chain1_off = false;          // a launch timed out (the GPU is shared?): multi-launch path until a tune
+  int32_t chain1_timeouts = 0;      // timed-out launches seen on this handle
   // live step-kernel timing (wg_profile_*)
   bool prof = false;
   std::vector<hipEvent_t> ev;  // pool of (start, stop) pairs

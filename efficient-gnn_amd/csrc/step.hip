@@ -18,8 +18,8 @@
 //    chunk writes a float64 partial.  The last chunk to arrive finishes the row
 //    in the same kernel (inkernel_combine = 1, the default): partials are sc1
 //    (write-through) stores drained by every storing wave (s_waitcnt
-//    vmcnt(0)), then one agent-scope atomic add per chunk on a monotonic
-//    per-row counter; the workgroup whose add completes the row reads every
+//    vmcnt(0)), then one agent-scope atomic add per chunk on a
+//    per-row counter (the completing arrival resets it to 0); the workgroup whose add completes the row reads every
 //    chunk's partial with sc1 loads, in chunk order, and runs the epilogue.
 //    This relies on gfx950's cache behaviour (sc1 stores write through to L2,
 //    sc1 loads bypass the L1), the hand-off of MI355X_MICROARCH.md's table
@@ -192,8 +192,10 @@ __device__ __forceinline__ void unit_body(const StepArgs& a, const Seg* __restri
     __syncthreads();
     const int2 rc = a.rowchunks[row];
     if (threadIdx.x == 0) {
-      const int old = __hip_atomic_fetch_add(a.arrivals + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = ((old + 1) % rc.y) == 0;  // monotonic counter: every rc.y-th arrival completes a step
+      // the arrival that completes the row resets its counter (uint32, equality: no history)
+      const uint32_t old = __hip_atomic_fetch_add(a.arrivals + row, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old + 1u == (uint32_t)rc.y;
+      if (s_last) __hip_atomic_store(a.arrivals + row, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (s_last && threadIdx.x < LF) {
@@ -493,9 +495,9 @@ template <int VEC, int NW>
 void launch_main(const Plan& plan, const StepArgs& a, hipStream_t stream) {
   const dim3 grid(plan.tab.total_blocks), block(NW * 64);
   if constexpr (VEC == 4) {
-    if (a.pcol) {  // a.vidx carries the padded-CSR loop variant (gather4 tuning value)
+    if (a.pcol) {  // a.p4v: the padded-CSR loop variant (gather4 tuning value)
       const Seg* sg = plan.d_segs;
-      switch (a.vidx) {
+      switch (a.p4v) {
         case 121: hipLaunchKernelGGL((cheb_step_occ_kernel<NW, 21>), grid, block, 0, stream, a, sg, plan.tab.n); break;
         case 31: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 31>), grid, block, 0, stream, a, sg, plan.tab.n); break;
         case 22: hipLaunchKernelGGL((cheb_step_kernel<4, false, NW, 22>), grid, block, 0, stream, a, sg, plan.tab.n); break;
@@ -711,7 +713,7 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, b
     if (!rc_) rc_ = dmalloc(&p.partial, ch.size() * (size_t)p.width);
     if (!rc_) rc_ = dmalloc(&p.rowchunks, rc.size());
     if (!rc_) rc_ = dmalloc(&p.arrivals, rc.size());
-    if (!rc_ && hipMemset(p.arrivals, 0, sizeof(int32_t) * rc.size()) != hipSuccess) rc_ = WG_ERR_HIP;
+    if (!rc_ && hipMemset(p.arrivals, 0, sizeof(uint32_t) * rc.size()) != hipSuccess) rc_ = WG_ERR_HIP;
     if (rc_) {
       p.release();
       return rc_;
@@ -879,10 +881,18 @@ int build_sell(wg_laplacian_s* L, Plan* p, int LF) {
     }
   }
   sell.resize(sell.size() + (size_t)4 * G, pad4);  // the next-turn id reads past the last wave
-  if (int rc = dmalloc(&p->wmeta, wm.size())) return rc;
-  if (int rc = dmalloc(&p->sell, sell.size())) return rc;
-  WG_HIP_TRY(hipMemcpy(p->wmeta, wm.data(), sizeof(int2) * wm.size(), hipMemcpyHostToDevice));
-  WG_HIP_TRY(hipMemcpy(p->sell, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice));
+  auto undo = [&](int rc) {  // no half-built table: the next call builds both arrays again
+    (void)hipFree(p->wmeta);
+    (void)hipFree(p->sell);
+    p->wmeta = nullptr;
+    p->sell = nullptr;
+    return rc;
+  };
+  if (int rc = dmalloc(&p->wmeta, wm.size())) return undo(rc);
+  if (int rc = dmalloc(&p->sell, sell.size())) return undo(rc);
+  if (hipMemcpy(p->wmeta, wm.data(), sizeof(int2) * wm.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p->sell, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return undo(fail(WG_ERR_HIP, "build_sell: upload failed"));
   return WG_OK;
 }
 
@@ -966,7 +976,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.prp = L->prp;
         a.pcol = L->pcol;
         a.u_bytes = (uint32_t)(L->n_cols * F * 4);
-        a.vidx = L->tune.gather4;  // the loop variant (launch_main)
+        a.p4v = L->tune.gather4;  // the loop variant (launch_main)
         if (L->tune.sell && plan->tab.total_blocks > 0) {  // team waves on SELL-ordered ids
           if (int rc2 = build_sell(L, plan, LF)) return rc2;
           a.wmeta = plan->wmeta;

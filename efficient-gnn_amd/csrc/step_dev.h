@@ -28,7 +28,7 @@ struct StepArgs {
   const ChunkDesc* chunks;
   double* partial;
   const int2* rowchunks;  // split rows: {first chunk, chunk count}
-  int32_t* arrivals;      // split rows: in-kernel combine counters (nullable = combine_kernel)
+  uint32_t* arrivals;     // split rows: in-kernel combine counters, 0 between launches (nullable = combine_kernel)
   int64_t seg_mask;
   int32_t nt;
   int32_t bcast;
@@ -57,6 +57,7 @@ struct StepArgs {
   // of u_bytes bytes, so a pad id's offset falls outside it and its load returns 0 with no request
   const int32_t* prp;
   const int32_t* pcol;
+  int32_t p4v;        // the padded-CSR loop variant (tuning key gather4; launch_main)
   uint32_t u_bytes;
   unsigned long long* trace;  // -DWG_TIMING_PROBES, knob "trace": per-wave timeline of one launch
   const int2* wmeta;  // team waves in SELL order (Plan::sell): per wave {first chunk, turns}

@@ -36,7 +36,7 @@ struct TeamArgs {
   const int4* wd;
   int32_t n_waves;
   double* wpart;   // [slots][LF * 4] float64 partials of part waves
-  int32_t* warr;   // [long rows] monotonic arrival counters
+  uint32_t* warr;  // [long rows] arrival counters (0 between launches: the last arrival resets)
 };
 
 // MINW: minimum waves per SIMD the registers are held to (6 = the natural 77 VGPRs); LATE: the
@@ -90,8 +90,11 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int last = 0;
     if (lane == 0) {
-      const int old = __hip_atomic_fetch_add(t.warr + d1.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = ((old + 1) % d1.y) == 0;  // monotonic counter: every parts-th arrival completes a step
+      // the arrival that completes the row resets its counter: every launch starts from 0, whatever
+      // the history of earlier launches (uint32, compared for equality: no wrap-around modulus)
+      const uint32_t old = __hip_atomic_fetch_add(t.warr + d1.w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old + 1u == (uint32_t)d1.y;
+      if (last) __hip_atomic_store(t.warr + d1.w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     last = __shfl(last, 0, 64);
     if (!last || lane >= LF) return;
@@ -151,6 +154,7 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
   std::vector<int4> sell;
   const int4 pad4{kPadCol, kPadCol, kPadCol, kPadCol};
   int32_t slots = 0, longs = 0;
+  tp->max_parts = tp->npot_rows = 0;
   auto chunk = [&](int64_t r, int64_t ch) {  // the 4 ids of chunk ch of row r
     int32_t id[4];
     for (int i = 0; i < 4; ++i) {
@@ -180,6 +184,8 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
       }
       slots += parts;
       ++longs;
+      tp->max_parts = std::max(tp->max_parts, parts);
+      if (parts & (parts - 1)) ++tp->npot_rows;
       ++r;
       continue;
     }
@@ -259,11 +265,12 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
   if (!rc) rc = dmalloc(&tp->sell, sell.size());
   if (!rc) rc = dmalloc(&tp->wpart, (size_t)std::max(slots, 1) * tp->width);
   if (!rc) rc = dmalloc(&tp->warr, (size_t)std::max(longs, 1));
-  if (rc) return rc;
-  if (!wd.empty()) WG_HIP_TRY(hipMemcpy(tp->wd, wd.data(), sizeof(int4) * wd.size(), hipMemcpyHostToDevice));
-  WG_HIP_TRY(hipMemcpy(tp->sell, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice));
-  WG_HIP_TRY(hipMemset(tp->warr, 0, sizeof(int32_t) * std::max(longs, 1)));
-  return WG_OK;
+  if (!rc && ((!wd.empty() && hipMemcpy(tp->wd, wd.data(), sizeof(int4) * wd.size(), hipMemcpyHostToDevice)) ||
+              hipMemcpy(tp->sell, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice) ||
+              hipMemset(tp->warr, 0, sizeof(uint32_t) * std::max(longs, 1))))
+    rc = fail(WG_ERR_HIP, "team waves: upload failed");
+  if (rc) tp->release();  // no half-built table (wd non-null marks a built one)
+  return rc;
 }
 
 int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream) {

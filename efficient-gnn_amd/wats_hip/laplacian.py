@@ -252,8 +252,10 @@ class NormalizedLaplacian:
         return _lib.load().wg_laplacian_describe(self.handle, int(F)).decode()
 
     def chain_status(self) -> bool:
-        """True if a one-launch chain (csrc/chain.hip) gave up a barrier wait
-        (its results are invalid); synchronous."""
+        """True if the handle's last one-launch chain (csrc/chain.hip) gave up a
+        wait (its results are NaN) and no call has reported it yet.  Waits for
+        that launch only (an event, not a device sync).  A timeout switches the
+        handle to the multi-launch path until the next tune()."""
         out = ctypes.c_int32(0)
         with torch.cuda.device(self.device):
             check(_lib.load().wg_chain_status(self.handle, ctypes.byref(out)), "chain_status")

@@ -274,14 +274,26 @@ def graph_wavelet_features(adj_matrix, k: int = 3, s: float = 0.8, X0=None, retu
     n, F = X.shape
     S = torch.empty(n, F, dtype=torch.float32, device=L.device)
     H = torch.empty(n, F, dtype=torch.float32, device=L.device)
+    lib = _lib.load()
     with torch.cuda.device(L.device):
-        check(_lib.load().wg_wavelet_features(L.handle, ptr(X), F, int(k), float(s), ptr(S), ptr(H),
-                                              stream_handle(L.device)), "wavelet_features")
-    if F == 1 and L.chain_status():
-        # the one-launch chain (csrc/chain.hip) gave up a wait: its rows depending on the
-        # missing data are NaN.  The reference returns host arrays, so this sync is its own.
-        raise WaveletError("graph_wavelet_features: the one-launch chain timed out waiting for a worker "
-                           "(results invalid, written as NaN)")
+        def run():
+            check(lib.wg_wavelet_features(L.handle, ptr(X), F, int(k), float(s), ptr(S), ptr(H),
+                                          stream_handle(L.device)), "wavelet_features")
+        try:
+            run()
+        except WaveletError as e:
+            # an earlier asynchronous call's one-launch chain timed out (reported now, WG_ERR_TIMEOUT);
+            # the handle has switched to the multi-launch path: this call runs there
+            if "status -5:" not in str(e):   # WG_ERR_TIMEOUT
+                raise
+            run()
+        # the one-launch chain (csrc/chain.hip, F = 1 small graphs) waits on other workgroups, so
+        # it needs every worker resident; on a GPU shared with another process a wait can give up
+        # (its rows are then NaN).  Check that chain alone (an event wait, not a device sync; the
+        # reference returns host arrays anyway) and rerun the call on the multi-launch path, which
+        # the handle now keeps.  Skipped while the caller captures a graph (no waits allowed then).
+        if F == 1 and not torch.cuda.is_current_stream_capturing() and L.chain_status():
+            run()
     return (H, S) if return_S else H
 
 

@@ -236,9 +236,15 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
  * hanging; that launch then writes NaN for every S / H row that depends on the
  * missing data and records the failure in host-mapped memory, and the NEXT
  * wg_wavelet_features call on the handle returns WG_ERR_TIMEOUT without
- * launching.  wg_chain_status (synchronous) reports a failure since the last
- * report in *timed_out_host (1 = a chain's results are invalid; tuning key
- * "chain_fault" = j injects one: worker 0 skips publishing phase j). */
+ * launching.  wg_chain_status waits for the handle's last one-launch chain
+ * (an event: no device-wide sync) and reports a failure since the last report
+ * in *timed_out_host (1 = a chain's results are invalid; tuning key
+ * "chain_fault" = j injects one: worker 0 skips publishing phase j).  Either
+ * report switches the handle to the multi-launch path (until the next tune),
+ * so calling again recomputes the features there (the Python
+ * graph_wavelet_features does so by itself).  The plan never asks for more
+ * workers than the occupancy query lets be resident (one per CU at most);
+ * when the graph would need more, the multi-launch path runs. */
 int wg_chain_status(wg_laplacian_t L, int32_t* timed_out_host);
 
 /* Tuning: key "iter" (team-mode nonzeros per lane sub-group; default by
