@@ -101,6 +101,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   // hipGraph (dist.hip keys its exec on this counter): plan buffers are freed below,
   // and launch-time knobs are baked into the captured kernel arguments
   ++L->tune_gen;
+  L->chain1_off = false;  // any tune gives a one-launch chain that timed out another chance
   if (!strcmp(key, "iter")) {
     if (value < 1) return fail(WG_ERR_INVALID, "iter must be >= 1");
     L->tune.iter = (int32_t)value;
@@ -226,6 +227,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "team_order")) {
     if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
     L->tune.team_order = (int32_t)value;
+  } else if (!strcmp(key, "fold")) {
+    L->tune.fold = value ? 1 : 0;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "team_iter")) {
     if (value < 8 || value > 4096) return fail(WG_ERR_INVALID, "team_iter must be in [8, 4096]");
     L->tune.team_iter = (int32_t)value;
@@ -467,9 +471,16 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
                         step_single_tile(L, F, {b0, b1, sint, S, H});
   // the first value-free Clenshaw step gathers u_0 = X0 * dinv: written by the same pass
   const bool u0_fused = fuse_fin && u0 && !lp && L->tune.clenshaw && K >= 1;
-  int rc = fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, u0_fused ? L->ws + 3 * stride : nullptr,
-                                               stream)
-                    : launch_permute_pad(L, F, Fp, X0, b0, stream);
+  // fold (tuning key "fold", default on): no permute-in pass at all.  The first step's team-kernel
+  // launch gathers the caller's X0 through caller-row ids scaled by dinv (u_0 on the fly), reads its
+  // own X0 rows at perm[row] and writes the internal X0 the later steps read, and finishes the
+  // closed-form rows (team.hip cheb_team4_first_kernel): arxiv-size F = 40 -19.6 us of pass per chain
+  const bool fold = u0_fused && g4 && !tp0 && L->tune.fold && L->tune.team && L->tune.uscale &&
+                    pick_vec(F, {X0, b0, b1, sint, S, H}) == 4;
+  int rc = fold ? WG_OK
+           : fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, u0_fused ? L->ws + 3 * stride : nullptr,
+                                                 stream)
+                      : launch_permute_pad(L, F, Fp, X0, b0, stream);
   if (rc) return rc;
   if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * Fp, hipMemcpyDeviceToDevice, stream));
   if (lp) {
@@ -504,7 +515,7 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     // (L_hat b = -dinv_i sum_j u_j); X0 itself stays unscaled (the first step reads the values)
     const int useu = (L->unit && L->tune.uscale && L->tune.hot == 0) ? 1 : 0;
     float* ub = u0 ? L->ws + 3 * stride : nullptr;  // u_0 = X0 * dinv (active rows)
-    if (u0 && !u0_fused && (rc = launch_scale_rows(L, L->n_active, Fp, b0, ub, stream))) return rc;
+    if (u0 && !u0_fused && !fold && (rc = launch_scale_rows(L, L->n_active, Fp, b0, ub, stream))) return rc;
     for (int32_t k = K - 1; k >= 1; --k) {
       float* out = bk2 ? bk2 : bufs[nb++];
       const double ck = c[k] - (bk2 == nullptr && k + 2 == K ? c[K] : 0.0);  // implicit b_{k+2} = c_K X0
@@ -512,8 +523,13 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
       cl.uin = useu && (bk1 != b0 || u0);
       cl.uprev = useu && bk2 != nullptr;
       cl.uout = useu;
-      rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? ub : bk1, bk2, out, nullptr, nullptr, 1.0, 0.0, stream,
-                       /*active_only=*/true, nullptr, &cl);
+      if (fold && bk1 == b0) {  // the first launch (fold): X0 in caller order, the internal copy written
+        cl.x0c = X0;
+        cl.x0i = b0;
+        cl.closed = TeamFirst{L->n_active, n, coef, S, H};
+      }
+      rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold ? X0 : ub) : bk1, bk2, out, nullptr, nullptr, 1.0, 0.0,
+                       stream, /*active_only=*/true, nullptr, &cl);
       if (rc) return rc;
       bk2 = const_cast<float*>(bk1 == b0 ? nullptr : bk1);
       bk1 = out;
@@ -524,7 +540,11 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     ClenArgs cl{b0, c0, K == 1 ? c[1] : 1.0, 1};
     cl.uin = useu && (bk1 != b0 || u0);
     cl.uprev = useu && K >= 3;
-    rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? ub : bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
+    if (fold && bk1 == b0) {  // K == 1: the final step is the first launch
+      cl.x0c = X0;
+      cl.closed = TeamFirst{L->n_active, n, coef, S, H};
+    }
+    rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold ? X0 : ub) : bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
                      1.0, 0.0, stream, /*active_only=*/true, fuse_fin ? S : nullptr, &cl);
     if (rc) return rc;
   } else {

@@ -78,6 +78,9 @@ struct TeamPlan {
   uint32_t* warr = nullptr;  // device [n_long]: arrival counters, reset by each row's last arrival
   int32_t n_waves = 0, n_slots = 0, n_long = 0, width = 0;
   int32_t max_parts = 0, npot_rows = 0;  // long rows: most parts; rows whose part count is not a power of 2
+  int64_t n_sell = 0;        // int4 chunks in sell (its padding included)
+  int4* sell0 = nullptr;     // device [n_sell]: sell with caller-row ids (the folded chain's first launch)
+  double* sdinv = nullptr;   // device [4 n_sell]: dinv of each id slot of sell (0 for pads)
   void release();
 };
 
@@ -235,6 +238,9 @@ struct Tuning {
   int32_t sell = 1;          // padded-CSR steps: team waves read their ids in SELL order (step.hip build_sell)
   int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 .. 13:
                              // register-budget / turn-size variants (team.hip launch_team4; all time the same)
+  int32_t fold = 1;          // wg_wavelet_features on the team kernel: no permute-in pass (the first launch
+                             // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
+                             // the closed-form rows; team.hip cheb_team4_first_kernel); 0 = the pass
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
   int64_t team_tail = 8 << 20;  // the hybrid step's tail on the team kernel up to this many entries
   int32_t team_order = -1;   // team.hip: wave dispatch order (0 longest rows first, 1 reversed, 2 .. 7 mixed;
@@ -361,6 +367,14 @@ int get_plan(wg_laplacian_s* L, int LF, int VEC, bool active_only, Plan** out, b
 // Clenshaw form of the heat sum (wavelet_features): a step computes
 //   out = ck * X0 + cacc * (L_hat . xm1) - xm2      (xm2 NULL = 0)
 // into xk (final == 0), or into S [S_out / H] as the finished sum (final == 1).
+// the folded chain's first launch (team.hip cheb_team4_first_kernel): closed-form rows and their outputs
+struct TeamFirst {
+  int64_t closed_from = 0, n_rows = 0;
+  double coef = 0.0;
+  float* S = nullptr;
+  float* H = nullptr;
+};
+
 struct ClenArgs {
   const float* x0;  // X0, internal order, same width / stride as the chain
   double ck;
@@ -369,6 +383,12 @@ struct ClenArgs {
   // unweighted graphs (L->unit): the chain vectors as u = b * dinv (no CSR values read);
   // uin: xm1 is u, uprev: xm2 is u, uout: write u (not on the final step)
   int uin = 0, uprev = 0, uout = 0;
+  // fold (the chain's first launch, team kernel only): gather the caller's X0 (x0c, caller rows) as
+  // u = X0 * dinv on the fly, read the own X0 row at perm[row], write the internal X0 (x0i, read by
+  // the later steps through x0), and finish the closed-form rows (closed.S / closed.H, caller order)
+  const float* x0c = nullptr;
+  float* x0i = nullptr;
+  TeamFirst closed;
 };
 int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const float* xm2, float* xk,
                 float* S, float* H, double alpha0, double alpha_k, hipStream_t stream, bool active_only = false,
@@ -395,7 +415,9 @@ int build_pcol(wg_laplacian_s* L);
 int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32_t* dcol,
                      const int32_t* drsplit, int order, TeamPlan* tp);
 struct StepArgs;
-int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream);
+int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream,
+                 const TeamFirst* first = nullptr);
+int build_team_first(wg_laplacian_s* L, TeamPlan* tp);
 // the value-free VEC-4 gathers on the padded CSR apply to an F-wide (internal width) signal
 bool gather4_applies(const wg_laplacian_s* L, int64_t F);
 int launch_l1_normalize(const float* S, float* H, int64_t n, int64_t F, hipStream_t stream);

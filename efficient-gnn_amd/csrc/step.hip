@@ -958,6 +958,9 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       // workgroup kernel and its tiered plan (Reddit-size F = 41, width 48: 1 / 2 / 4 / 8-way shards
       // 798 / 411 / 224 / 133 us per step with the team tail vs 719 / 367 / 233 / 145; r04 s38)
       const bool team_here = L->tune.team && (!hyb || L->nnz - hyb->dense_nnz <= L->tune.team_tail);
+      const bool fold = cl && cl->x0c;  // the folded chain's first launch (team kernel only)
+      if (fold && !(g4 && team_here && !hyb && f0 == 0))
+        return fail(WG_ERR_INVALID, "launch_step: a folded first launch needs the team kernel");
       if (g4 && team_here) {
         if (!plan->team.wd)
           if (int rc2 = build_team_waves(L, plan->row1, LF, L->tune.team_iter, hyb ? hyb->tcol : L->col,
@@ -968,6 +971,15 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.probe = L->tune.probe;
         a.probe_h2 = L->tune.probe_h2;
         a.probe_fold = L->tune.probe_fold;
+        if (fold) {
+          if (int rc2 = build_team_first(L, &plan->team)) return rc2;
+          a.xm1 = cl->x0c;
+          a.x0c = cl->x0c;
+          a.x0i = cl->x0i;
+          a.perm_in = L->perm;
+          if (int rc2 = launch_team4(plan->team, a, L->tune.team, stream, &cl->closed)) return rc2;
+          continue;
+        }
         if (int rc2 = launch_team4(plan->team, a, L->tune.team, stream)) return rc2;
         continue;
       }

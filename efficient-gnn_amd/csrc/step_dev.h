@@ -62,6 +62,16 @@ struct StepArgs {
   unsigned long long* trace;  // -DWG_TIMING_PROBES, knob "trace": per-wave timeline of one launch
   const int2* wmeta;  // team waves in SELL order (Plan::sell): per wave {first chunk, turns}
   const int4* sell;
+  // the chain's FIRST value-free launch without a permute-in pass (team.hip, tuning key "fold"): the
+  // gathers read the caller's X0 (xm1 = x0c) through ids already mapped to caller rows (sell = the
+  // team table's sell0) and scale each gathered row by its column's dinv (sdinv: one float64 per id
+  // slot), so u_0 = X0 * dinv is never stored; the epilogue reads its own X0 row at caller row
+  // perm_in[row] and writes it to x0i (the internal X0 the later steps read)
+  int32_t first;
+  const double* sdinv;
+  const float* x0c;
+  float* x0i;
+  const int32_t* perm_in;
 };
 
 // a padded-CSR column id whose byte offset (id * row bytes <= 256) lies past every gathered buffer
@@ -164,6 +174,11 @@ __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int
 #pragma unroll
       for (int j = 0; j < VEC; ++j) in.prev[j] = 0.0f;
     }
+    if (a.first) {  // the caller's X0 row (no permute-in pass)
+      in.orow = a.perm_in[row];
+      load_vec<VEC>(a.x0c + (int64_t)in.orow * a.ld + (int64_t)fs * VEC, in.sold);
+      return;
+    }
     load_vec<VEC>(a.x0 + off, in.sold);
     return;
   }
@@ -187,7 +202,18 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] *= -in.dinv;
   }
-  if (in.iso) {  // L_hat_ii = -1 (scipy setdiag(1 - iso), then "- identity")
+  if (a.first) {  // the internal X0 row for the later steps; an isolated row's diagonal term is X0 itself
+    if (a.x0i) {
+      double x[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) x[j] = (double)in.sold[j];
+      store_vec<VEC>(a.x0i + off, x);
+    }
+    if (in.iso) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] -= (double)in.sold[j];
+    }
+  } else if (in.iso) {  // L_hat_ii = -1 (scipy setdiag(1 - iso), then "- identity")
     float x[VEC];
     if (a.k == 1) {
 #pragma unroll
@@ -605,9 +631,28 @@ __device__ __forceinline__ void sum_turn(const u32x4_t* x, int n, double (&acc)[
 
 // CPT: chunks per turn (2: a turn of 8 gathers, a single chunk last when the count is odd; 1:
 // turns of 4 gathers and fewer live registers)
-template <int CPT = 2>
+// FIRST: u_0 = X0 * dinv on the fly: each gathered 16-B slice x of caller row perm[c] becomes
+// fl32(x * dinv[c]) (scale_rows' rounding, so the sums are the permute-in path's bit for bit); the
+// chunk's 4 dinv values (32 B per chunk at twice its id offset) are loaded with its gathers
+__device__ __forceinline__ void scale_chunk(const __amdgpu_buffer_rsrc_t& rd, uint32_t off, u32x4_t* x) {
+  const u32x4_t d01 = __builtin_amdgcn_raw_buffer_load_b128(rd, 2u * off, 0, 0);
+  const u32x4_t d23 = __builtin_amdgcn_raw_buffer_load_b128(rd, 2u * off + 16u, 0, 0);
+  const double d[4] = {__hiloint2double((int)d01.y, (int)d01.x), __hiloint2double((int)d01.w, (int)d01.z),
+                       __hiloint2double((int)d23.y, (int)d23.x), __hiloint2double((int)d23.w, (int)d23.z)};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    x[u].x = __float_as_uint((float)((double)__uint_as_float(x[u].x) * d[u]));
+    x[u].y = __float_as_uint((float)((double)__uint_as_float(x[u].y) * d[u]));
+    x[u].z = __float_as_uint((float)((double)__uint_as_float(x[u].z) * d[u]));
+    x[u].w = __float_as_uint((float)((double)__uint_as_float(x[u].w) * d[u]));
+  }
+}
+
+template <int CPT = 2, bool FIRST = false>
 __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int G, int g, int fs, double (&acc)[4]) {
   if (wm.y <= 0) return;
+  const __amdgpu_buffer_rsrc_t rd =  // FIRST only (unused otherwise)
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.sdinv), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xm1), 0,
                                                                       (int)a.u_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(const_cast<int4*>(a.sell), 0, 0x7fffffff,
@@ -634,6 +679,7 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
       u32x4_t x[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) x[u] = gather(cc[u]);
+      if constexpr (FIRST) scale_chunk(rd, off - cstep, x);
       sum_turn(x, 4, acc);
       c0 = n0;
     }
@@ -648,6 +694,10 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
     u32x4_t x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) x[u] = gather(cc[u]);
+    if constexpr (FIRST) {
+      scale_chunk(rd, off - 2 * cstep, x);
+      scale_chunk(rd, off - cstep, x + 4);
+    }
 #ifdef WG_TIMING_PROBES
     if (a.probe_h2 == -6) {  // one more id-load instruction per turn (its cost through the address unit)
       const u32x4_t e = ld(off + 2 * cstep);
@@ -666,6 +716,7 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
     u32x4_t x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) x[u] = gather(cc[u]);
+    if constexpr (FIRST) scale_chunk(rd, off, x);
     sum_turn(x, 4, acc);
   }
 }

@@ -37,12 +37,63 @@ struct TeamArgs {
   int32_t n_waves;
   double* wpart;   // [slots][LF * 4] float64 partials of part waves
   uint32_t* warr;  // [long rows] arrival counters (0 between launches: the last arrival resets)
+  // the first launch of a folded chain (a.first) also finishes the purely isolated rows [closed_from,
+  // n_rows) in closed form, S = coef * X0 and H = S / (|S|_1 + 1e-8) at their caller rows (what the
+  // permute-in pass did), in n_closed_waves extra waves after the table's
+  int32_t n_closed_waves;
+  int64_t closed_from, n_rows;
+  double coef;
+  float* cS;
+  float* cH;
 };
+
+constexpr int kClosedRG = 4;  // row groups per closed-form wave (their loads all issued before any use)
+
+// rows [closed_from, n_rows): one LF-lane sub-group per row, kClosedRG groups of G rows per wave
+__device__ __forceinline__ void closed_wave(const TeamArgs& t, int64_t cw) {
+  const StepArgs& a = t.a;
+  const int lane = threadIdx.x & 63;
+  const int LF = a.LF;
+  const int G = 64 / LF;
+  const int sg = lane / LF;
+  const int fs = lane - sg * LF;
+  int64_t rows[kClosedRG], rs[kClosedRG];
+  bool act[kClosedRG];
+  float x[kClosedRG][4];
+#pragma unroll
+  for (int q = 0; q < kClosedRG; ++q) {
+    rows[q] = t.closed_from + (cw * kClosedRG + q) * G + sg;
+    act[q] = sg < G && rows[q] < t.n_rows;
+    rs[q] = act[q] ? a.perm_in[rows[q]] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < kClosedRG; ++q)
+    if (act[q]) load_vec<4>(a.x0c + rs[q] * a.ld + fs * 4, x[q]);
+#pragma unroll
+  for (int q = 0; q < kClosedRG; ++q) {
+    double sv[4];
+    double part = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sv[j] = t.coef * (double)x[q][j];
+      part += fabs(sv[j]);
+    }
+    double tot = 0.0;  // the row's L1 norm, in column order (finalize_kernel's order)
+    for (int r = 0; r < LF; ++r) tot += __shfl(part, sg * LF + r, 64);
+    if (!act[q]) continue;
+    const double den = tot + 1e-8;
+    double h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[j] = sv[j] / den;
+    store_vec<4>(t.cS + rs[q] * a.ld + fs * 4, sv);
+    store_vec<4>(t.cH + rs[q] * a.ld + fs * 4, h);
+  }
+}
 
 // MINW: minimum waves per SIMD the registers are held to (6 = the natural 77 VGPRs); LATE: the
 // epilogue's X0 / previous-row operands loaded after the gathers instead of before (fewer live
 // registers in the loop)
-template <bool LATE, int CPT>
+template <bool LATE, int CPT, bool FIRST = false>
 __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
   const StepArgs& a = t.a;
 #ifdef WG_TIMING_PROBES
@@ -73,7 +124,7 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
 #endif
   if (active) {
     if (!LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
-    accumulate_sell<CPT>(a, int2{d0.x, d0.y}, G, sg, fs, acc);
+    accumulate_sell<CPT, FIRST>(a, int2{d0.x, d0.y}, G, sg, fs, acc);
     if (LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
   }
   reduce_subgroups<4>(acc, LN, LF, team * LN * LF, fs);  // every lane (shuffles)
@@ -123,11 +174,54 @@ __global__ __launch_bounds__(256, MINW) void cheb_team4_kernel(TeamArgs t) {
   if (w < t.n_waves) team_wave<LATE, CPT>(t, w);
 }
 
+// the first launch of a folded chain (no permute-in pass): gathers of the caller's X0 scaled by
+// dinv, the internal X0 written by the epilogues, and the closed-form rows after the table's waves
+__global__ __launch_bounds__(256, 6) void cheb_team4_first_kernel(TeamArgs t) {
+  const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w < t.n_waves) team_wave<false, 2, true>(t, w);
+  else if (w < t.n_waves + t.n_closed_waves) closed_wave(t, w - t.n_waves);
+}
+
 }  // namespace
 
 void TeamPlan::release() {
-  for (void* q : {(void*)wd, (void*)sell, (void*)wpart, (void*)warr}) (void)hipFree(q);
+  for (void* q : {(void*)wd, (void*)sell, (void*)wpart, (void*)warr, (void*)sell0, (void*)sdinv}) (void)hipFree(q);
   *this = TeamPlan{};
+}
+
+// The first launch's id table (fold): the SELL ids mapped to caller rows (perm) and each id slot's
+// dinv (float64; 0 for pads, whose gathers return 0)
+int build_team_first(wg_laplacian_s* L, TeamPlan* tp) {
+  if (tp->sell0) return WG_OK;
+  if (!tp->sell || tp->n_sell <= 0) return fail(WG_ERR_INVALID, "team first: no wave table");
+  std::vector<int4> sell(tp->n_sell);
+  WG_HIP_TRY(hipMemcpy(sell.data(), tp->sell, sizeof(int4) * sell.size(), hipMemcpyDeviceToHost));
+  std::vector<int32_t> perm(L->n_rows);
+  std::vector<double> dinv(L->n_cols);
+  if (L->n_rows) WG_HIP_TRY(hipMemcpy(perm.data(), L->perm, sizeof(int32_t) * perm.size(), hipMemcpyDeviceToHost));
+  if (L->n_cols) WG_HIP_TRY(hipMemcpy(dinv.data(), L->dinv, sizeof(double) * dinv.size(), hipMemcpyDeviceToHost));
+  std::vector<double> sd(sell.size() * 4, 0.0);
+  for (size_t i = 0; i < sell.size(); ++i) {
+    int32_t* id = &sell[i].x;
+    for (int j = 0; j < 4; ++j) {
+      if (id[j] == kPadCol) continue;
+      if (id[j] < 0 || id[j] >= L->n_rows) return fail(WG_ERR_INVALID, "team first: column %d outside the rows", id[j]);
+      sd[4 * i + j] = dinv[id[j]];
+      id[j] = perm[id[j]];
+    }
+  }
+  int rc = dmalloc(&tp->sell0, sell.size());
+  if (!rc) rc = dmalloc(&tp->sdinv, sd.size());
+  if (!rc && (hipMemcpy(tp->sell0, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice) ||
+              hipMemcpy(tp->sdinv, sd.data(), sizeof(double) * sd.size(), hipMemcpyHostToDevice)))
+    rc = fail(WG_ERR_HIP, "team first: upload failed");
+  if (rc) {
+    (void)hipFree(tp->sell0);
+    (void)hipFree(tp->sdinv);
+    tp->sell0 = nullptr;
+    tp->sdinv = nullptr;
+  }
+  return rc;
 }
 
 // The wave table and SELL ids of the rows [0, n) of L's operator (internal order, rows by
@@ -258,6 +352,7 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
     wd.swap(o);
   }
   tp->n_waves = (int32_t)(wd.size() / 2);
+  tp->n_sell = (int64_t)sell.size();
   tp->n_slots = slots;
   tp->n_long = longs;
   tp->width = LF * 4;
@@ -273,8 +368,7 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
   return rc;
 }
 
-int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream) {
-  if (tp.n_waves <= 0) return WG_OK;
+int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t stream, const TeamFirst* first) {
   TeamArgs t{};
   t.a = a;
   t.wd = tp.wd;
@@ -282,6 +376,27 @@ int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t
   t.wpart = tp.wpart;
   t.warr = tp.warr;
   t.a.sell = tp.sell;
+  if (first) {  // the folded chain's first launch
+    if (!tp.sell0 || a.LF * 4 > 64 * 4) return fail(WG_ERR_INVALID, "launch_team4: no first-launch table");
+    const int G = 64 / a.LF;
+    t.a.first = 1;
+    t.a.sell = tp.sell0;
+    t.a.sdinv = tp.sdinv;
+    t.closed_from = first->closed_from;
+    t.n_rows = first->n_rows;
+    t.coef = first->coef;
+    t.cS = first->S;
+    t.cH = first->H;
+    const int64_t nc = std::max<int64_t>(0, first->n_rows - first->closed_from);
+    t.n_closed_waves = (int32_t)ceil_div(nc, (int64_t)G * kClosedRG);
+    if (nc && (!t.cS || !t.cH)) return fail(WG_ERR_INVALID, "launch_team4: closed-form rows need S and H");
+    const int64_t nw = (int64_t)tp.n_waves + t.n_closed_waves;
+    if (nw <= 0) return WG_OK;
+    hipLaunchKernelGGL(cheb_team4_first_kernel, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, stream, t);
+    WG_LAUNCH_CHECK();
+    return WG_OK;
+  }
+  if (tp.n_waves <= 0) return WG_OK;
   const dim3 grid((unsigned)ceil_div(tp.n_waves, 4)), block(256);
   switch (variant) {
     case 7: hipLaunchKernelGGL((cheb_team4_kernel<7, false>), grid, block, 0, stream, t); break;

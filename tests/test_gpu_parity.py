@@ -922,3 +922,31 @@ def test_split_row_counters_reset(team):
     ref = O.graph_wavelet_features(g.to_scipy(), k=16, s=0.8, X0=X, return_all=True)
     assert_parity(_np(first), ref["S"], what=f"split rows team={team} S")
     L.close()
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 16])
+def test_fold_first_launch(K):
+    """No permute-in pass (tuning key fold, default on): the chain's first
+    team-kernel launch gathers the caller's X0 through caller-row ids scaled by
+    dinv on the fly, reads its own X0 rows through perm, writes the internal X0
+    for the later steps and finishes the closed-form rows.  u_0 is rounded as
+    the pass rounded it, so S / H equal the permute-in path's bit for bit
+    (K = 1: the final step is the first launch; K = 2 / 3: the implicit b_K
+    branches), and both equal the oracle -- on the arxiv-size graph (45 % closed
+    rows) and with no closed rows."""
+    g = named_graph("ogbn-arxiv")
+    for gg in (g, connect_isolated(g, seed=7)):
+        X = np.random.default_rng(K).standard_normal((gg.n, 40)).astype(np.float32)
+        L = NormalizedLaplacian.from_graph(gg)
+        out = {}
+        for fold in (1, 0):
+            L.tune(fold=fold)
+            H, S = wats_hip.graph_wavelet_features(L, k=K, X0=torch.from_numpy(X), return_S=True)
+            torch.cuda.synchronize()
+            out[fold] = (_np(S), _np(H))
+        assert "team:" in L.describe(40)
+        assert np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][1], out[0][1]), "fold changed S / H"
+        ref = O.graph_wavelet_features(gg.to_scipy(), k=K, s=0.8, X0=X, return_all=True)
+        assert_parity(out[1][0], ref["S"], what=f"fold K={K} S")
+        assert_parity(out[1][1], ref["H"], what=f"fold K={K} H")
+        L.close()
