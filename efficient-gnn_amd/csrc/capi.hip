@@ -228,7 +228,8 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
     L->tune.team_order = (int32_t)value;
   } else if (!strcmp(key, "fold")) {
-    L->tune.fold = value ? 1 : 0;
+    if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "fold must be 0, 1 or 2");
+    L->tune.fold = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "team_iter")) {
     if (value < 8 || value > 4096) return fail(WG_ERR_INVALID, "team_iter must be in [8, 4096]");
@@ -477,7 +478,9 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
   // closed-form rows (team.hip cheb_team4_first_kernel): arxiv-size F = 40 -19.6 us of pass per chain
   const bool fold = u0_fused && g4 && !tp0 && L->tune.fold && L->tune.team && L->tune.uscale &&
                     pick_vec(F, {X0, b0, b1, sint, S, H}) == 4;
-  int rc = fold ? WG_OK
+  const bool fold2 = fold && L->tune.fold == 2;  // a pass writes u_0 (internal order) only
+  int rc = fold2 ? launch_permute_u0(L, F, X0, L->ws + 3 * stride, stream)
+           : fold ? WG_OK
            : fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, u0_fused ? L->ws + 3 * stride : nullptr,
                                                  stream)
                       : launch_permute_pad(L, F, Fp, X0, b0, stream);
@@ -526,9 +529,9 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
       if (fold && bk1 == b0) {  // the first launch (fold): X0 in caller order, the internal copy written
         cl.x0c = X0;
         cl.x0i = b0;
-        cl.closed = TeamFirst{L->n_active, n, coef, S, H};
+        cl.closed = TeamFirst{L->n_active, n, coef, S, H, !fold2};
       }
-      rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold ? X0 : ub) : bk1, bk2, out, nullptr, nullptr, 1.0, 0.0,
+      rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold && !fold2 ? X0 : ub) : bk1, bk2, out, nullptr, nullptr, 1.0, 0.0,
                        stream, /*active_only=*/true, nullptr, &cl);
       if (rc) return rc;
       bk2 = const_cast<float*>(bk1 == b0 ? nullptr : bk1);
@@ -542,9 +545,9 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     cl.uprev = useu && K >= 3;
     if (fold && bk1 == b0) {  // K == 1: the final step is the first launch
       cl.x0c = X0;
-      cl.closed = TeamFirst{L->n_active, n, coef, S, H};
+      cl.closed = TeamFirst{L->n_active, n, coef, S, H, !fold2};
     }
-    rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold ? X0 : ub) : bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
+    rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold && !fold2 ? X0 : ub) : bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
                      1.0, 0.0, stream, /*active_only=*/true, fuse_fin ? S : nullptr, &cl);
     if (rc) return rc;
   } else {

@@ -240,7 +240,8 @@ struct Tuning {
                              // register-budget / turn-size variants (team.hip launch_team4; all time the same)
   int32_t fold = 1;          // wg_wavelet_features on the team kernel: no permute-in pass (the first launch
                              // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
-                             // the closed-form rows; team.hip cheb_team4_first_kernel); 0 = the pass
+                             // the closed-form rows; team.hip cheb_team4_first_kernel); 2 = a pass writes
+                             // u_0 only (the first launch gathers it; the rest as 1); 0 = the full pass
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
   int64_t team_tail = 8 << 20;  // the hybrid step's tail on the team kernel up to this many entries
   int32_t team_order = -1;   // team.hip: wave dispatch order (0 longest rows first, 1 reversed, 2 .. 7 mixed;
@@ -373,6 +374,7 @@ struct TeamFirst {
   double coef = 0.0;
   float* S = nullptr;
   float* H = nullptr;
+  bool gather_x0 = true;  // gathers of the caller's X0 scaled by dinv (else of u_0, from a pass)
 };
 
 struct ClenArgs {
@@ -404,6 +406,7 @@ bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const 
 // permute-in that also writes the closed-form rows' S and H in the caller's order
 // u: also u_0 = X0 * dinv of the active rows (or nullptr); zero (a row shard's second exchange
 // slot): the closed rows' u rows zeroed in u and in zero
+int launch_permute_u0(wg_laplacian_s* L, int64_t F, const float* src, float* u, hipStream_t stream);
 int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
                              float* H, float* u, hipStream_t stream, float* zero = nullptr);
 // caller rows (stride F) -> internal rows (stride Fp), pad columns zeroed

@@ -422,7 +422,7 @@ __global__ __launch_bounds__(kBlock) void permute_in_closed_kernel(int64_t n, in
         part += fabs(sv[j]);
       }
       if (!closed) {
-        store_vec<VEC>(dst + row * F + fs * VEC, sv);
+        if (dst) store_vec<VEC>(dst + row * F + fs * VEC, sv);  // (fold 2: u_0 only)
         if (u) {  // u_0 = X0 * dinv for the first value-free step (scale_rows_kernel's rounding)
           const double di = dinv[row];
           double uv[VEC];
@@ -972,8 +972,10 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.probe_h2 = L->tune.probe_h2;
         a.probe_fold = L->tune.probe_fold;
         if (fold) {
-          if (int rc2 = build_team_first(L, &plan->team)) return rc2;
-          a.xm1 = cl->x0c;
+          if (cl->closed.gather_x0) {
+            if (int rc2 = build_team_first(L, &plan->team)) return rc2;
+            a.xm1 = cl->x0c;
+          }
           a.x0c = cl->x0c;
           a.x0i = cl->x0i;
           a.perm_in = L->perm;
@@ -1122,6 +1124,22 @@ bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const 
   int64_t max_tile = 64 * (int64_t)vec;
   if (L->tune.tile_f > 0) max_tile = std::max<int64_t>(vec, std::min<int64_t>(max_tile, L->tune.tile_f / vec * vec));
   return F <= max_tile;
+}
+
+// u_0 = X0 * dinv of the active rows only, internal order (fold 2)
+int launch_permute_u0(wg_laplacian_s* L, int64_t F, const float* src, float* u, hipStream_t stream) {
+  const int64_t n = L->n_active;
+  if (n == 0) return WG_OK;
+  if (F % 4) return fail(WG_ERR_INVALID, "permute_u0: F %% 4 != 0");
+  const int LF = (int)(F / 4);
+  if (LF > 64) return fail(WG_ERR_INVALID, "permute_u0: F too wide");
+  const int G = 64 / LF;
+  constexpr int kRG = 4;
+  const dim3 grid((unsigned)ceil_div(n, 4 * G * kRG));
+  hipLaunchKernelGGL((permute_in_closed_kernel<4, kRG>), grid, dim3(kBlock), 0, stream, n, F, LF, L->perm, src,
+                     (float*)nullptr, n, 0.0, (float*)nullptr, (float*)nullptr, L->dinv, u, (int64_t)0, (float*)nullptr);
+  WG_LAUNCH_CHECK();
+  return WG_OK;
 }
 
 int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,

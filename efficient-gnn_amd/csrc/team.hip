@@ -176,9 +176,11 @@ __global__ __launch_bounds__(256, MINW) void cheb_team4_kernel(TeamArgs t) {
 
 // the first launch of a folded chain (no permute-in pass): gathers of the caller's X0 scaled by
 // dinv, the internal X0 written by the epilogues, and the closed-form rows after the table's waves
+// GX: the gathers read the caller's X0 scaled by dinv (fold 1); else u_0 from a pass (fold 2)
+template <bool GX>
 __global__ __launch_bounds__(256, 6) void cheb_team4_first_kernel(TeamArgs t) {
   const int w = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w < t.n_waves) team_wave<false, 2, true>(t, w);
+  if (w < t.n_waves) team_wave<false, 2, GX>(t, w);
   else if (w < t.n_waves + t.n_closed_waves) closed_wave(t, w - t.n_waves);
 }
 
@@ -377,11 +379,14 @@ int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t
   t.warr = tp.warr;
   t.a.sell = tp.sell;
   if (first) {  // the folded chain's first launch
-    if (!tp.sell0 || a.LF * 4 > 64 * 4) return fail(WG_ERR_INVALID, "launch_team4: no first-launch table");
+    const bool gx = first->gather_x0;
+    if (gx && !tp.sell0) return fail(WG_ERR_INVALID, "launch_team4: no first-launch table");
     const int G = 64 / a.LF;
     t.a.first = 1;
-    t.a.sell = tp.sell0;
-    t.a.sdinv = tp.sdinv;
+    if (gx) {
+      t.a.sell = tp.sell0;
+      t.a.sdinv = tp.sdinv;
+    }
     t.closed_from = first->closed_from;
     t.n_rows = first->n_rows;
     t.coef = first->coef;
@@ -392,7 +397,8 @@ int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t
     if (nc && (!t.cS || !t.cH)) return fail(WG_ERR_INVALID, "launch_team4: closed-form rows need S and H");
     const int64_t nw = (int64_t)tp.n_waves + t.n_closed_waves;
     if (nw <= 0) return WG_OK;
-    hipLaunchKernelGGL(cheb_team4_first_kernel, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, stream, t);
+    if (gx) hipLaunchKernelGGL(cheb_team4_first_kernel<true>, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, stream, t);
+    else hipLaunchKernelGGL(cheb_team4_first_kernel<false>, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, stream, t);
     WG_LAUNCH_CHECK();
     return WG_OK;
   }

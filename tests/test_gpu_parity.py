@@ -901,6 +901,8 @@ def test_split_row_counters_reset(team):
     g = rmat_graph(30000, 600000, seed=11)
     L = NormalizedLaplacian.from_graph(g)
     L.tune(team=team)
+    if not team:   # the workgroup kernel: rows over 384 entries split into chunks of 192
+        L.tune(block_iter=16, chunk_iter=8)
     X = np.random.default_rng(7).standard_normal((g.n, 40)).astype(np.float32)
     Xt = torch.from_numpy(X)
     first = None
