@@ -238,6 +238,9 @@ struct Tuning {
   int32_t sell = 1;          // padded-CSR steps: team waves read their ids in SELL order (step.hip build_sell)
   int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 .. 13:
                              // register-budget / turn-size variants (team.hip launch_team4; all time the same)
+  int32_t prod = 0;          // wg_wavelet_features on the team kernel: the heat-kernel polynomial as a product
+                             // of quadratic factors (capi.hip prod_factors): 2 own-row streams per step
+                             // instead of Clenshaw's 3; 0 = Clenshaw
   int32_t fold = 1;          // wg_wavelet_features on the team kernel: no permute-in pass (the first launch
                              // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
                              // the closed-form rows; team.hip cheb_team4_first_kernel); 2 = a pass writes
@@ -385,6 +388,10 @@ struct ClenArgs {
   // unweighted graphs (L->unit): the chain vectors as u = b * dinv (no CSR values read);
   // uin: xm1 is u, uprev: xm2 is u, uout: write u (not on the final step)
   int uin = 0, uprev = 0, uout = 0;
+  // the product-form chain (capi.hip, tuning key "prod"): out = ck * X0' + cacc * (L_hat b) + cprev * b''
+  // with X0' = x0 read as u (divided by dinv) when x0u; x0 == nullptr: no X0 term at all
+  double cprev = -1.0;
+  int x0u = 0;
   // fold (the chain's first launch, team kernel only): gather the caller's X0 (x0c, caller rows) as
   // u = X0 * dinv on the fly, read the own X0 row at perm[row], write the internal X0 (x0i, read by
   // the later steps through x0), and finish the closed-form rows (closed.S / closed.H, caller order)

@@ -72,6 +72,7 @@ struct Lds1Args {
   int32_t k;
   double alpha0;
   double alpha_k;
+  int32_t probe_fold;  // -DWG_TIMING_PROBES, hub teams: tail columns folded into [hub, hub + probe_fold)
 };
 
 // T_k,i = 2 (L_hat T_{k-1})_i - T_{k-2,i}  (k == 1: T_1 = L_hat T_0), S, u_k.
@@ -194,6 +195,9 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
   const int32_t* __restrict__ rp = a.brp;
   const int32_t gs = a.gshift;
   auto x_of = [&](int32_t c) {
+#ifdef WG_TIMING_PROBES
+    if (a.probe_fold > 0 && c >= H && c != kPadCol) c = H + ((c - H) & (a.probe_fold - 1));
+#endif
     const float xl = u[min(c, H)];
     const uint32_t off = c >= H ? (uint32_t)(c - gs) * 4u : kDrop;
     const float xg = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
@@ -1211,6 +1215,7 @@ int launch_lds1_step(wg_laplacian_s* L, Lds1Plan* p, int32_t k, const float* u_k
   a.k = k;
   a.alpha0 = alpha0;
   a.alpha_k = alpha_k;
+  a.probe_fold = L->tune.probe_fold;
   if (p->mode == 4) {
     if (int rc = ensure_dyn_lds((const void*)cheb_hub1_kernel, 160 * 1024 - 64)) return rc;
     a.brp = L->rowptr;

@@ -934,9 +934,11 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       if (cl) {  // Clenshaw: the generic (k >= 2) paths, S written only by the final step
         a.k = 2;
         a.clen = cl->final_ ? 2 : 1;
-        a.x0 = cl->x0 + f0;
+        a.x0 = cl->x0 ? cl->x0 + f0 : nullptr;
         a.ck = cl->ck;
         a.cacc = cl->cacc;
+        a.cprev = cl->cprev;
+        a.x0u = cl->x0u;
         if (!cl->final_) a.S = nullptr;
         a.dinv = L->dinv;
         a.uin = cl->uin;

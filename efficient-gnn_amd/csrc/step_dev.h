@@ -35,7 +35,9 @@ struct StepArgs {
   int32_t vidx;
   int32_t clen;        // 0 = forward recurrence + heat sum; 1 / 2 = Clenshaw step / final (ClenArgs)
   const float* x0;     // Clenshaw: X0 rows (internal order, stride ld)
-  double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc - xm2
+  double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc + cprev * xm2 (cprev -1; x0 nullable: no X0 term)
+  double cprev;
+  int32_t x0u;         // x0 holds u = x * dinv (the product form's own row of the gathered vector)
   // Clenshaw on unweighted graphs (L_hat_ij = -dinv_i dinv_j): the chain carries u = b * dinv, so the
   // gathers need no values (val == nullptr: every value 1).  uin: xm1 holds u; uprev: xm2 holds u;
   // uout: xk gets u.
@@ -179,7 +181,12 @@ __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int
       load_vec<VEC>(a.x0c + (int64_t)in.orow * a.ld + (int64_t)fs * VEC, in.sold);
       return;
     }
-    load_vec<VEC>(a.x0 + off, in.sold);
+    if (a.x0) {
+      load_vec<VEC>(a.x0 + off, in.sold);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) in.sold[j] = 0.0f;
+    }
     return;
   }
   load_vec<VEC>((a.k == 1 ? a.xm1 : a.xm2) + off, in.prev);
@@ -226,11 +233,12 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
     for (int j = 0; j < VEC; ++j) acc[j] -= (double)x[j] * xs;
   }
   double t[VEC];
-  if (a.clen) {  // Clenshaw: b = ck * X0 + cacc * (L_hat b') - b''
+  if (a.clen) {  // Clenshaw: b = ck * X0 + cacc * (L_hat b') - b'' (product form: cprev, x0u)
     const double ps = a.uprev ? 1.0 / in.dinv : 1.0;
+    const double xs0 = a.x0u ? 1.0 / in.dinv : 1.0;
 #pragma unroll
     for (int j = 0; j < VEC; ++j)
-      t[j] = a.ck * (double)in.sold[j] + a.cacc * acc[j] - (double)in.prev[j] * ps;
+      t[j] = a.ck * ((double)in.sold[j] * xs0) + a.cacc * acc[j] + a.cprev * ((double)in.prev[j] * ps);
     if (a.uout && a.xk) {
       double u[VEC];
 #pragma unroll
