@@ -31,6 +31,8 @@ def main():
     for k, cs in acc.items():
         out[k] = {c: sum(v) / len(v) for c, v in cs.items()}
         out[k]["dispatches"] = max(len(v) for v in cs.values())
+        # per counter: FETCH_SIZE and WRITE_SIZE (separate passes) must cover the same dispatch set
+        out[k]["dispatches_per_counter"] = {c: len(v) for c, v in cs.items()}
     text = json.dumps(out, indent=1, sort_keys=True)
     if a.out:
         with open(a.out, "w") as fh:
