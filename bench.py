@@ -651,7 +651,10 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
-        prof = L.profile_collect() if profile else None
+        prof = None
+        if profile:
+            d = L.profile_durations()
+            prof = dict(sum_ms=sum(d), launches=len(d), max_ms=max(d) if d else 0.0, durations=d)
         L.profile_enable(False)
         ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) if evs else []
         return t1 - t0, prof, ms[len(ms) // 2] if ms else None
@@ -670,6 +673,19 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
         elapsed = _allreduce(elapsed, dist.ReduceOp.MAX, device)
         edges_k = _allreduce(edges_k, dist.ReduceOp.SUM, device)
     avg_ms = prof["sum_ms"] / max(1, prof["launches"])
+    # the folded chain (tuning key fold): each pass's first launch is
+    # cheb_team4_first_kernel, which also does the former permute-in pass's work; the roofline is
+    # the dominant kernel's (cheb_team4_kernel, the other K - 1 launches, as rocprof averages it)
+    team_path = F > 1 and "team:" in L.describe(F)
+    folded = team_path and unit and F % 4 == 0 and K >= 2 and prof["launches"] == args.steps * K and \
+        int((getattr(args, "tune", None) or {}).get("fold", 1)) == 1
+    first_us = None
+    if folded:
+        d = prof["durations"]
+        first = [d[i] for i in range(len(d)) if i % K == 0]
+        plain = [d[i] for i in range(len(d)) if i % K != 0]
+        first_us = sum(first) / len(first) * 1e3
+        avg_ms = sum(plain) / len(plain)
     one_launch_chain = F == 1 and "chain1:" in L.describe(1)
     if one_launch_chain:   # csrc/chain.hip: one launch runs all K steps: per step = / K
         avg_ms /= K
@@ -690,7 +706,7 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
     traffic, traffic_src = None, None
     tj = args.traffic_json
     if tj == "auto":
-        tj = os.path.join(REPO, "profiles", "r04", "s48_traffic.json") \
+        tj = os.path.join(REPO, "profiles", "r05", "s5_traffic.json") \
             if (config == "ogbn-arxiv" and F == 40 and K == 16) else None
     if tj and tj != "none" and os.path.exists(tj):
         traffic = json.load(open(tj)).get("bytes_per_launch")
@@ -724,8 +740,9 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_source": (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction: "
-                               f"an upper bound) + WRITE_SIZE per launch of this kernel on this workload"
+            "traffic_source": (f"{traffic_src}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950's 128-B requests counted "
+                               f"as 64 B; TCC_EA0_RDREQ_128B x 128 B agrees within 0.4 %) + WRITE_SIZE per launch "
+                               f"of this kernel on this workload"
                                if traffic is not None else None),
             "kernel": lds_kernel_name(lds_info, one_launch_chain, "team:" in L.describe(F)),
             "byte_model": _byte_model(lds_info) if lds_info else
@@ -747,6 +764,13 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
             "avg_launch_us": avg_ms * 1e3,
             "max_launch_us": prof["max_ms"] * 1e3,
             "launches": prof["launches"],
+            "first_launch_us": first_us,
+            "all_launches_avg_us": prof["sum_ms"] / max(1, prof["launches"]) * 1e3,
+            "launch_note": ("avg_launch_us / achieved / frac: the K - 1 plain step launches of each pass "
+                            "(cheb_team4_kernel, the dominant kernel as rocprof averages it); first_launch_us: "
+                            "each pass's first launch (cheb_team4_first_kernel: also reads the caller's X0 "
+                            "through perm, writes the internal X0 and the closed-form rows' S / H -- the former "
+                            "permute-in pass)") if folded else None,
         },
         "chain_ms": prof["sum_ms"] / args.steps,
         "median_step_ms_profiled": median_ms,

@@ -814,6 +814,20 @@ int wg_profile_collect(wg_laplacian_t L, double* sum_ms, int64_t* launches, doub
   return WG_OK;
 }
 
+int wg_profile_durations(wg_laplacian_t L, double* ms, int64_t cap, int64_t* n) {
+  if (!L || !n || (cap > 0 && !ms)) return fail(WG_ERR_INVALID, "wg_profile_durations: NULL argument");
+  const int64_t have = (int64_t)(L->ev_used / 2);
+  for (int64_t i = 0; i < have && i < cap; ++i) {
+    WG_HIP_TRY(hipEventSynchronize(L->ev[2 * i + 1]));
+    float t = 0.0f;
+    WG_HIP_TRY(hipEventElapsedTime(&t, L->ev[2 * i], L->ev[2 * i + 1]));
+    ms[i] = (double)t;
+  }
+  *n = have;
+  L->ev_used = 0;
+  return WG_OK;
+}
+
 int wg_row_l1_normalize(const float* S, float* H, int64_t n_rows, int64_t F, void* stream_) {
   if (n_rows < 0 || F < 1 || (n_rows && (!S || !H))) return fail(WG_ERR_INVALID, "wg_row_l1_normalize: bad arguments");
   if (n_rows == 0) return WG_OK;

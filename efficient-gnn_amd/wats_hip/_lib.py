@@ -63,6 +63,7 @@ SIGNATURES = {
     "wg_laplacian_describe": (ctypes.c_char_p, [c_vp, c_i64]),
     "wg_laplacian_set_halo_groups": (ctypes.c_int, [c_vp, c_i32, c_vp]),
     "wg_profile_enable": (ctypes.c_int, [c_vp, c_i32]),
+    "wg_profile_durations": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_i64, ctypes.POINTER(c_i64)]),
     "wg_profile_collect": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_i64),
                                           ctypes.POINTER(ctypes.c_double)]),
     "wg_row_l1_normalize": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_vp]),

@@ -272,6 +272,13 @@ class NormalizedLaplacian:
               "profile_collect")
         return dict(sum_ms=s.value, launches=n.value, max_ms=m.value)
 
+    def profile_durations(self, cap: int = 1 << 16) -> list:
+        """Synchronise on the recorded events -> each launch's ms, in launch order; resets."""
+        buf = (ctypes.c_double * cap)()
+        n = ctypes.c_int64(0)
+        check(_lib.load().wg_profile_durations(self.handle, buf, cap, ctypes.byref(n)), "profile_durations")
+        return [buf[i] for i in range(min(n.value, cap))]
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.load().wg_laplacian_destroy(self._h)

@@ -277,6 +277,10 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F);
 int wg_profile_enable(wg_laplacian_t L, int32_t enable);
 int wg_profile_collect(wg_laplacian_t L, double* sum_ms_host, int64_t* launches_host,
                        double* max_ms_host);
+/* The same events, one duration per launch in launch order (ms_host[i], i < min(cap, *n_host);
+ * *n_host = launches recorded): e.g. a folded chain's first launch apart from its K - 1 plain step
+ * launches.  Synchronous; resets the record like wg_profile_collect. */
+int wg_profile_durations(wg_laplacian_t L, double* ms_host, int64_t cap, int64_t* n_host);
 
 /* a6 standalone: H = S / (||S||_1,row + 1e-8) (calibration/WATS.py:71-72). */
 int wg_row_l1_normalize(const float* S, float* H, int64_t n_rows, int64_t F, void* stream);
