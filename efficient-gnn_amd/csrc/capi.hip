@@ -228,6 +228,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "team_order")) {
     if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
     L->tune.team_order = (int32_t)value;
+  } else if (!strcmp(key, "ucmem")) {
+    if (value < 0 || value > 3) return fail(WG_ERR_INVALID, "ucmem must be in [0, 3]");
+    L->tune.ucmem = (int32_t)value;  // plan-time for the id arrays (plans dropped below)
   } else if (!strcmp(key, "prod")) {
     L->tune.prod = value ? 1 : 0;
     return WG_OK;  // launch-time choice
@@ -554,6 +557,19 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
   const bool fold = u0_fused && g4 && !tp0 && L->tune.fold && L->tune.team && L->tune.uscale &&
                     pick_vec(F, {X0, b0, b1, sint, S, H}) == 4;
   const bool fold2 = fold && L->tune.fold == 2;  // a pass writes u_0 (internal order) only
+  float* x0int = b0;  // the internal X0 the steps read (fold: written by the first launch)
+  if (fold && !fold2 && (L->tune.ucmem & 2)) {
+    const size_t want = (size_t)n * Fp;
+    if (L->x0uc_floats < want) {
+      WG_HIP_TRY(hipStreamSynchronize(stream));
+      (void)hipFree(L->x0uc);
+      L->x0uc = nullptr;
+      L->x0uc_floats = 0;
+      if (int rc0 = dmalloc_uc(&L->x0uc, want)) return rc0;
+      L->x0uc_floats = want;
+    }
+    x0int = L->x0uc;
+  }
   int rc = fold2 ? launch_permute_u0(L, F, X0, L->ws + 3 * stride, stream)
            : fold ? WG_OK
            : fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, u0_fused ? L->ws + 3 * stride : nullptr,
@@ -586,7 +602,7 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
         cl.x0u = x0u;
         if (first) {  // the chain's first launch: gathers the caller's X0 (own_x0 / x0u unused)
           cl.x0c = X0;
-          cl.x0i = b0;
+          cl.x0i = x0int;
           cl.closed = TeamFirst{L->n_active, n, coef, S, H};
           gather = X0;
           first = false;
@@ -599,10 +615,10 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
         // w = L v
         if ((rc = half(vsrc, nullptr, 0, 0.0, 1.0, nullptr, 0, 0.0, W, false))) return rc;
         // v' = f (L w - a w + b v): own w as u (x0u), own v as u (or X0 itself for the first factor)
-        if ((rc = half(W, W, 1, -pf[q].a * fq, fq, q == 0 ? b0 : V, q == 0 ? 0 : 1, pf[q].b * fq, V, last))) return rc;
+        if ((rc = half(W, W, 1, -pf[q].a * fq, fq, q == 0 ? x0int : V, q == 0 ? 0 : 1, pf[q].b * fq, V, last))) return rc;
       } else {
         // v' = f (L v - a v): gathers v, so it writes W, and the two swap
-        if ((rc = half(vsrc, q == 0 ? b0 : V, q == 0 ? 0 : 1, -pf[q].a * fq, fq, nullptr, 0, 0.0, W, last))) return rc;
+        if ((rc = half(vsrc, q == 0 ? x0int : V, q == 0 ? 0 : 1, -pf[q].a * fq, fq, nullptr, 0, 0.0, W, last))) return rc;
         std::swap(V, W);
       }
     }
@@ -645,13 +661,13 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     for (int32_t k = K - 1; k >= 1; --k) {
       float* out = bk2 ? bk2 : bufs[nb++];
       const double ck = c[k] - (bk2 == nullptr && k + 2 == K ? c[K] : 0.0);  // implicit b_{k+2} = c_K X0
-      ClenArgs cl{b0, ck, cacc, 0};
+      ClenArgs cl{x0int, ck, cacc, 0};
       cl.uin = useu && (bk1 != b0 || u0);
       cl.uprev = useu && bk2 != nullptr;
       cl.uout = useu;
       if (fold && bk1 == b0) {  // the first launch (fold): X0 in caller order, the internal copy written
         cl.x0c = X0;
-        cl.x0i = b0;
+        cl.x0i = x0int;
         cl.closed = TeamFirst{L->n_active, n, coef, S, H, !fold2};
       }
       rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold && !fold2 ? X0 : ub) : bk1, bk2, out, nullptr, nullptr, 1.0, 0.0,
@@ -663,7 +679,7 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     }
     // final: S = c_0 X0 + L_hat b_1 - b_2 (K == 1: L_hat b_1 = c_1 L_hat X0; K == 2: b_2 = c_2 X0)
     const double c0 = c[0] - (K == 2 ? c[2] : 0.0);
-    ClenArgs cl{b0, c0, K == 1 ? c[1] : 1.0, 1};
+    ClenArgs cl{x0int, c0, K == 1 ? c[1] : 1.0, 1};
     cl.uin = useu && (bk1 != b0 || u0);
     cl.uprev = useu && K >= 3;
     if (fold && bk1 == b0) {  // K == 1: the final step is the first launch
