@@ -228,9 +228,6 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "team_order")) {
     if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
     L->tune.team_order = (int32_t)value;
-  } else if (!strcmp(key, "ucmem")) {
-    if (value < 0 || value > 3) return fail(WG_ERR_INVALID, "ucmem must be in [0, 3]");
-    L->tune.ucmem = (int32_t)value;  // plan-time for the id arrays (plans dropped below)
   } else if (!strcmp(key, "prod")) {
     L->tune.prod = value ? 1 : 0;
     return WG_OK;  // launch-time choice
@@ -263,6 +260,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;
   } else if (!strcmp(key, "probe_h2")) {
     L->tune.probe_h2 = (int32_t)value;  // negative: the skeleton probes (step.hip, step_dev.h)
+    return WG_OK;
+  } else if (!strcmp(key, "coldnt")) {
+    L->tune.coldnt = (int32_t)std::max<int64_t>(0, value);
     return WG_OK;
   } else if (!strcmp(key, "probe_fold")) {
     L->tune.probe_fold = (int32_t)value;  // -1: ids from one 4-KB window (accumulate_u4)
@@ -558,18 +558,6 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
                     pick_vec(F, {X0, b0, b1, sint, S, H}) == 4;
   const bool fold2 = fold && L->tune.fold == 2;  // a pass writes u_0 (internal order) only
   float* x0int = b0;  // the internal X0 the steps read (fold: written by the first launch)
-  if (fold && !fold2 && (L->tune.ucmem & 2)) {
-    const size_t want = (size_t)n * Fp;
-    if (L->x0uc_floats < want) {
-      WG_HIP_TRY(hipStreamSynchronize(stream));
-      (void)hipFree(L->x0uc);
-      L->x0uc = nullptr;
-      L->x0uc_floats = 0;
-      if (int rc0 = dmalloc_uc(&L->x0uc, want)) return rc0;
-      L->x0uc_floats = want;
-    }
-    x0int = L->x0uc;
-  }
   int rc = fold2 ? launch_permute_u0(L, F, X0, L->ws + 3 * stride, stream)
            : fold ? WG_OK
            : fuse_fin ? launch_permute_in_closed(L, F, X0, b0, coef, S, H, u0_fused ? L->ws + 3 * stride : nullptr,

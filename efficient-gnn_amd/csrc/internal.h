@@ -45,15 +45,6 @@ int dmalloc(T** p, size_t count) {
   WG_HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
   return WG_OK;
 }
-// device memory the GPU does not keep in its L2 (hipDeviceMallocUncached): streams read once per
-// launch, so they do not evict the gathered rows (tuning key "ucmem"); freed with hipFree
-template <typename T>
-int dmalloc_uc(T** p, size_t count) {
-  *p = nullptr;
-  if (count == 0) count = 1;
-  WG_HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(p), count * sizeof(T), hipDeviceMallocUncached));
-  return WG_OK;
-}
 
 // ---------------------------------------------------------------------------
 // Step-kernel launch plan (per signal-tile shape), see step.hip.
@@ -228,6 +219,7 @@ struct Tuning {
   int32_t trace = 0;         // timing only (-DWG_TIMING_PROBES): record the trace-th step launch's per-wave timeline
   int32_t probe_h2 = 0;      // timing only (-DWG_TIMING_PROBES): see StepArgs
   int32_t probe_fold = 0;    // timing only (-DWG_TIMING_PROBES): see StepArgs
+  int32_t coldnt = 0;        // timing only (-DWG_TIMING_PROBES): team gathers of columns >= coldnt non-temporal
   int32_t tile_rg = 1;       // hybrid step, 128-row blocks: 16-row groups per wave (1: 8 waves, 2: 4 waves)
   int32_t tile_mfma = 0;     // hybrid step, 128-row blocks of width 48 / 64: 16 = v_mfma_f32_16x16x32_bf16,
                              // 32 = v_mfma_f32_32x32x16_bf16 (cheb_tiles32_kernel: each B read serves 32
@@ -250,7 +242,6 @@ struct Tuning {
   int32_t prod = 0;          // wg_wavelet_features on the team kernel: the heat-kernel polynomial as a product
                              // of quadratic factors (capi.hip prod_factors): 2 own-row streams per step
                              // instead of Clenshaw's 3; 0 = Clenshaw
-  int32_t ucmem = 0;         // team path: 1 = the SELL id array, 2 = the internal X0 copy in L2-uncached memory
   int32_t fold = 1;          // wg_wavelet_features on the team kernel: no permute-in pass (the first launch
                              // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
                              // the closed-form rows; team.hip cheb_team4_first_kernel); 2 = a pass writes
@@ -350,8 +341,6 @@ struct wg_laplacian_s {
   // workspace for wg_wavelet_features
   float* ws = nullptr;
   size_t ws_floats = 0;
-  float* x0uc = nullptr;      // the folded chain's internal X0 in L2-uncached memory (tuning key ucmem & 2)
-  size_t x0uc_floats = 0;
   // widths F whose plans and workspace wg_wavelet_features has built (at tuning generation
   // warm_gen): only those may run on a stream the caller is capturing
   std::vector<int64_t> warm_widths;

@@ -525,7 +525,7 @@ wg_laplacian_s::~wg_laplacian_s() {
   for (auto& kv : plans) kv.second.release();
   wg::release_lds1(this);
   for (void* p : {(void*)rowptr, (void*)col, (void*)val, (void*)iso, (void*)perm, (void*)iperm, (void*)rowsum,
-                  (void*)ws, (void*)x0uc, (void*)dinv, (void*)prp, (void*)pcol, (void*)trace_buf})
+                  (void*)ws, (void*)dinv, (void*)prp, (void*)pcol, (void*)trace_buf})
     (void)hipFree(p);
 }
 

@@ -54,6 +54,8 @@ struct StepArgs {
   // probe_h2: columns below it gather one aligned 128-B line (lanes of columns 32.. skip);
   // probe_fold: every gathered column folded into [0, probe_fold)
   int32_t probe_h2, probe_fold;
+  int32_t coldnt;  // -DWG_TIMING_PROBES: gathers of columns >= coldnt with the non-temporal hint (the hot rows
+                   // are not evicted by once-used cold lines?), the others plain: two loads, one dropped
   // value-free gathers on the padded CSR (cheb_step_kernel<..., P4 = true>): each row's column ids
   // padded to a multiple of 4 with kPadCol (prp / pcol); the gathered vector xm1 as a raw buffer
   // of u_bytes bytes, so a pad id's offset falls outside it and its load returns 0 with no request
@@ -675,6 +677,15 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
 #ifdef WG_TIMING_PROBES
     if (a.probe_fold > 0 && c != (uint32_t)kPadCol) c &= (uint32_t)(a.probe_fold - 1);
     if (a.probe_h2 == -1) return u32x4_t{c, 0u, 0u, 0u};
+#endif
+#ifdef WG_TIMING_PROBES
+    if (a.coldnt > 0) {
+      const uint32_t off = __umul24(c, rb) + lo;
+      const bool cold = c >= (uint32_t)a.coldnt;
+      const u32x4_t h = __builtin_amdgcn_raw_buffer_load_b128(rs, cold ? 0xFFFFFFF0u : off, 0, 0);
+      const u32x4_t q = __builtin_amdgcn_raw_buffer_load_b128(rs, cold ? off : 0xFFFFFFF0u, 0, 2);
+      return h | q;
+    }
 #endif
     return __builtin_amdgcn_raw_buffer_load_b128(rs, __umul24(c, rb) + lo, 0, 0);
   };

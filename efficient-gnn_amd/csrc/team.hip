@@ -212,8 +212,8 @@ int build_team_first(wg_laplacian_s* L, TeamPlan* tp) {
       id[j] = perm[id[j]];
     }
   }
-  int rc = (L->tune.ucmem & 1) ? dmalloc_uc(&tp->sell0, sell.size()) : dmalloc(&tp->sell0, sell.size());
-  if (!rc) rc = (L->tune.ucmem & 1) ? dmalloc_uc(&tp->sdinv, sd.size()) : dmalloc(&tp->sdinv, sd.size());
+  int rc = dmalloc(&tp->sell0, sell.size());
+  if (!rc) rc = dmalloc(&tp->sdinv, sd.size());
   if (!rc && (hipMemcpy(tp->sell0, sell.data(), sizeof(int4) * sell.size(), hipMemcpyHostToDevice) ||
               hipMemcpy(tp->sdinv, sd.data(), sizeof(double) * sd.size(), hipMemcpyHostToDevice)))
     rc = fail(WG_ERR_HIP, "team first: upload failed");
@@ -359,7 +359,7 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
   tp->n_long = longs;
   tp->width = LF * 4;
   int rc = dmalloc(&tp->wd, std::max<size_t>(wd.size(), 2));
-  if (!rc) rc = (L->tune.ucmem & 1) ? dmalloc_uc(&tp->sell, sell.size()) : dmalloc(&tp->sell, sell.size());
+  if (!rc) rc = dmalloc(&tp->sell, sell.size());
   if (!rc) rc = dmalloc(&tp->wpart, (size_t)std::max(slots, 1) * tp->width);
   if (!rc) rc = dmalloc(&tp->warr, (size_t)std::max(longs, 1));
   if (!rc && ((!wd.empty() && hipMemcpy(tp->wd, wd.data(), sizeof(int4) * wd.size(), hipMemcpyHostToDevice)) ||
