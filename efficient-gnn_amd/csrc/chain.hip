@@ -264,11 +264,12 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
       u[i] = a.u0[c];
     }
   }
+  __shared__ int s_local;
+  if (tid == 0) s_local = 0;
+  __syncthreads();  // the staged rows, ids and passes (and s_local) before any wave reads them
   // chain_l2: every worker publishes its XCD, then reads every worker's; if all share one XCD, the
   // granules are plain stores that stay in that XCD's L2 (the sc1 polls of the same XCD hit it), else
   // write-through as always -- the same choice on every worker, made before any granule is published
-  __shared__ int s_local;
-  if (tid == 0) s_local = 0;
   if (a.l2local && a.P > 1) {
     if (tid == 0) {
       uint32_t xcc;
