@@ -77,6 +77,8 @@ struct ChainArgs {
   float* H;
   uint32_t* xtab;             // [P] l2local handshake: {epoch << 8 | XCC id} per worker
   int32_t l2local;            // tuning key "chain_l2": granules as plain stores when every worker is on one XCD
+  int32_t flat;               // tuning key "chain_flat" (direct mode): each phase gathers every entry of the
+                              // worker at once into LDS (one round trip), then the passes sum from LDS
   double c[kChainMaxK + 1];   // heat coefficients exp(-s k)
 };
 
@@ -221,7 +223,8 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
   const int pass0 = wp[0], npass = wp[kChainWaves] - pass0;
   const int wc0 = a.P == 1 ? 0 : a.wcol_off[w];
   const int nu = a.P == 1 ? a.n_act : a.wcol_off[w + 1] - wc0;       // columns this worker gathers
-  const ChainLayout lay(nu, nr, ne, npass, a.P == 1);
+  const bool flat = a.direct && a.flat;                               // u's LDS slot holds one float per entry
+  const ChainLayout lay(flat ? max(nu, ne) : nu, nr, ne, npass, a.P == 1);
   float* u = reinterpret_cast<float*>(smem);                         // [nu] the gathered u (local ids)
   float* u2 = reinterpret_cast<float*>(smem + lay.u2);               // [n_act] one worker: the next u
   double* dv = reinterpret_cast<double*>(smem + lay.dv);             // [nr] dinv, negative = isolated row
@@ -332,6 +335,21 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
           }
         }
     }
+    if (flat) {  // every entry's granule (u_0 in phase 1), four loads in flight per lane, into LDS
+      for (int e = tid; e < ne; e += 4 * kChainThreads) {
+        int c4[4] = {0, 0, 0, 0};
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (e + i * kChainThreads < ne) c4[n++] = id[e + i * kChainThreads];
+        float x[4];
+        if (!fetch_u(a, gprev, j, want, c4, n, x, deadline)) chain_fail(a, &s_bad, ep);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < n) u[e + i * kChainThreads] = x[i];
+      }
+      __syncthreads();
+    }
     for (int pi = pb; pi < pe; ++pi) {
       const int2 P = pas[pi];
       const int lts = P.y >> 8;
@@ -343,7 +361,19 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
         const bool act = team < (P.y & 0xff);
         const int li = row - row0;
         double s = 0.0;
-        if (act && a.direct) {  // the same four chains, each term a granule (or u_0) from memory
+        if (act && flat) {  // the direct path's four chains in its order, the terms from LDS
+          const int b = lrp[li], e = lrp[li + 1];
+          double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+          int q = b + tl;
+          for (; q + 3 * TS < e; q += 4 * TS) {
+            s += (double)u[q];
+            s1 += (double)u[q + TS];
+            s2 += (double)u[q + 2 * TS];
+            s3 += (double)u[q + 3 * TS];
+          }
+          for (; q < e; q += TS) s += (double)u[q];
+          s = (s + s1) + (s2 + s3);
+        } else if (act && a.direct) {  // the same four chains, each term a granule (or u_0) from memory
           const int b = lrp[li], e = lrp[li + 1];
           double s1 = 0.0, s2 = 0.0, s3 = 0.0;
           int q = b + tl;
@@ -572,7 +602,9 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
         wcol_off[w + 1] = (int32_t)wcols.size();
         nu = (int64_t)cs.size();
       }
-      const ChainLayout lay(nu, r - r0, rp[r] - rp[r0], (int64_t)wps.size(), P == 1);
+      const bool flat = L->tune.chain_direct && L->tune.chain_flat && P > 1;  // one LDS float per entry
+      const ChainLayout lay(flat ? std::max<int64_t>(nu, rp[r] - rp[r0]) : nu, r - r0, rp[r] - rp[r0],
+                            (int64_t)wps.size(), P == 1);
       lds = std::max(lds, (size_t)lay.bytes);
       if (lay.bytes > kChainLds) fits = false;
     }
@@ -724,6 +756,7 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.H = H;
   a.xtab = p->xtab;
   a.l2local = (L->tune.chain_l2 && a.stride == 8 && p->P <= 64) ? 1 : 0;
+  a.flat = L->tune.chain_flat ? 1 : 0;  // the plan's LDS layout was sized with it (plan-shaping key)
   for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
   if (int rc = prof_mark(L, stream, true)) return rc;
   hipLaunchKernelGGL(cheb_chain1_kernel, dim3((unsigned)(p->P * a.stride)), dim3(kChainThreads), (size_t)p->lds_bytes,

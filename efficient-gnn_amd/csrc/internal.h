@@ -232,6 +232,7 @@ struct Tuning {
                              // profiles/r03/s13_chain1_worker_sweep.log)
   int32_t chain_direct = 1;  // chain.hip: gathers read the granules straight from memory (no LDS staging of u)
   int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works; P <= 32)
+  int32_t chain_flat = 0;    // chain.hip direct mode: a phase's gathers all at once into LDS, then sums from LDS
   int32_t chain_l2 = 0;      // chain.hip with chain_xcd: plain granule stores (they stay in that XCD's L2) once a
                              // handshake shows every worker on one XCD, else write-through as always
   int32_t chain_fault = 0;   // chain.hip fault injection (tests of the timeout path): worker 0 does not publish
