@@ -207,11 +207,6 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "chain_direct")) {
     L->tune.chain_direct = value ? 1 : 0;  // also the auto worker count: plans rebuilt
-  } else if (!strcmp(key, "chain_flat")) {
-    L->tune.chain_flat = value ? 1 : 0;  // plan-shaping (the workers' LDS layout): plans dropped below
-  } else if (!strcmp(key, "chain_l2")) {
-    L->tune.chain_l2 = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "chain_xcd")) {
     L->tune.chain_xcd = value ? 1 : 0;
     return WG_OK;  // launch-time choice

@@ -75,10 +75,6 @@ struct ChainArgs {
   int32_t fault_phase;        // fault injection (tuning key "chain_fault", tests): worker 0 skips this phase's publish
   float* S;                   // caller order
   float* H;
-  uint32_t* xtab;             // [P] l2local handshake: {epoch << 8 | XCC id} per worker
-  int32_t l2local;            // tuning key "chain_l2": granules as plain stores when every worker is on one XCD
-  int32_t flat;               // tuning key "chain_flat" (direct mode): each phase gathers every entry of the
-                              // worker at once into LDS (one round trip), then the passes sum from LDS
   double c[kChainMaxK + 1];   // heat coefficients exp(-s k)
 };
 
@@ -223,8 +219,7 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
   const int pass0 = wp[0], npass = wp[kChainWaves] - pass0;
   const int wc0 = a.P == 1 ? 0 : a.wcol_off[w];
   const int nu = a.P == 1 ? a.n_act : a.wcol_off[w + 1] - wc0;       // columns this worker gathers
-  const bool flat = a.direct && a.flat;                               // u's LDS slot holds one float per entry
-  const ChainLayout lay(flat ? max(nu, ne) : nu, nr, ne, npass, a.P == 1);
+  const ChainLayout lay(nu, nr, ne, npass, a.P == 1);
   float* u = reinterpret_cast<float*>(smem);                         // [nu] the gathered u (local ids)
   float* u2 = reinterpret_cast<float*>(smem + lay.u2);               // [n_act] one worker: the next u
   double* dv = reinterpret_cast<double*>(smem + lay.dv);             // [nr] dinv, negative = isolated row
@@ -267,40 +262,7 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
       u[i] = a.u0[c];
     }
   }
-  __shared__ int s_local;
-  if (tid == 0) s_local = 0;
-  __syncthreads();  // the staged rows, ids and passes (and s_local) before any wave reads them
-  // chain_l2: every worker publishes its XCD, then reads every worker's; if all share one XCD, the
-  // granules are plain stores that stay in that XCD's L2 (the sc1 polls of the same XCD hit it), else
-  // write-through as always -- the same choice on every worker, made before any granule is published
-  if (a.l2local && a.P > 1) {
-    if (tid == 0) {
-      uint32_t xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      __hip_atomic_store(a.xtab + w, (ep << 8) | (xcc & 0xffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid < 64) {
-      const uint64_t dl = wall_clock64() + (uint64_t)a.wait_ticks;
-      bool same = true, ok = true;
-      for (int q = tid; q < a.P; q += 64) {
-        uint32_t v = __hip_atomic_load(a.xtab + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((v >> 8) != (ep & 0xffffffu)) {
-          __builtin_amdgcn_s_sleep(1);
-          if (wall_clock64() > dl) {
-            ok = false;
-            break;
-          }
-          v = __hip_atomic_load(a.xtab + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const uint32_t v0 = __hip_atomic_load(a.xtab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((v & 0xffu) != (v0 & 0xffu)) same = false;
-      }
-      const bool all_same = __all(same) && __all(ok);
-      if (tid == 0) s_local = all_same ? 1 : 0;
-    }
-    __syncthreads();
-  }
-  const bool l2local = s_local != 0;
+  __syncthreads();
 #ifdef WG_CHAIN_TRACE  // timing build: worker 0 prints its phase timeline (s_memtime cycles)
   long long tr[2 * kChainMaxK + 4];
   int ntr = 0;
@@ -335,21 +297,6 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
           }
         }
     }
-    if (flat) {  // every entry's granule (u_0 in phase 1), four loads in flight per lane, into LDS
-      for (int e = tid; e < ne; e += 4 * kChainThreads) {
-        int c4[4] = {0, 0, 0, 0};
-        int n = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (e + i * kChainThreads < ne) c4[n++] = id[e + i * kChainThreads];
-        float x[4];
-        if (!fetch_u(a, gprev, j, want, c4, n, x, deadline)) chain_fail(a, &s_bad, ep);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (i < n) u[e + i * kChainThreads] = x[i];
-      }
-      __syncthreads();
-    }
     for (int pi = pb; pi < pe; ++pi) {
       const int2 P = pas[pi];
       const int lts = P.y >> 8;
@@ -361,19 +308,7 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
         const bool act = team < (P.y & 0xff);
         const int li = row - row0;
         double s = 0.0;
-        if (act && flat) {  // the direct path's four chains in its order, the terms from LDS
-          const int b = lrp[li], e = lrp[li + 1];
-          double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-          int q = b + tl;
-          for (; q + 3 * TS < e; q += 4 * TS) {
-            s += (double)u[q];
-            s1 += (double)u[q + TS];
-            s2 += (double)u[q + 2 * TS];
-            s3 += (double)u[q + 3 * TS];
-          }
-          for (; q < e; q += TS) s += (double)u[q];
-          s = (s + s1) + (s2 + s3);
-        } else if (act && a.direct) {  // the same four chains, each term a granule (or u_0) from memory
+        if (act && a.direct) {  // the same four chains, each term a granule (or u_0) from memory
           const int b = lrp[li], e = lrp[li + 1];
           double s1 = 0.0, s2 = 0.0, s3 = 0.0;
           int q = b + tl;
@@ -420,10 +355,8 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
             const float un = bad ? __int_as_float(0x7fc00000) : (float)(t * di);
             cu[li] = un;
             if (a.P == 1) u2[row] = un;
-            else if (!(j == a.fault_phase && w == 0)) {
-              if (l2local) gnext[row] = tag | __float_as_uint(un);  // one 8-B store: stays in this XCD's L2
-              else __hip_atomic_store(gnext + row, tag | __float_as_uint(un), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            else if (!(j == a.fault_phase && w == 0))
+              __hip_atomic_store(gnext + row, tag | __float_as_uint(un), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           } else {
             const int32_t r = a.perm[row];
             const float nan = __int_as_float(0x7fc00000);
@@ -602,9 +535,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
         wcol_off[w + 1] = (int32_t)wcols.size();
         nu = (int64_t)cs.size();
       }
-      const bool flat = L->tune.chain_direct && L->tune.chain_flat && P > 1;  // one LDS float per entry
-      const ChainLayout lay(flat ? std::max<int64_t>(nu, rp[r] - rp[r0]) : nu, r - r0, rp[r] - rp[r0],
-                            (int64_t)wps.size(), P == 1);
+      const ChainLayout lay(nu, r - r0, rp[r] - rp[r0], (int64_t)wps.size(), P == 1);
       lds = std::max(lds, (size_t)lay.bytes);
       if (lay.bytes > kChainLds) fits = false;
     }
@@ -639,7 +570,6 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   if (!rc) rc = upload(&p->wpass, wpass);
   if (!rc) rc = upload(&p->passes, passes);
   if (!rc) rc = dmalloc(&p->bar, 4);
-  if (!rc) rc = dmalloc(&p->xtab, 64);
   if (!rc) rc = dmalloc(&p->gbuf, (size_t)4 * p->ustride);
   if (!rc) rc = dmalloc(&p->u0, (size_t)std::max<int64_t>(na, 1));
   if (!rc) rc = dmalloc(&p->x0, (size_t)std::max<int64_t>(na, 1));
@@ -650,7 +580,6 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   WG_HIP_TRY(hipHostGetDevicePointer((void**)&p->d_host_flag, p->host_flag, 0));
   p->seen = 0;
   WG_HIP_TRY(hipMemset(p->bar, 0, 4 * sizeof(int32_t)));
-  WG_HIP_TRY(hipMemset(p->xtab, 0xff, 64 * sizeof(uint32_t)));  // no epoch matches
   WG_HIP_TRY(hipMemset(p->gbuf, 0, 4 * p->ustride * sizeof(uint64_t)));  // tag 0: never a live phase's
   char buf[192];
   snprintf(buf, sizeof(buf), "chain1: one launch per chain, %d workers x %d threads, %lld active rows, %lld nonzeros, "
@@ -664,7 +593,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
 
 void ChainPlan::release() {
   for (void* q : {(void*)ids, (void*)wcols, (void*)wcol_off, (void*)gids, (void*)bcols, (void*)bcol_off, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar,
-                  (void*)gbuf, (void*)u0, (void*)x0, (void*)xtab})
+                  (void*)gbuf, (void*)u0, (void*)x0})
     (void)hipFree(q);
   if (host_flag) (void)hipHostFree(host_flag);
   if (done) (void)hipEventDestroy(done);
@@ -754,9 +683,6 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.fault_phase = L->tune.chain_fault;
   a.S = S;
   a.H = H;
-  a.xtab = p->xtab;
-  a.l2local = (L->tune.chain_l2 && a.stride == 8 && p->P <= 64) ? 1 : 0;
-  a.flat = L->tune.chain_flat ? 1 : 0;  // the plan's LDS layout was sized with it (plan-shaping key)
   for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
   if (int rc = prof_mark(L, stream, true)) return rc;
   hipLaunchKernelGGL(cheb_chain1_kernel, dim3((unsigned)(p->P * a.stride)), dim3(kChainThreads), (size_t)p->lds_bytes,

@@ -232,9 +232,6 @@ struct Tuning {
                              // profiles/r03/s13_chain1_worker_sweep.log)
   int32_t chain_direct = 1;  // chain.hip: gathers read the granules straight from memory (no LDS staging of u)
   int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works; P <= 32)
-  int32_t chain_flat = 0;    // chain.hip direct mode: a phase's gathers all at once into LDS, then sums from LDS
-  int32_t chain_l2 = 0;      // chain.hip with chain_xcd: plain granule stores (they stay in that XCD's L2) once a
-                             // handshake shows every worker on one XCD, else write-through as always
   int32_t chain_fault = 0;   // chain.hip fault injection (tests of the timeout path): worker 0 does not publish
                              // phase chain_fault; the launch's S / H come out NaN and the next call fails
   int32_t gather4 = 21;      // value-free VEC-4 steps on the padded CSR (step.hip build_pcol / accumulate_u4):
@@ -275,7 +272,6 @@ struct ChainPlan {
   int32_t* wpass = nullptr;   // device [P][17]: each worker's waves' ranges of passes
   int2* passes = nullptr;     // device: one wave pass {first row, rows | log2 team size << 8}
   int32_t* bar = nullptr;     // device [4]: [2] epoch of the last timed-out launch, [3] launch epoch
-  uint32_t* xtab = nullptr;   // device [64]: the chain_l2 handshake (epoch << 8 | XCC id per worker)
   int32_t* host_flag = nullptr;    // host-mapped (pinned): epoch of the last timed-out launch
   int32_t* d_host_flag = nullptr;  // its device address
   int32_t seen = 0;                // the host_flag value already reported

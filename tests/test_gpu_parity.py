@@ -978,34 +978,3 @@ def test_product_form_chain(K):
         assert np.abs(_np(H) - ref["H"])[big].max() <= 1e-6
         L.close()
 
-
-@pytest.mark.parametrize("wg,flat", [(8, 0), (32, 0), (32, 1), (16, 1)])
-def test_chain1_l2_local(wg, flat):
-    """chain_xcd + chain_l2: the one-launch chain's workers placed on one XCD hand their granules
-    over through that XCD's L2 (plain stores, sc1 polls) once a start-of-launch handshake shows every
-    worker on the same XCD (else write-through as always): the same sums in the same order, so S / H
-    are bitwise those of the write-through hand-off, and equal the oracle; repeated launches stable.
-    chain_flat: each phase gathers all the worker's entries at once into LDS, then sums them there
-    in the direct path's order (bitwise the same again)."""
-    g = rmat_graph(19717, 88648, seed=4)
-    L = NormalizedLaplacian.from_graph(g)
-    X = np.random.default_rng(wg).standard_normal((g.n, 1)).astype(np.float32)
-    out = {}
-    for l2 in (0, 1):
-        L.tune(chain_wg=wg, chain_xcd=1, chain_l2=l2, chain_flat=flat)
-        for _ in range(3):
-            H, S = wats_hip.graph_wavelet_features(L, k=16, s=0.8, X0=torch.from_numpy(X), return_S=True)
-            torch.cuda.synchronize()
-            assert "chain1:" in L.describe(1) and not L.chain_status()
-            out.setdefault(l2, []).append((_np(S), _np(H)))
-    for l2 in (0, 1):
-        for S, H in out[l2]:
-            assert np.array_equal(S, out[0][0][0]) and np.array_equal(H, out[0][0][1])
-    if flat:   # the same worker count without flat gathers: the same sums
-        L.tune(chain_wg=wg, chain_xcd=1, chain_l2=0, chain_flat=0)
-        H0, S0 = wats_hip.graph_wavelet_features(L, k=16, s=0.8, X0=torch.from_numpy(X), return_S=True)
-        torch.cuda.synchronize()
-        assert np.array_equal(_np(S0), out[0][0][0])
-    ref = O.graph_wavelet_features(g.to_scipy(), k=16, s=0.8, X0=X, return_all=True)
-    assert_parity(out[1][0][0], ref["S"], what=f"chain1 l2-local P={wg} S")
-    L.close()
