@@ -921,9 +921,11 @@ def main():
             picked_other = None
         line["metric"] = (f"Chebyshev SpMM-chain edges*K/s ({cfg}-size, K={line['config']['K']}, F="
                           f"{line['config']['F']}, row-sharded over {world} GPUs)")
-        line["headline_note"] = ("N > 1 headline: BASELINE.json configs[3] (Reddit-size, 1-D row-sharded, RCCL "
-                                 "halo exchange); the N = 1 line carries the same run at one rank as `sharded`; "
-                                 "same_config_1gpu: the same config unsharded on one GPU")
+        line["headline_note"] = ("N > 1 headline: BASELINE.json configs[3] (Reddit-size, 1-D row-sharded, halo "
+                                 f"exchange '{line['config'].get('exchange')}': the faster of the IPC pull and RCCL "
+                                 "grouped send/recv whose check passed, exchange_compare); the N = 1 line carries "
+                                 "the same run at one rank as `sharded`; same_config_1gpu: the same config "
+                                 "unsharded on one GPU")
         try:
             torch.cuda.empty_cache()
             line["same_config_1gpu"] = one_gpu_chain(cfg, args.K, args.F, args.steps, args.seed, args.s, device,
