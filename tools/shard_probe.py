@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--config", default="reddit")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--ranks", default="", help="comma-separated ranks to probe one after another (one graph)")
     ap.add_argument("--lds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--F", type=int, default=1, help="signal width (F > 1: the gather kernel at this width)")
@@ -41,6 +42,12 @@ def main():
     indptr = ip.cpu().numpy()
     deg = np.diff(indptr).astype(np.float32)
     b = partition_rows(indptr, a.world)
+    for rk in ([int(x) for x in a.ranks.split(",")] if a.ranks else [a.rank]):
+        a.rank = rk
+        one_rank(a, b, ip, ix, indptr, deg, dev, K)
+
+
+def one_rank(a, b, ip, ix, indptr, deg, dev, K):
     r0, r1 = int(b[a.rank]), int(b[a.rank + 1])
     cols = ix[int(indptr[r0]):int(indptr[r1])].to(torch.int64)
     # the shard as wats_hip.dist builds it: [own | halo], halo grouped by owner, each group in
@@ -64,13 +71,15 @@ def main():
     if a.groups and a.world > 1:
         offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
         check(_lib.load().wg_laplacian_set_halo_groups(L.handle, a.world, offs.ctypes.data), "set_halo_groups")
-    del ip, ix, cols, local
+    del cols, local
     lib = _lib.load()
     for knobs in (a.grid.split(";") if a.grid else [""]):
         kv = dict(lds=a.lds)
         kv.update({x.split("=")[0]: int(x.split("=")[1]) for x in knobs.split(",") if x})
         L.tune(**kv)
         probe(L, lib, n_own, n_cols, K, a, dev, kv)
+    L.close()
+    torch.cuda.empty_cache()
 
 
 def probe(L, lib, n_own, n_cols, K, a, dev, kv):
