@@ -205,6 +205,8 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < 0 || value > kChainMaxK) return fail(WG_ERR_INVALID, "chain_fault must be in [0, %d]", kChainMaxK);
     L->tune.chain_fault = (int32_t)value;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "chain_solo")) {
+    L->tune.chain_solo = value ? 1 : 0;  // plans rebuilt
   } else if (!strcmp(key, "chain_direct")) {
     L->tune.chain_direct = value ? 1 : 0;  // also the auto worker count: plans rebuilt
   } else if (!strcmp(key, "chain_xcd")) {
@@ -260,6 +262,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;
   } else if (!strcmp(key, "probe_h2")) {
     L->tune.probe_h2 = (int32_t)value;  // negative: the skeleton probes (step.hip, step_dev.h)
+    return WG_OK;
+  } else if (!strcmp(key, "probe_ns")) {
+    L->tune.probe_ns = (int32_t)value;
     return WG_OK;
   } else if (!strcmp(key, "coldnt")) {
     L->tune.coldnt = (int32_t)std::max<int64_t>(0, value);

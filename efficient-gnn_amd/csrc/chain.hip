@@ -402,6 +402,175 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
 #endif
 }
 
+
+// ---- solo: the whole chain in ONE workgroup, no exchange at all.  PubMed-size
+// graphs do not fit one workgroup's LDS with their 16-bit ids (177 KB for 88.6 k entries), so the
+// chain above runs 128 workers and pays two Infinity-Cache trips per phase.  Here the ids live in
+// the 1024 threads' REGISTERS (E entries per thread, two per VGPR: column | row-end bit 15), and LDS
+// holds only u (every active row, plus a zero pad column), X0, the rows' float64 sums and one carry
+// per thread.  A phase is two passes and two workgroup barriers:
+//   pass 1: thread t sums u over its E consecutive entries (row order, balanced), blocks of loads
+//           issued before their sums; at a row end the sum goes to rsum[row]; what is left (the
+//           start of a row that continues in the next thread) goes to carry[t];
+//   pass 2: rows t + 1024 m (R per thread) run the Clenshaw epilogue of cheb_chain1_kernel on
+//           rsum; a row that began in earlier threads is finished by the thread of its end:
+//           carry[cs .. t - 1] in thread order, then its own part (deterministic).
+// The host orders each row segment's entries so that the 32 lanes of a read group hit distinct
+// LDS banks where they can (build_solo_plan).  One workgroup: no co-residency, no wait, no timeout.
+constexpr int kSoloBlock = 16;  // pass 1: loads issued per block before their sums
+constexpr int kSoloMaxR = 10;   // rows per thread (<= 10 240 active rows; LDS caps it lower)
+
+struct SoloArgs {
+  int32_t n_act;
+  int32_t K;
+  int32_t off_x0, off_rsum, off_carry;  // LDS byte offsets
+  const uint32_t* ids;                  // [E / 2][threads]
+  const int32_t* row0;
+  const int32_t* crow;
+  const int32_t* cs;
+  const uint8_t* cont;
+  const double* dinv;
+  const uint8_t* iso;
+  const int32_t* perm;
+  const float* x0;  // [n_act] internal X0 (chain_prologue_kernel)
+  const float* u0;  // [n_act] u_0 = X0 * dinv
+  float* S;
+  float* H;
+  double c[kChainMaxK + 1];
+};
+
+template <int E>
+__device__ __forceinline__ uint32_t solo_entry(const uint32_t (&w)[E / 2], int q) {
+  return (q & 1) ? (w[q >> 1] >> 16) : (w[q >> 1] & 0xffffu);
+}
+
+template <int E, int R>
+__global__ __launch_bounds__(kChainThreads) void cheb_chain_solo_kernel(SoloArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int na = a.n_act;
+  float* u = reinterpret_cast<float*>(smem);                        // [na + 1] u of the previous phase
+  float* x0 = reinterpret_cast<float*>(smem + a.off_x0);            // [na]
+  double* rsum = reinterpret_cast<double*>(smem + a.off_rsum);      // [na] the rows' sums of a phase
+  double* carry = reinterpret_cast<double*>(smem + a.off_carry);    // [threads] the unfinished row's part
+  uint32_t idw[E / 2];
+#pragma unroll
+  for (int q = 0; q < E / 2; ++q) idw[q] = a.ids[q * kChainThreads + t];
+  // per own row, float32 to keep the ids in registers: dinv (negative: isolated row), 1 / dinv
+  // (negative: a continued row, finished by the thread of its end), u two phases back
+  float dsi[R], rdi[R], pu[R];
+#pragma unroll
+  for (int m = 0; m < R; ++m) {
+    const int i = t + m * kChainThreads;
+    dsi[m] = 0.0f;
+    rdi[m] = 0.0f;
+    pu[m] = 0.0f;
+    if (i < na) {
+      const double di = a.dinv[i];
+      dsi[m] = a.iso[i] ? -(float)di : (float)di;
+      rdi[m] = (float)((a.cont[i] ? -1.0 : 1.0) / di);
+    }
+  }
+  const int crow = a.crow[t], cs = a.cs[t];
+  float cdsi = 0.0f, crdi = 0.0f, cpu = 0.0f;
+  if (crow >= 0) {
+    const double di = a.dinv[crow];
+    cdsi = a.iso[crow] ? -(float)di : (float)di;
+    crdi = (float)(1.0 / di);
+  }
+  for (int i = t; i < na; i += kChainThreads) {
+    u[i] = a.u0[i];
+    x0[i] = a.x0[i];
+  }
+  if (t == 0) u[na] = 0.0f;  // the pad column
+  const int row0 = a.row0[t];
+  __syncthreads();
+  const int K = a.K;
+  for (int j = 1; j <= K; ++j) {
+    const int k = K - j;  // cheb_chain1_kernel's phase coefficients
+    const double cacc = (j == 1) ? (k == 0 ? a.c[K] : 2.0 * a.c[K]) : (k == 0 ? 1.0 : 2.0);
+    const double ck = a.c[k] - (j == 2 ? a.c[K] : 0.0);
+    const bool prevs = j >= 3;
+    double acc = 0.0;
+    int row = row0;
+    // the decoded addresses and row-end flags must not be hoisted out of the phase loop (E more
+    // live registers): the words are opaque to the compiler once per phase
+#pragma unroll
+    for (int q = 0; q < E / 2; ++q) asm volatile("" : "+v"(idw[q]));
+    // likewise the own rows' float64 operands and LDS addresses (pass 2): recomputed per phase
+    int tp = t;
+    asm volatile("" : "+v"(tp));
+#pragma unroll
+    for (int m = 0; m < R; ++m) asm volatile("" : "+v"(dsi[m]), "+v"(rdi[m]));
+#pragma unroll
+    for (int b = 0; b < E; b += kSoloBlock) {
+      float x[kSoloBlock];
+#pragma unroll
+      for (int q = 0; q < kSoloBlock; ++q) x[q] = u[solo_entry<E>(idw, b + q) & 0x7fffu];
+#pragma unroll
+      for (int q = 0; q < kSoloBlock; ++q) {
+        acc += (double)x[q];
+        if (solo_entry<E>(idw, b + q) & 0x8000u) {
+          rsum[row] = acc;
+          ++row;
+          acc = 0.0;
+        }
+      }
+    }
+    carry[t] = acc;
+    __syncthreads();  // every sum and carry of the phase written, every read of u done
+    auto epi = [&](int i, double s, float ds, float rdf, float& p) {
+      const double di = fabs((double)ds);
+      const double rd = (double)rdf;
+      const float ui = u[i];  // this row's u of the previous phase
+      double lb = -di * s;
+      if (ds < 0.0f) lb -= (double)ui * rd;  // isolated row: L_hat_ii = -1
+      const double tt = ck * (double)x0[i] + cacc * lb - (prevs ? (double)p * rd : 0.0);
+      if (k > 0) {
+        p = ui;
+        u[i] = (float)(tt * di);
+      } else {
+        const int32_t r = a.perm[i];
+        a.S[r] = (float)tt;
+        a.H[r] = (float)(tt / (fabs(tt) + 1e-8));
+      }
+    };
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const int i = tp + m * kChainThreads;
+      if (i < na && rdi[m] > 0.0f) epi(i, rsum[i], dsi[m], rdi[m], pu[m]);
+    }
+    if (crow >= 0) {
+      double s = 0.0;
+      for (int q = cs; q < t; ++q) s += carry[q];
+      s += rsum[crow];
+      epi(crow, s, cdsi, crdi, cpu);
+    }
+    if (k == 0) break;
+    __syncthreads();  // the phase's u written before the next phase reads it
+  }
+}
+
+// the instantiation for (E, R) (build_solo_plan picks E from these)
+const void* solo_kernel(int E, int R) {
+  if (R > 8) {
+    switch (E) {
+      case 16: return (const void*)cheb_chain_solo_kernel<16, kSoloMaxR>;
+      case 32: return (const void*)cheb_chain_solo_kernel<32, kSoloMaxR>;
+      case 64: return (const void*)cheb_chain_solo_kernel<64, kSoloMaxR>;
+      case 96: return (const void*)cheb_chain_solo_kernel<96, kSoloMaxR>;
+      default: return nullptr;
+    }
+  }
+  switch (E) {
+    case 16: return (const void*)cheb_chain_solo_kernel<16, 8>;
+    case 32: return (const void*)cheb_chain_solo_kernel<32, 8>;
+    case 64: return (const void*)cheb_chain_solo_kernel<64, 8>;
+    case 96: return (const void*)cheb_chain_solo_kernel<96, 8>;
+    default: return nullptr;
+  }
+}
+
 template <typename T>
 int upload(T** d, const std::vector<T>& h) {
   if (int rc = dmalloc(d, h.size())) return rc;
@@ -433,6 +602,185 @@ void make_passes(const std::vector<int32_t>& rp, int64_t r0, int64_t r1, std::ve
   }
 }
 
+
+// The solo plan (cheb_chain_solo_kernel), or WG_ERR_UNSUPPORTED when the graph does not fit one
+// workgroup: u, X0 and the float64 sums of every active row in LDS, <= 96 entries and <= 10 rows per
+// thread.  Entries in row order, an empty row as one pad entry (so that every row has an end),
+// split evenly over the threads.  Within each (thread, row) segment the entries may be summed in any
+// order; slot by slot, a read group's 32 lanes (threads 32 g ..) take, fewest choices first, the
+// entry whose LDS bank (column mod 32) has the fewest distinct columns so far -- the same column is a
+// broadcast, free (MI355X_MICROARCH.md, LDS: ds_read_b32 serves two groups of 32 lanes, one cycle
+// per extra distinct address on a bank).
+int build_solo_plan(wg_laplacian_s* L, ChainPlan* p, const std::vector<int32_t>& rp, const std::vector<uint16_t>& ids) {
+  const int64_t na = L->n_active;
+  const int T = kChainThreads;
+  if (na < 1 || na + 1 >= 0x8000) return WG_ERR_UNSUPPORTED;
+  auto al = [](int64_t x) { return (x + 15) & ~(int64_t)15; };
+  const int64_t off_x0 = al(4 * (na + 1)), off_rsum = al(off_x0 + 4 * na), off_carry = al(off_rsum + 8 * na);
+  const int64_t lds = al(off_carry + 8 * T);
+  if (lds > kChainLds) return WG_ERR_UNSUPPORTED;
+  const int R = (int)((na + T - 1) / T);
+  if (R > kSoloMaxR) return WG_ERR_UNSUPPORTED;
+  std::vector<uint16_t> ecol;
+  std::vector<int32_t> erow;
+  std::vector<int64_t> rfirst(na), rlast(na);
+  ecol.reserve(rp[na] + na);
+  erow.reserve(rp[na] + na);
+  for (int64_t r = 0; r < na; ++r) {
+    rfirst[r] = (int64_t)ecol.size();
+    if (rp[r + 1] == rp[r]) {
+      ecol.push_back((uint16_t)na);
+      erow.push_back((int32_t)r);
+    }
+    for (int64_t e = rp[r]; e < rp[r + 1]; ++e) {
+      ecol.push_back(ids[e]);
+      erow.push_back((int32_t)r);
+    }
+    rlast[r] = (int64_t)ecol.size() - 1;
+  }
+  const int64_t ne = (int64_t)ecol.size();
+  const int64_t per = (ne + T - 1) / T;
+  int E = 0;
+  for (int e : {16, 32, 64, 96})  // (128 entries spill registers)
+    if (per <= e) {
+      E = e;
+      break;
+    }
+  if (!E) return WG_ERR_UNSUPPORTED;
+  std::vector<int64_t> B(T + 1);
+  for (int t = 0; t <= T; ++t) B[t] = ne * t / T;
+  std::vector<int32_t> row0(T, 0), crow(T, -1), cs(T, 0);
+  std::vector<uint8_t> cont(na, 0);
+  for (int t = 0; t < T; ++t) {
+    if (B[t] == B[t + 1]) continue;
+    const int32_t r = erow[B[t]];
+    row0[t] = r;
+    if (rfirst[r] < B[t] && rlast[r] < B[t + 1]) {  // a row that began in earlier threads ends here
+      crow[t] = r;
+      cont[r] = 1;
+      cs[t] = (int32_t)(std::upper_bound(B.begin(), B.end(), rfirst[r]) - B.begin()) - 1;
+    }
+  }
+  // slots[t][q]: column | row-end bit; pads (past a thread's entries) read the zero pad column
+  std::vector<uint16_t> slots((size_t)T * E, (uint16_t)na);
+  int64_t cyc_plain = 0, cyc_sched = 0;  // LDS cycles of pass 1 (sum over slots and groups of the worst bank)
+  for (int g = 0; g < T / 32; ++g) {
+    struct Seg {
+      int64_t b, e;  // entry range [b, e) of one (thread, row) piece
+      bool end;      // the row ends in it
+    };
+    std::vector<std::vector<Seg>> segs(32);
+    for (int l = 0; l < 32; ++l) {
+      const int t = 32 * g + l;
+      for (int64_t x = B[t]; x < B[t + 1];) {
+        int64_t y = x;
+        while (y < B[t + 1] && erow[y] == erow[x]) ++y;
+        segs[l].push_back(Seg{x, y, rlast[erow[x]] == y - 1});
+        x = y;
+      }
+    }
+    // plain order: the cycles the schedule is measured against
+    for (int q = 0; q < E; ++q) {
+      int load[32] = {0};
+      std::vector<uint16_t> seen;
+      for (int l = 0; l < 32; ++l) {
+        const int t = 32 * g + l;
+        const uint16_t c = B[t] + q < B[t + 1] ? ecol[B[t] + q] : (uint16_t)na;
+        if (std::find(seen.begin(), seen.end(), c) != seen.end()) continue;
+        seen.push_back(c);
+        ++load[c & 31];
+      }
+      cyc_plain += *std::max_element(load, load + 32);
+    }
+    std::vector<std::vector<uint16_t>> pool(32);
+    std::vector<size_t> si(32, 0);
+    std::vector<int64_t> pos(32, 0);  // slots filled
+    for (int q = 0; q < E; ++q) {
+      int load[32] = {0};
+      std::vector<uint16_t> seen;
+      std::vector<int> order;
+      for (int l = 0; l < 32; ++l) {
+        if (pool[l].empty() && si[l] < segs[l].size()) {  // the lane's next segment
+          const Seg& sg = segs[l][si[l]];
+          pool[l].assign(ecol.begin() + sg.b, ecol.begin() + sg.e);
+        }
+        order.push_back(l);
+      }
+      std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        const size_t px = pool[x].empty() ? 0 : pool[x].size(), py = pool[y].empty() ? 0 : pool[y].size();
+        return px < py;
+      });
+      for (int l : order) {
+        const int t = 32 * g + l;
+        uint16_t c = (uint16_t)na;
+        if (!pool[l].empty()) {
+          size_t best = 0;
+          int bc = 1 << 30;
+          for (size_t i = 0; i < pool[l].size(); ++i) {
+            const uint16_t ci = pool[l][i];
+            const int cost = std::find(seen.begin(), seen.end(), ci) != seen.end() ? -1 : load[ci & 31];
+            if (cost < bc) {
+              bc = cost;
+              best = i;
+            }
+          }
+          c = pool[l][best];
+          pool[l][best] = pool[l].back();
+          pool[l].pop_back();
+          uint16_t v = c;
+          if (pool[l].empty()) {  // the segment's last slot carries the row end
+            if (segs[l][si[l]].end) v |= 0x8000;
+            ++si[l];
+          }
+          slots[(size_t)t * E + q] = v;
+          ++pos[l];
+        }
+        if (std::find(seen.begin(), seen.end(), c) == seen.end()) {
+          seen.push_back(c);
+          ++load[c & 31];
+        }
+      }
+      cyc_sched += *std::max_element(load, load + 32);
+    }
+    for (int l = 0; l < 32; ++l)
+      if (pos[l] != B[32 * g + l + 1] - B[32 * g + l]) return fail(WG_ERR_INVALID, "solo plan: slots lost");
+  }
+  std::vector<uint32_t> w((size_t)(E / 2) * T);
+  for (int t = 0; t < T; ++t)
+    for (int q = 0; q < E / 2; ++q)
+      w[(size_t)q * T + t] = (uint32_t)slots[(size_t)t * E + 2 * q] | ((uint32_t)slots[(size_t)t * E + 2 * q + 1] << 16);
+  const void* kern = solo_kernel(E, R);
+  if (!kern) return WG_ERR_UNSUPPORTED;
+  if (int rc = ensure_dyn_lds(kern, kChainLds)) return rc;
+  p->P = 1;
+  p->n_act = (int32_t)na;
+  p->lds_bytes = (int32_t)lds;
+  p->solo_E = E;
+  p->solo_R = R;
+  p->ustride = (int32_t)((na + 63) / 64 * 64);
+  int rc = upload(&p->sids, w);
+  if (!rc) rc = upload(&p->srow0, row0);
+  if (!rc) rc = upload(&p->scrow, crow);
+  if (!rc) rc = upload(&p->scs, cs);
+  if (!rc) rc = upload(&p->scont, cont);
+  if (!rc) rc = dmalloc(&p->bar, 4);
+  if (!rc) rc = dmalloc(&p->u0, (size_t)na);
+  if (!rc) rc = dmalloc(&p->x0, (size_t)na);
+  if (rc) return rc;
+  WG_HIP_TRY(hipMemset(p->bar, 0, 4 * sizeof(int32_t)));
+  WG_HIP_TRY(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
+  WG_HIP_TRY(hipHostMalloc((void**)&p->host_flag, sizeof(int32_t), hipHostMallocMapped));
+  *p->host_flag = 0;
+  WG_HIP_TRY(hipHostGetDevicePointer((void**)&p->d_host_flag, p->host_flag, 0));
+  p->seen = 0;
+  char buf[256];
+  snprintf(buf, sizeof(buf), "chain1: one launch per chain, 1 workers x %d threads (solo: %d entries and %d rows per "
+           "thread in registers), %lld active rows, %lld nonzeros, LDS %d B; pass-1 LDS cycles %lld (plain order %lld)\n",
+           T, E, R, (long long)na, (long long)rp[na], p->lds_bytes, (long long)cyc_sched, (long long)cyc_plain);
+  p->text = buf;
+  return WG_OK;
+}
+
 int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   const int64_t na = L->n_active;
   std::vector<int32_t> rp(na + 1);
@@ -444,6 +792,11 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   for (int64_t e = 0; e < nnz; ++e) {
     if (col[e] < 0 || col[e] >= na) return fail(WG_ERR_INVALID, "chain plan: column %d outside the active rows", col[e]);
     ids[e] = (uint16_t)col[e];
+  }
+  if (L->tune.chain_solo && L->tune.chain_wg <= 0) {  // one workgroup, ids in registers, when it fits
+    const int rc = build_solo_plan(L, p, rp, ids);
+    if (rc != WG_ERR_UNSUPPORTED) return rc;
+    p->release();
   }
   // workers: contiguous row ranges of equal cost (entries + an epilogue weight per row); per worker,
   // wave passes dealt to its 16 waves by longest-first greedy balance
@@ -593,7 +946,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
 
 void ChainPlan::release() {
   for (void* q : {(void*)ids, (void*)wcols, (void*)wcol_off, (void*)gids, (void*)bcols, (void*)bcol_off, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar,
-                  (void*)gbuf, (void*)u0, (void*)x0})
+                  (void*)gbuf, (void*)u0, (void*)x0, (void*)sids, (void*)srow0, (void*)scrow, (void*)scs, (void*)scont})
     (void)hipFree(q);
   if (host_flag) (void)hipHostFree(host_flag);
   if (done) (void)hipEventDestroy(done);
@@ -644,6 +997,37 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   hipLaunchKernelGGL(chain_prologue_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, n,
                      (int64_t)p->n_act, L->perm, X0, L->dinv, coef, p->x0, p->u0, S, H, p->bar + 3);
   WG_LAUNCH_CHECK();
+  if (p->solo_E) {  // one workgroup (cheb_chain_solo_kernel)
+    SoloArgs a{};
+    a.n_act = p->n_act;
+    a.K = K;
+    auto al = [](int64_t x) { return (int32_t)((x + 15) & ~(int64_t)15); };
+    a.off_x0 = al(4 * ((int64_t)p->n_act + 1));
+    a.off_rsum = al(a.off_x0 + 4 * (int64_t)p->n_act);
+    a.off_carry = al(a.off_rsum + 8 * (int64_t)p->n_act);
+    a.ids = p->sids;
+    a.row0 = p->srow0;
+    a.crow = p->scrow;
+    a.cs = p->scs;
+    a.cont = p->scont;
+    a.dinv = L->dinv;
+    a.iso = L->iso;
+    a.perm = L->perm;
+    a.x0 = p->x0;
+    a.u0 = p->u0;
+    a.S = S;
+    a.H = H;
+    for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
+    const void* kern = solo_kernel(p->solo_E, p->solo_R);
+    if (!kern) return fail(WG_ERR_INVALID, "chain solo: no kernel for E=%d", p->solo_E);
+    if (int rc = prof_mark(L, stream, true)) return rc;
+    void* args[] = {&a};
+    WG_HIP_TRY(hipLaunchKernel(kern, dim3(1), dim3(kChainThreads), args, (size_t)p->lds_bytes, stream));
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    WG_HIP_TRY(hipStreamIsCapturing(stream, &cs));
+    if (cs == hipStreamCaptureStatusNone) WG_HIP_TRY(hipEventRecord(p->done, stream));
+    return prof_mark(L, stream, false);
+  }
   if (int rc = ensure_dyn_lds((const void*)cheb_chain1_kernel, kChainLds)) return rc;
   static int wall_khz[64] = {0};  // the wall clock's rate per device (constant)
   int dev = 0;

@@ -974,6 +974,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.probe_h2 = L->tune.probe_h2;
         a.probe_fold = L->tune.probe_fold;
         a.coldnt = L->tune.coldnt;
+        a.probe_ns = L->tune.probe_ns;
         if (fold) {
           if (cl->closed.gather_x0) {
             if (int rc2 = build_team_first(L, &plan->team)) return rc2;

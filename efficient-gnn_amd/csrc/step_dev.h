@@ -54,6 +54,7 @@ struct StepArgs {
   // probe_h2: columns below it gather one aligned 128-B line (lanes of columns 32.. skip);
   // probe_fold: every gathered column folded into [0, probe_fold)
   int32_t probe_h2, probe_fold;
+  int32_t probe_ns;  // -DWG_TIMING_PROBES: Clenshaw epilogue without its X0 (bit 0) / b_{k+2} (bit 1) row loads
   int32_t coldnt;  // -DWG_TIMING_PROBES: gathers of columns >= coldnt with the non-temporal hint (the hot rows
                    // are not evicted by once-used cold lines?), the others plain: two loads, one dropped
   // value-free gathers on the padded CSR (cheb_step_kernel<..., P4 = true>): each row's column ids
@@ -172,6 +173,12 @@ __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int
   in.orow = a.out_perm ? a.out_perm[row] : (int32_t)row;
   if (a.clen) {
     in.dinv = (a.uin | a.uprev | a.uout) ? a.dinv[row] : 1.0;
+#ifdef WG_TIMING_PROBES
+    if (a.probe_ns & 2) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) in.prev[j] = 0.0f;
+    } else
+#endif
     if (a.xm2) {
       load_vec<VEC>(a.xm2 + off, in.prev);
     } else {
@@ -183,6 +190,12 @@ __device__ __forceinline__ void epi_prefetch(const StepArgs& a, int64_t row, int
       load_vec<VEC>(a.x0c + (int64_t)in.orow * a.ld + (int64_t)fs * VEC, in.sold);
       return;
     }
+#ifdef WG_TIMING_PROBES
+    if (a.probe_ns & 1) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) in.sold[j] = 0.0f;
+    } else
+#endif
     if (a.x0) {
       load_vec<VEC>(a.x0 + off, in.sold);
     } else {

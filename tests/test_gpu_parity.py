@@ -742,15 +742,19 @@ def test_chain_under_torch_graph_capture():
 
 # ----------------------------------------------------------------- the one-launch chain (chain.hip)
 @pytest.mark.parametrize("n,nnz,K,knobs", [(19717, 88648, 16, {}), (2708, 10556, 8, {}), (2708, 10556, 3, {"chain_wg": 1}),
-                                           (19717, 88648, 1, {}), (19717, 88648, 2, {"chain_wg": 3}),
+                                           (19717, 88648, 1, {}), (19717, 88648, 2, {}), (19717, 88648, 3, {}),
+                                           (19717, 88648, 32, {}), (2708, 10556, 1, {}),
+                                           (19717, 88648, 2, {"chain_wg": 3}),
                                            (19717, 88648, 32, {"chain_wg": 16, "chain_xcd": 1}),
-                                           (19717, 88648, 16, {"chain_xcd": 1}),
-                                           (19717, 88648, 16, {"chain_direct": 1}), (19717, 88648, 2, {"chain_direct": 1}),
+                                           (19717, 88648, 16, {"chain_solo": 0, "chain_xcd": 1}),
+                                           (19717, 88648, 16, {"chain_solo": 0, "chain_direct": 1}),
+                                           (19717, 88648, 2, {"chain_solo": 0, "chain_direct": 1}),
                                            (19717, 88648, 32, {"chain_wg": 16, "chain_direct": 1}),
-                                           (6000, 150000, 16, {"chain_wg": 5})])
+                                           (6000, 150000, 16, {"chain_wg": 5}), (6000, 150000, 16, {})])
 def test_chain1_vs_oracle(n, nnz, K, knobs):
-    """F = 1 small graphs run the whole chain in one launch (P workers, a
-    device-counter barrier per step): PubMed-size K = 16 (the
+    """F = 1 small graphs run the whole chain in one launch: one
+    workgroup with the ids in registers (solo, the default where it fits: Cora
+    and PubMed size) or P workers exchanging granules: PubMed-size K = 16 (the
     BASELINE configs[1] workload) and Cora-size K = 8, K = 1 / 2 / 3 / 32
     (every branch of the Clenshaw phase coefficients), 1 to 16 workers, XCD
     placement, against the oracle with the reference signal and a random one,
@@ -765,6 +769,8 @@ def test_chain1_vs_oracle(n, nnz, K, knobs):
         H2, S2 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=Xt, return_S=True)
         torch.cuda.synchronize()
         assert "chain1:" in L.describe(1), L.describe(1)
+        solo = not knobs and nnz < 98000
+        assert ("(solo:" in L.describe(1)) == solo, L.describe(1)
         assert not L.chain_status(), "a chain barrier wait timed out"
         assert torch.equal(S1, S2) and torch.equal(H1, H2)
         X0 = L.log1p_degree().cpu().numpy() if X is None else X
@@ -802,6 +808,35 @@ def test_chain1_directed_multi_worker(wg):
             assert_parity(_np(S), ref["S"], what=f"chain1 directed P={wg} direct={direct} S")
         out[direct] = _np(S)
     assert np.array_equal(out[0], out[1]), "direct gathers changed the sums"
+    L.close()
+
+
+@pytest.mark.parametrize("K", [16, 5])
+def test_chain_solo_directed(K):
+    """The one-workgroup chain (cheb_chain_solo_kernel) on a directed graph with self
+    loops and isolated nodes: active rows with no entries (each a pad entry that
+    ends its row), isolated-flag rows, rows that continue across threads (their
+    sums finished by the thread of the row's end from the others' carries);
+    against the oracle, bitwise repeatable, and against the multi-worker chain
+    and the multi-launch path to rounding."""
+    g = random_graph(6000, 0.0015, seed=K, directed=True, weighted=False, self_loop_frac=0.05, isolated_frac=0.05)
+    L = NormalizedLaplacian.from_graph(g)
+    X = np.random.default_rng(K).standard_normal((g.n, 1)).astype(np.float32)
+    ref = O.graph_wavelet_features(g.to_scipy(), k=K, s=0.8, X0=X, return_all=True)
+    H1, S1 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=torch.from_numpy(X), return_S=True)
+    H2, S2 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=torch.from_numpy(X), return_S=True)
+    torch.cuda.synchronize()
+    assert "(solo:" in L.describe(1), L.describe(1)
+    assert torch.equal(S1, S2) and torch.equal(H1, H2)
+    assert_parity(_np(S1), ref["S"], what=f"chain solo directed K={K} S")
+    big = np.abs(ref["S"]) > 1e-3 * np.abs(ref["S"]).max()
+    assert np.abs(_np(H1)[big] - ref["H"][big]).max() <= 1e-5
+    for knobs in ({"chain_wg": 4}, {"chain": 0}):
+        L.tune(**knobs)
+        _, S0 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=torch.from_numpy(X), return_S=True)
+        torch.cuda.synchronize()
+        assert "(solo:" not in L.describe(1)
+        assert_parity(_np(S1), _np(S0).astype(np.float64), what=f"chain solo vs {knobs}")
     L.close()
 
 
