@@ -206,7 +206,8 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.chain_fault = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "chain_solo")) {
-    L->tune.chain_solo = value ? 1 : 0;  // plans rebuilt
+    if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "chain_solo must be 0, 1 (auto) or 2 (wherever it fits)");
+    L->tune.chain_solo = (int32_t)value;  // plans rebuilt
   } else if (!strcmp(key, "chain_direct")) {
     L->tune.chain_direct = value ? 1 : 0;  // also the auto worker count: plans rebuilt
   } else if (!strcmp(key, "chain_xcd")) {

@@ -406,29 +406,29 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
 // ---- solo: the whole chain in ONE workgroup, no exchange at all.  PubMed-size
 // graphs do not fit one workgroup's LDS with their 16-bit ids (177 KB for 88.6 k entries), so the
 // chain above runs 128 workers and pays two Infinity-Cache trips per phase.  Here the ids live in
-// the 1024 threads' REGISTERS (E entries per thread, two per VGPR: column | row-end bit 15), and LDS
-// holds only u (every active row, plus a zero pad column), X0, the rows' float64 sums and one carry
-// per thread.  A phase is two passes and two workgroup barriers:
-//   pass 1: thread t sums u over its E consecutive entries (row order, balanced), blocks of loads
-//           issued before their sums; at a row end the sum goes to rsum[row]; what is left (the
-//           start of a row that continues in the next thread) goes to carry[t];
-//   pass 2: rows t + 1024 m (R per thread) run the Clenshaw epilogue of cheb_chain1_kernel on
-//           rsum; a row that began in earlier threads is finished by the thread of its end:
-//           carry[cs .. t - 1] in thread order, then its own part (deterministic).
-// The host orders each row segment's entries so that the 32 lanes of a read group hit distinct
-// LDS banks where they can (build_solo_plan).  One workgroup: no co-residency, no wait, no timeout.
-constexpr int kSoloBlock = 16;  // pass 1: loads issued per block before their sums
-constexpr int kSoloMaxR = 10;   // rows per thread (<= 10 240 active rows; LDS caps it lower)
+// the 1024 threads' REGISTERS (E slots per lane, two 16-bit LDS byte offsets per VGPR) and LDS holds
+// u twice (the gathered u_{k+1} and, in place, u_{k+2} -> u_k), X0 and dinv: 16 B per active row.
+// Each wave runs a static list of passes (the plan): a pass gives 64 / TS rows of similar length a
+// team of TS lanes each and lasts L slots (ceil(length / TS), the pass's longest row); a lane sums
+// its slots' u in float32, flushed to float64 every 8 slots; at the pass's last slot (uniform: a
+// scalar compare) the team's sums meet by shuffles and the row's epilogue writes u_k over u_{k+2}:
+//   u_k = dinv (ck X0 - cacc dinv s) - u_{k+2} [- cacc u_{k+1} on isolated rows]
+// (cheb_chain1_kernel's b_k = ck X0 + cacc L_hat b_{k+1} - b_{k+2} times dinv, no division; the
+// last phase's u_0 = S dinv is divided out at the end).  One workgroup barrier per phase.  The plan orders each team's entries slot by slot so that a read
+// group's 32 lanes hit distinct LDS banks where they can.  No co-residency, no wait, no timeout.
+constexpr int kSoloBlock = 16;  // loads issued per block before their sums
+constexpr int64_t kSoloMaxNnz = 1 << 15;  // the auto plan's limit (build_chain_plan)
+constexpr int kSoloSlots = 8;   // a pass's team size keeps ceil(length / TS) within this many slots
 
 struct SoloArgs {
   int32_t n_act;
   int32_t K;
-  int32_t off_x0, off_rsum, off_carry;  // LDS byte offsets
-  const uint32_t* ids;                  // [E / 2][threads]
-  const int32_t* row0;
-  const int32_t* crow;
-  const int32_t* cs;
-  const uint8_t* cont;
+  int32_t off_ub, off_x0, off_dv, off_pt;  // LDS byte offsets (u buffer A at 0; off_pt: the pass table)
+  int32_t n_pass;
+  const uint32_t* ids;             // [E / 2][threads]: two 16-bit LDS byte offsets (column * 4) per word
+  const int4* passes;              // {first row, rows | log2 TS << 8, L, 0}
+  const int32_t* wpass;            // [waves + 1]: each wave's passes
+  const int32_t* wslots;           // [waves]: slots each wave uses
   const double* dinv;
   const uint8_t* iso;
   const int32_t* perm;
@@ -444,129 +444,121 @@ __device__ __forceinline__ uint32_t solo_entry(const uint32_t (&w)[E / 2], int q
   return (q & 1) ? (w[q >> 1] >> 16) : (w[q >> 1] & 0xffffu);
 }
 
-template <int E, int R>
+template <int E>
 __global__ __launch_bounds__(kChainThreads) void cheb_chain_solo_kernel(SoloArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int t = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int na = a.n_act;
-  float* u = reinterpret_cast<float*>(smem);                        // [na + 1] u of the previous phase
-  float* x0 = reinterpret_cast<float*>(smem + a.off_x0);            // [na]
-  double* rsum = reinterpret_cast<double*>(smem + a.off_rsum);      // [na] the rows' sums of a phase
-  double* carry = reinterpret_cast<double*>(smem + a.off_carry);    // [threads] the unfinished row's part
+  float* x0 = reinterpret_cast<float*>(smem + a.off_x0);  // [na]
+  float* dv = reinterpret_cast<float*>(smem + a.off_dv);  // [na] dinv, negative: isolated row
+  int4* pt = reinterpret_cast<int4*>(smem + a.off_pt);     // [n_pass] every wave's passes
   uint32_t idw[E / 2];
 #pragma unroll
-  for (int q = 0; q < E / 2; ++q) idw[q] = a.ids[q * kChainThreads + t];
-  // per own row, float32 to keep the ids in registers: dinv (negative: isolated row), 1 / dinv
-  // (negative: a continued row, finished by the thread of its end), u two phases back
-  float dsi[R], rdi[R], pu[R];
-#pragma unroll
-  for (int m = 0; m < R; ++m) {
-    const int i = t + m * kChainThreads;
-    dsi[m] = 0.0f;
-    rdi[m] = 0.0f;
-    pu[m] = 0.0f;
-    if (i < na) {
-      const double di = a.dinv[i];
-      dsi[m] = a.iso[i] ? -(float)di : (float)di;
-      rdi[m] = (float)((a.cont[i] ? -1.0 : 1.0) / di);
+  for (int q = 0; q < E / 2; ++q) idw[q] = a.ids[q * kChainThreads + tid];
+  {
+    float* ua = reinterpret_cast<float*>(smem);
+    float* ub = reinterpret_cast<float*>(smem + a.off_ub);
+    for (int i = tid; i < na; i += kChainThreads) {
+      ua[i] = a.u0[i];
+      ub[i] = 0.0f;
+      x0[i] = a.x0[i];
+      const float d = (float)a.dinv[i];
+      dv[i] = a.iso[i] ? -d : d;
     }
+    if (tid == 0) ua[na] = ub[na] = 0.0f;  // the pad column
+    for (int i = tid; i < a.n_pass; i += kChainThreads) pt[i] = a.passes[i];
   }
-  const int crow = a.crow[t], cs = a.cs[t];
-  float cdsi = 0.0f, crdi = 0.0f, cpu = 0.0f;
-  if (crow >= 0) {
-    const double di = a.dinv[crow];
-    cdsi = a.iso[crow] ? -(float)di : (float)di;
-    crdi = (float)(1.0 / di);
-  }
-  for (int i = t; i < na; i += kChainThreads) {
-    u[i] = a.u0[i];
-    x0[i] = a.x0[i];
-  }
-  if (t == 0) u[na] = 0.0f;  // the pad column
-  const int row0 = a.row0[t];
+  // a pass descriptor as scalars (uniform over the wave)
+  auto pass_at = [&](int i) -> int4 {
+    const int4 v = pt[i];
+    return int4{__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                __builtin_amdgcn_readfirstlane(v.z), 0};
+  };
+  const int p0 = a.wpass[wave], p1 = a.wpass[wave + 1];
+  const int nslots = a.wslots[wave];
   __syncthreads();
   const int K = a.K;
+  int cur = 0;  // the buffer of u_{k+1} (gathered); the other holds u_{k+2} and receives u_k
   for (int j = 1; j <= K; ++j) {
     const int k = K - j;  // cheb_chain1_kernel's phase coefficients
     const double cacc = (j == 1) ? (k == 0 ? a.c[K] : 2.0 * a.c[K]) : (k == 0 ? 1.0 : 2.0);
     const double ck = a.c[k] - (j == 2 ? a.c[K] : 0.0);
     const bool prevs = j >= 3;
-    double acc = 0.0;
-    int row = row0;
-    // the decoded addresses and row-end flags must not be hoisted out of the phase loop (E more
-    // live registers): the words are opaque to the compiler once per phase
+    const unsigned char* ug = smem + (cur ? a.off_ub : 0);
+    float* uo = reinterpret_cast<float*>(smem + (cur ? 0 : a.off_ub));
+    const float* ugf = reinterpret_cast<const float*>(ug);
+    // the decoded offsets must not be hoisted out of the phase loop (E more live registers)
 #pragma unroll
     for (int q = 0; q < E / 2; ++q) asm volatile("" : "+v"(idw[q]));
-    // likewise the own rows' float64 operands and LDS addresses (pass 2): recomputed per phase
-    int tp = t;
-    asm volatile("" : "+v"(tp));
-#pragma unroll
-    for (int m = 0; m < R; ++m) asm volatile("" : "+v"(dsi[m]), "+v"(rdi[m]));
-#pragma unroll
-    for (int b = 0; b < E; b += kSoloBlock) {
-      float x[kSoloBlock];
-#pragma unroll
-      for (int q = 0; q < kSoloBlock; ++q) x[q] = u[solo_entry<E>(idw, b + q) & 0x7fffu];
-#pragma unroll
-      for (int q = 0; q < kSoloBlock; ++q) {
-        acc += (double)x[q];
-        if (solo_entry<E>(idw, b + q) & 0x8000u) {
-          rsum[row] = acc;
-          ++row;
-          acc = 0.0;
-        }
+    int pi = p0;
+    int4 pd = pi < p1 ? pass_at(pi) : int4{0, 0, 0, 0};
+    int4 pn = pi + 1 < p1 ? pass_at(pi + 1) : int4{0, 0, 0, 0};  // the next pass, read ahead
+    int pend = pi < p1 ? pd.z - 1 : -1;  // the slot that ends the current pass
+    float accf = 0.0f;
+    double accd = 0.0;
+    auto finish = [&]() {
+      const int lts = pd.y >> 8;
+      const int TS = 1 << lts;
+      const int team = lane >> lts;
+      double sum = accd + (double)accf;
+      for (int off = TS >> 1; off >= 1; off >>= 1) sum += __shfl_xor(sum, off, 64);
+      if ((lane & (TS - 1)) == 0 && team < (pd.y & 0xff)) {
+        const int row = pd.x + team;
+        const float dr = dv[row];
+        const double di = fabs((double)dr);
+        const double xr = (double)x0[row];
+        const double u2 = prevs ? (double)uo[row] : 0.0;  // u_{k+2} (own row)
+        const double u1 = dr < 0.0f ? (double)ugf[row] : 0.0;  // isolated row: L_hat_ii = -1
+        // b_k * dinv; the last phase's (S * dinv) is divided out after the loop
+        uo[row] = (float)(di * (ck * xr - cacc * di * sum) - u2 - cacc * u1);
       }
-    }
-    carry[t] = acc;
-    __syncthreads();  // every sum and carry of the phase written, every read of u done
-    auto epi = [&](int i, double s, float ds, float rdf, float& p) {
-      const double di = fabs((double)ds);
-      const double rd = (double)rdf;
-      const float ui = u[i];  // this row's u of the previous phase
-      double lb = -di * s;
-      if (ds < 0.0f) lb -= (double)ui * rd;  // isolated row: L_hat_ii = -1
-      const double tt = ck * (double)x0[i] + cacc * lb - (prevs ? (double)p * rd : 0.0);
-      if (k > 0) {
-        p = ui;
-        u[i] = (float)(tt * di);
+      accf = 0.0f;
+      accd = 0.0;
+      ++pi;
+      if (pi < p1) {
+        pd = pn;
+        pend += pd.z;
+        if (pi + 1 < p1) pn = pass_at(pi + 1);
       } else {
-        const int32_t r = a.perm[i];
-        a.S[r] = (float)tt;
-        a.H[r] = (float)(tt / (fabs(tt) + 1e-8));
+        pend = -1;
       }
     };
 #pragma unroll
-    for (int m = 0; m < R; ++m) {
-      const int i = tp + m * kChainThreads;
-      if (i < na && rdi[m] > 0.0f) epi(i, rsum[i], dsi[m], rdi[m], pu[m]);
+    for (int b = 0; b < E; b += kSoloBlock) {
+      if (b >= nslots) break;  // uniform
+      float x[kSoloBlock];
+#pragma unroll
+      for (int q = 0; q < kSoloBlock; ++q) x[q] = *reinterpret_cast<const float*>(ug + solo_entry<E>(idw, b + q));
+#pragma unroll
+      for (int q = 0; q < kSoloBlock; ++q) {
+        accf += x[q];
+        if ((q & 7) == 7) {
+          accd += (double)accf;
+          accf = 0.0f;
+        }
+        if (b + q == pend) finish();
+      }
     }
-    if (crow >= 0) {
-      double s = 0.0;
-      for (int q = cs; q < t; ++q) s += carry[q];
-      s += rsum[crow];
-      epi(crow, s, cdsi, crdi, cpu);
-    }
-    if (k == 0) break;
-    __syncthreads();  // the phase's u written before the next phase reads it
+    __syncthreads();  // u_k complete before the next phase gathers it
+    cur ^= 1;
+  }
+  // S = (S * dinv) / dinv and H = S / (|S|_1 + 1e-8), to the caller's rows
+  const float* us = reinterpret_cast<const float*>(smem + (cur ? a.off_ub : 0));
+  for (int i = tid; i < na; i += kChainThreads) {
+    const double t = (double)us[i] / fabs((double)dv[i]);
+    const int32_t r = a.perm[i];
+    a.S[r] = (float)t;
+    a.H[r] = (float)(t / (fabs(t) + 1e-8));
   }
 }
 
-// the instantiation for (E, R) (build_solo_plan picks E from these)
-const void* solo_kernel(int E, int R) {
-  if (R > 8) {
-    switch (E) {
-      case 16: return (const void*)cheb_chain_solo_kernel<16, kSoloMaxR>;
-      case 32: return (const void*)cheb_chain_solo_kernel<32, kSoloMaxR>;
-      case 64: return (const void*)cheb_chain_solo_kernel<64, kSoloMaxR>;
-      case 96: return (const void*)cheb_chain_solo_kernel<96, kSoloMaxR>;
-      default: return nullptr;
-    }
-  }
+const void* solo_kernel(int E) {
   switch (E) {
-    case 16: return (const void*)cheb_chain_solo_kernel<16, 8>;
-    case 32: return (const void*)cheb_chain_solo_kernel<32, 8>;
-    case 64: return (const void*)cheb_chain_solo_kernel<64, 8>;
-    case 96: return (const void*)cheb_chain_solo_kernel<96, 8>;
+    case 32: return (const void*)cheb_chain_solo_kernel<32>;
+    case 64: return (const void*)cheb_chain_solo_kernel<64>;
+    case 96: return (const void*)cheb_chain_solo_kernel<96>;
+    case 128: return (const void*)cheb_chain_solo_kernel<128>;
     default: return nullptr;
   }
 }
@@ -604,165 +596,150 @@ void make_passes(const std::vector<int32_t>& rp, int64_t r0, int64_t r1, std::ve
 
 
 // The solo plan (cheb_chain_solo_kernel), or WG_ERR_UNSUPPORTED when the graph does not fit one
-// workgroup: u, X0 and the float64 sums of every active row in LDS, <= 96 entries and <= 10 rows per
-// thread.  Entries in row order, an empty row as one pad entry (so that every row has an end),
-// split evenly over the threads.  Within each (thread, row) segment the entries may be summed in any
-// order; slot by slot, a read group's 32 lanes (threads 32 g ..) take, fewest choices first, the
-// entry whose LDS bank (column mod 32) has the fewest distinct columns so far -- the same column is a
-// broadcast, free (MI355X_MICROARCH.md, LDS: ds_read_b32 serves two groups of 32 lanes, one cycle
-// per extra distinct address on a bank).
+// workgroup (16 B of LDS per active row, <= 128 slots per lane).
+// Passes: consecutive rows (descending length) sharing a team size TS, the smallest power of two
+// with ceil(length / TS) <= kSoloSlots; 64 / TS rows per pass, L = the longest row's ceil(length /
+// TS) slots.  Passes go to the 16 waves longest first onto the least loaded wave (L + an epilogue's
+// worth of slots).  Slot by slot, each read group's 32 lanes take, fewest choices first, an entry of
+// their row (a team's lanes share its row's entries) whose LDS bank (column mod 32) has the fewest
+// distinct columns so far -- the same column is a broadcast, free (MI355X_MICROARCH.md, LDS:
+// ds_read_b32 serves two groups of 32 lanes, one cycle per extra distinct address on a bank).
 int build_solo_plan(wg_laplacian_s* L, ChainPlan* p, const std::vector<int32_t>& rp, const std::vector<uint16_t>& ids) {
   const int64_t na = L->n_active;
   const int T = kChainThreads;
-  if (na < 1 || na + 1 >= 0x8000) return WG_ERR_UNSUPPORTED;
+  if (na < 1 || 4 * (na + 1) > 0xffff) return WG_ERR_UNSUPPORTED;  // 16-bit LDS byte offsets
   auto al = [](int64_t x) { return (x + 15) & ~(int64_t)15; };
-  const int64_t off_x0 = al(4 * (na + 1)), off_rsum = al(off_x0 + 4 * na), off_carry = al(off_rsum + 8 * na);
-  const int64_t lds = al(off_carry + 8 * T);
-  if (lds > kChainLds) return WG_ERR_UNSUPPORTED;
-  const int R = (int)((na + T - 1) / T);
-  if (R > kSoloMaxR) return WG_ERR_UNSUPPORTED;
-  std::vector<uint16_t> ecol;
-  std::vector<int32_t> erow;
-  std::vector<int64_t> rfirst(na), rlast(na);
-  ecol.reserve(rp[na] + na);
-  erow.reserve(rp[na] + na);
-  for (int64_t r = 0; r < na; ++r) {
-    rfirst[r] = (int64_t)ecol.size();
-    if (rp[r + 1] == rp[r]) {
-      ecol.push_back((uint16_t)na);
-      erow.push_back((int32_t)r);
+  const int64_t off_ub = al(4 * (na + 1)), off_x0 = al(off_ub + 4 * (na + 1)), off_dv = al(off_x0 + 4 * na);
+  if (al(off_dv + 4 * na) > kChainLds) return WG_ERR_UNSUPPORTED;
+  struct Pass {
+    int32_t row0, n, lts, L;
+  };
+  std::vector<Pass> passes;
+  for (int64_t r = 0; r < na;) {
+    auto ts_of = [&](int64_t len) {
+      int l = 0;
+      while (l < 6 && (len + (1 << l) - 1) / (1 << l) > kSoloSlots) ++l;
+      return l;
+    };
+    const int64_t len0 = rp[r + 1] - rp[r];
+    const int lts = ts_of(len0);
+    int n = 0;
+    int64_t L = 1;
+    while (n < (64 >> lts) && r + n < na && ts_of(rp[r + n + 1] - rp[r + n]) == lts) {
+      L = std::max<int64_t>(L, (rp[r + n + 1] - rp[r + n] + (1 << lts) - 1) >> lts);
+      ++n;
     }
-    for (int64_t e = rp[r]; e < rp[r + 1]; ++e) {
-      ecol.push_back(ids[e]);
-      erow.push_back((int32_t)r);
-    }
-    rlast[r] = (int64_t)ecol.size() - 1;
+    passes.push_back(Pass{(int32_t)r, n, lts, (int32_t)L});
+    r += n;
   }
-  const int64_t ne = (int64_t)ecol.size();
-  const int64_t per = (ne + T - 1) / T;
+  // passes onto waves: longest first onto the least loaded (slots + an epilogue's worth)
+  constexpr int kEpiSlots = 6;
+  std::vector<int> order(passes.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return passes[x].L > passes[y].L; });
+  std::vector<int64_t> load(kChainWaves, 0), slots_w(kChainWaves, 0);
+  std::vector<std::vector<int>> per(kChainWaves);
+  for (int i : order) {
+    const int v = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[v] += passes[i].L + kEpiSlots;
+    slots_w[v] += passes[i].L;
+    per[v].push_back(i);
+  }
+  const int64_t need = *std::max_element(slots_w.begin(), slots_w.end());
   int E = 0;
-  for (int e : {16, 32, 64, 96})  // (128 entries spill registers)
-    if (per <= e) {
+  for (int e : {32, 64, 96, 128})
+    if (need <= e) {
       E = e;
       break;
     }
   if (!E) return WG_ERR_UNSUPPORTED;
-  std::vector<int64_t> B(T + 1);
-  for (int t = 0; t <= T; ++t) B[t] = ne * t / T;
-  std::vector<int32_t> row0(T, 0), crow(T, -1), cs(T, 0);
-  std::vector<uint8_t> cont(na, 0);
-  for (int t = 0; t < T; ++t) {
-    if (B[t] == B[t + 1]) continue;
-    const int32_t r = erow[B[t]];
-    row0[t] = r;
-    if (rfirst[r] < B[t] && rlast[r] < B[t + 1]) {  // a row that began in earlier threads ends here
-      crow[t] = r;
-      cont[r] = 1;
-      cs[t] = (int32_t)(std::upper_bound(B.begin(), B.end(), rfirst[r]) - B.begin()) - 1;
-    }
-  }
-  // slots[t][q]: column | row-end bit; pads (past a thread's entries) read the zero pad column
-  std::vector<uint16_t> slots((size_t)T * E, (uint16_t)na);
-  int64_t cyc_plain = 0, cyc_sched = 0;  // LDS cycles of pass 1 (sum over slots and groups of the worst bank)
-  for (int g = 0; g < T / 32; ++g) {
-    struct Seg {
-      int64_t b, e;  // entry range [b, e) of one (thread, row) piece
-      bool end;      // the row ends in it
-    };
-    std::vector<std::vector<Seg>> segs(32);
-    for (int l = 0; l < 32; ++l) {
-      const int t = 32 * g + l;
-      for (int64_t x = B[t]; x < B[t + 1];) {
-        int64_t y = x;
-        while (y < B[t + 1] && erow[y] == erow[x]) ++y;
-        segs[l].push_back(Seg{x, y, rlast[erow[x]] == y - 1});
-        x = y;
-      }
-    }
-    // plain order: the cycles the schedule is measured against
-    for (int q = 0; q < E; ++q) {
-      int load[32] = {0};
-      std::vector<uint16_t> seen;
-      for (int l = 0; l < 32; ++l) {
-        const int t = 32 * g + l;
-        const uint16_t c = B[t] + q < B[t + 1] ? ecol[B[t] + q] : (uint16_t)na;
-        if (std::find(seen.begin(), seen.end(), c) != seen.end()) continue;
-        seen.push_back(c);
-        ++load[c & 31];
-      }
-      cyc_plain += *std::max_element(load, load + 32);
-    }
-    std::vector<std::vector<uint16_t>> pool(32);
-    std::vector<size_t> si(32, 0);
-    std::vector<int64_t> pos(32, 0);  // slots filled
-    for (int q = 0; q < E; ++q) {
-      int load[32] = {0};
-      std::vector<uint16_t> seen;
-      std::vector<int> order;
-      for (int l = 0; l < 32; ++l) {
-        if (pool[l].empty() && si[l] < segs[l].size()) {  // the lane's next segment
-          const Seg& sg = segs[l][si[l]];
-          pool[l].assign(ecol.begin() + sg.b, ecol.begin() + sg.e);
-        }
-        order.push_back(l);
-      }
-      std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
-        const size_t px = pool[x].empty() ? 0 : pool[x].size(), py = pool[y].empty() ? 0 : pool[y].size();
-        return px < py;
-      });
-      for (int l : order) {
-        const int t = 32 * g + l;
-        uint16_t c = (uint16_t)na;
-        if (!pool[l].empty()) {
-          size_t best = 0;
-          int bc = 1 << 30;
-          for (size_t i = 0; i < pool[l].size(); ++i) {
-            const uint16_t ci = pool[l][i];
-            const int cost = std::find(seen.begin(), seen.end(), ci) != seen.end() ? -1 : load[ci & 31];
-            if (cost < bc) {
-              bc = cost;
-              best = i;
+  // slots: per lane, the byte offset (column * 4) of each slot's entry; pads read the zero column na
+  const uint16_t pad = (uint16_t)(4 * na);
+  std::vector<uint16_t> slot((size_t)T * E, pad);
+  std::vector<int4> ptab;
+  std::vector<int32_t> wpass(kChainWaves + 1, 0), wslots(kChainWaves, 0);
+  int64_t cyc_plain = 0, cyc_sched = 0;  // pass-1 LDS cycles (sum over slots and read groups of the worst bank)
+  for (int v = 0; v < kChainWaves; ++v) {
+    wpass[v] = (int32_t)ptab.size();
+    int q0 = 0;
+    for (int i : per[v]) {
+      const Pass& ps = passes[i];
+      ptab.push_back(int4{ps.row0, ps.n | (ps.lts << 8), ps.L, 0});
+      const int TS = 1 << ps.lts;
+      std::vector<std::vector<uint16_t>> pool(64 >> ps.lts);  // each team's remaining columns
+      for (int t = 0; t < ps.n; ++t)
+        for (int32_t e = rp[ps.row0 + t]; e < rp[ps.row0 + t + 1]; ++e) pool[t].push_back(ids[e]);
+      std::vector<std::vector<uint16_t>> plain(pool);  // the natural order, for the cycle count
+      for (int q = 0; q < ps.L; ++q) {
+        for (int g = 0; g < 2; ++g) {
+          int load_s[32] = {0}, load_p[32] = {0};
+          std::vector<uint16_t> seen_s, seen_p;
+          std::vector<int> lanes;
+          for (int l = 32 * g; l < 32 * g + 32; ++l) lanes.push_back(l);
+          std::stable_sort(lanes.begin(), lanes.end(),
+                           [&](int x, int y) { return pool[x >> ps.lts].size() < pool[y >> ps.lts].size(); });
+          for (int l : lanes) {
+            std::vector<uint16_t>& pl = pool[l >> ps.lts];
+            uint16_t c = (uint16_t)na;
+            if (!pl.empty()) {
+              size_t best = 0;
+              int bc = 1 << 30;
+              for (size_t x = 0; x < pl.size(); ++x) {
+                const int cost = std::find(seen_s.begin(), seen_s.end(), pl[x]) != seen_s.end() ? -1 : load_s[pl[x] & 31];
+                if (cost < bc) {
+                  bc = cost;
+                  best = x;
+                }
+              }
+              c = pl[best];
+              pl[best] = pl.back();
+              pl.pop_back();
+            }
+            slot[(size_t)(64 * v + l) * E + q0 + q] = (uint16_t)(4 * c);
+            if (std::find(seen_s.begin(), seen_s.end(), c) == seen_s.end()) {
+              seen_s.push_back(c);
+              ++load_s[c & 31];
+            }
+            // the plain order: lane tl of a team takes entries tl, tl + TS, ...
+            const int team = l >> ps.lts, tl = l & (TS - 1);
+            const size_t e = (size_t)q * TS + tl;
+            const uint16_t cp = (team < ps.n && e < plain[team].size()) ? plain[team][e] : (uint16_t)na;
+            if (std::find(seen_p.begin(), seen_p.end(), cp) == seen_p.end()) {
+              seen_p.push_back(cp);
+              ++load_p[cp & 31];
             }
           }
-          c = pool[l][best];
-          pool[l][best] = pool[l].back();
-          pool[l].pop_back();
-          uint16_t v = c;
-          if (pool[l].empty()) {  // the segment's last slot carries the row end
-            if (segs[l][si[l]].end) v |= 0x8000;
-            ++si[l];
-          }
-          slots[(size_t)t * E + q] = v;
-          ++pos[l];
-        }
-        if (std::find(seen.begin(), seen.end(), c) == seen.end()) {
-          seen.push_back(c);
-          ++load[c & 31];
+          cyc_sched += *std::max_element(load_s, load_s + 32);
+          cyc_plain += *std::max_element(load_p, load_p + 32);
         }
       }
-      cyc_sched += *std::max_element(load, load + 32);
+      for (const auto& pl : pool)
+        if (!pl.empty()) return fail(WG_ERR_INVALID, "solo plan: entries left over");
+      q0 += ps.L;
     }
-    for (int l = 0; l < 32; ++l)
-      if (pos[l] != B[32 * g + l + 1] - B[32 * g + l]) return fail(WG_ERR_INVALID, "solo plan: slots lost");
+    wslots[v] = q0;
   }
+  wpass[kChainWaves] = (int32_t)ptab.size();
+  const int64_t lds = al(off_dv + 4 * na) + 16 * (int64_t)ptab.size();  // + the pass table
+  if (lds > kChainLds) return WG_ERR_UNSUPPORTED;
+  p->solo_npass = (int32_t)ptab.size();
+  if (ptab.empty()) ptab.push_back(int4{0, 0, 0, 0});
   std::vector<uint32_t> w((size_t)(E / 2) * T);
   for (int t = 0; t < T; ++t)
     for (int q = 0; q < E / 2; ++q)
-      w[(size_t)q * T + t] = (uint32_t)slots[(size_t)t * E + 2 * q] | ((uint32_t)slots[(size_t)t * E + 2 * q + 1] << 16);
-  const void* kern = solo_kernel(E, R);
+      w[(size_t)q * T + t] = (uint32_t)slot[(size_t)t * E + 2 * q] | ((uint32_t)slot[(size_t)t * E + 2 * q + 1] << 16);
+  const void* kern = solo_kernel(E);
   if (!kern) return WG_ERR_UNSUPPORTED;
   if (int rc = ensure_dyn_lds(kern, kChainLds)) return rc;
   p->P = 1;
   p->n_act = (int32_t)na;
   p->lds_bytes = (int32_t)lds;
   p->solo_E = E;
-  p->solo_R = R;
   p->ustride = (int32_t)((na + 63) / 64 * 64);
   int rc = upload(&p->sids, w);
-  if (!rc) rc = upload(&p->srow0, row0);
-  if (!rc) rc = upload(&p->scrow, crow);
-  if (!rc) rc = upload(&p->scs, cs);
-  if (!rc) rc = upload(&p->scont, cont);
+  if (!rc) rc = upload(&p->spass, ptab);
+  if (!rc) rc = upload(&p->swpass, wpass);
+  if (!rc) rc = upload(&p->swslots, wslots);
   if (!rc) rc = dmalloc(&p->bar, 4);
   if (!rc) rc = dmalloc(&p->u0, (size_t)na);
   if (!rc) rc = dmalloc(&p->x0, (size_t)na);
@@ -774,9 +751,11 @@ int build_solo_plan(wg_laplacian_s* L, ChainPlan* p, const std::vector<int32_t>&
   WG_HIP_TRY(hipHostGetDevicePointer((void**)&p->d_host_flag, p->host_flag, 0));
   p->seen = 0;
   char buf[256];
-  snprintf(buf, sizeof(buf), "chain1: one launch per chain, 1 workers x %d threads (solo: %d entries and %d rows per "
-           "thread in registers), %lld active rows, %lld nonzeros, LDS %d B; pass-1 LDS cycles %lld (plain order %lld)\n",
-           T, E, R, (long long)na, (long long)rp[na], p->lds_bytes, (long long)cyc_sched, (long long)cyc_plain);
+  snprintf(buf, sizeof(buf), "chain1: one launch per chain, 1 workers x %d threads (solo: %d slots per lane in "
+           "registers, %d passes, busiest wave %lld slots), %lld active rows, %lld nonzeros, LDS %d B; LDS read "
+           "cycles per phase %lld (plain order %lld)\n",
+           T, E, (int)passes.size(), (long long)need, (long long)na, (long long)rp[na], p->lds_bytes,
+           (long long)cyc_sched, (long long)cyc_plain);
   p->text = buf;
   return WG_OK;
 }
@@ -793,7 +772,10 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
     if (col[e] < 0 || col[e] >= na) return fail(WG_ERR_INVALID, "chain plan: column %d outside the active rows", col[e]);
     ids[e] = (uint16_t)col[e];
   }
-  if (L->tune.chain_solo && L->tune.chain_wg <= 0) {  // one workgroup, ids in registers, when it fits
+  // one workgroup, ids in registers: auto up to kSoloMaxNnz entries (Cora-size K = 8: 29.3 vs 49.8 us per
+  // chain; PubMed-size K = 16: 217 vs 78.4 with 128 workers -- one CU's VALU and LDS, r05 s19-s20), or
+  // wherever it fits with chain_solo = 2
+  if (L->tune.chain_wg <= 0 && (L->tune.chain_solo == 2 || (L->tune.chain_solo == 1 && nnz <= kSoloMaxNnz))) {
     const int rc = build_solo_plan(L, p, rp, ids);
     if (rc != WG_ERR_UNSUPPORTED) return rc;
     p->release();
@@ -946,7 +928,7 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
 
 void ChainPlan::release() {
   for (void* q : {(void*)ids, (void*)wcols, (void*)wcol_off, (void*)gids, (void*)bcols, (void*)bcol_off, (void*)wdesc, (void*)wpass, (void*)passes, (void*)bar,
-                  (void*)gbuf, (void*)u0, (void*)x0, (void*)sids, (void*)srow0, (void*)scrow, (void*)scs, (void*)scont})
+                  (void*)gbuf, (void*)u0, (void*)x0, (void*)sids, (void*)spass, (void*)swpass, (void*)swslots})
     (void)hipFree(q);
   if (host_flag) (void)hipHostFree(host_flag);
   if (done) (void)hipEventDestroy(done);
@@ -1002,14 +984,16 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
     a.n_act = p->n_act;
     a.K = K;
     auto al = [](int64_t x) { return (int32_t)((x + 15) & ~(int64_t)15); };
-    a.off_x0 = al(4 * ((int64_t)p->n_act + 1));
-    a.off_rsum = al(a.off_x0 + 4 * (int64_t)p->n_act);
-    a.off_carry = al(a.off_rsum + 8 * (int64_t)p->n_act);
+    const int64_t na = p->n_act;
+    a.off_ub = al(4 * (na + 1));
+    a.off_x0 = al(a.off_ub + 4 * (na + 1));
+    a.off_dv = al(a.off_x0 + 4 * na);
+    a.off_pt = al(a.off_dv + 4 * na);
+    a.n_pass = p->solo_npass;
     a.ids = p->sids;
-    a.row0 = p->srow0;
-    a.crow = p->scrow;
-    a.cs = p->scs;
-    a.cont = p->scont;
+    a.passes = p->spass;
+    a.wpass = p->swpass;
+    a.wslots = p->swslots;
     a.dinv = L->dinv;
     a.iso = L->iso;
     a.perm = L->perm;
@@ -1018,8 +1002,8 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
     a.S = S;
     a.H = H;
     for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
-    const void* kern = solo_kernel(p->solo_E, p->solo_R);
-    if (!kern) return fail(WG_ERR_INVALID, "chain solo: no kernel for E=%d", p->solo_E);
+    const void* kern = solo_kernel(p->solo_E);
+    if (!kern) return fail(WG_ERR_INVALID, "chain solo: no kernel for %d slots", p->solo_E);
     if (int rc = prof_mark(L, stream, true)) return rc;
     void* args[] = {&a};
     WG_HIP_TRY(hipLaunchKernel(kern, dim3(1), dim3(kChainThreads), args, (size_t)p->lds_bytes, stream));

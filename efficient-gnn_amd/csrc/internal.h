@@ -231,7 +231,8 @@ struct Tuning {
                              // 0 = auto: one when its ids and two u buffers fit LDS (no exchange), else 64
                              // (PubMed-size K=16: 8 / 16 / 32 / 64 workers 187 / 139 / 119 / 113 us per chain,
                              // profiles/r03/s13_chain1_worker_sweep.log)
-  int32_t chain_solo = 1;    // chain.hip: one workgroup, column ids in registers, when it fits (auto worker count only)
+  int32_t chain_solo = 1;    // chain.hip: one workgroup, ids in registers (auto worker count only): 1 up to 2^15
+                             // entries, 2 wherever it fits, 0 never
   int32_t chain_direct = 1;  // chain.hip: gathers read the granules straight from memory (no LDS staging of u)
   int32_t chain_xcd = 0;     // chain.hip: workers on one XCD (grid of 8 P, every 8th workgroup works; P <= 32)
   int32_t chain_fault = 0;   // chain.hip fault injection (tests of the timeout path): worker 0 does not publish
@@ -281,13 +282,12 @@ struct ChainPlan {
   uint64_t* gbuf = nullptr;   // device [2][ustride]: tagged u granules {float bits, tag << 32}
   float* u0 = nullptr;        // device [n_act]: u_0 = X0 * dinv
   float* x0 = nullptr;        // device [n_act]: X0 in internal order
-  // solo (one workgroup, chain.hip cheb_chain_solo_kernel): E entries per thread, R rows per thread
-  int32_t solo_E = 0, solo_R = 0;
-  uint32_t* sids = nullptr;   // device [E / 2][threads]: two 16-bit entries per word (column | row-end bit)
-  int32_t* srow0 = nullptr;   // device [threads]: the row of each thread's first entry
-  int32_t* scrow = nullptr;   // device [threads]: the row continued into the thread from earlier ones, or -1
-  int32_t* scs = nullptr;     // device [threads]: the first thread that holds entries of that row
-  uint8_t* scont = nullptr;   // device [n_act]: 1 = the row is continued (finished by the thread of its end)
+  // solo (one workgroup, chain.hip cheb_chain_solo_kernel): E register slots per lane
+  int32_t solo_E = 0, solo_npass = 0;
+  uint32_t* sids = nullptr;   // device [E / 2][threads]: two 16-bit LDS byte offsets (column * 4) per word
+  int4* spass = nullptr;      // device: the waves' passes {first row, rows | log2 team size << 8, slots, 0}
+  int32_t* swpass = nullptr;  // device [waves + 1]: each wave's pass range
+  int32_t* swslots = nullptr; // device [waves]: the slots each wave uses
   std::string text;
   void release();
 };

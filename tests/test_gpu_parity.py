@@ -742,8 +742,9 @@ def test_chain_under_torch_graph_capture():
 
 # ----------------------------------------------------------------- the one-launch chain (chain.hip)
 @pytest.mark.parametrize("n,nnz,K,knobs", [(19717, 88648, 16, {}), (2708, 10556, 8, {}), (2708, 10556, 3, {"chain_wg": 1}),
-                                           (19717, 88648, 1, {}), (19717, 88648, 2, {}), (19717, 88648, 3, {}),
-                                           (19717, 88648, 32, {}), (2708, 10556, 1, {}),
+                                           (19717, 88648, 1, {}), (19717, 88648, 2, {"chain_solo": 2}),
+                                           (19717, 88648, 3, {"chain_solo": 2}), (19717, 88648, 16, {"chain_solo": 2}),
+                                           (19717, 88648, 32, {"chain_solo": 2}), (2708, 10556, 1, {}),
                                            (19717, 88648, 2, {"chain_wg": 3}),
                                            (19717, 88648, 32, {"chain_wg": 16, "chain_xcd": 1}),
                                            (19717, 88648, 16, {"chain_solo": 0, "chain_xcd": 1}),
@@ -769,7 +770,7 @@ def test_chain1_vs_oracle(n, nnz, K, knobs):
         H2, S2 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=Xt, return_S=True)
         torch.cuda.synchronize()
         assert "chain1:" in L.describe(1), L.describe(1)
-        solo = not knobs and nnz < 98000
+        solo = (not knobs and nnz <= 32768) or knobs.get("chain_solo") == 2
         assert ("(solo:" in L.describe(1)) == solo, L.describe(1)
         assert not L.chain_status(), "a chain barrier wait timed out"
         assert torch.equal(S1, S2) and torch.equal(H1, H2)
@@ -814,13 +815,13 @@ def test_chain1_directed_multi_worker(wg):
 @pytest.mark.parametrize("K", [16, 5])
 def test_chain_solo_directed(K):
     """The one-workgroup chain (cheb_chain_solo_kernel) on a directed graph with self
-    loops and isolated nodes: active rows with no entries (each a pad entry that
-    ends its row), isolated-flag rows, rows that continue across threads (their
-    sums finished by the thread of the row's end from the others' carries);
+    loops and isolated nodes: active rows with no entries, isolated-flag rows,
+    long rows summed by lane teams;
     against the oracle, bitwise repeatable, and against the multi-worker chain
     and the multi-launch path to rounding."""
     g = random_graph(6000, 0.0015, seed=K, directed=True, weighted=False, self_loop_frac=0.05, isolated_frac=0.05)
     L = NormalizedLaplacian.from_graph(g)
+    L.tune(chain_solo=2)   # ~54 k entries: past the auto limit
     X = np.random.default_rng(K).standard_normal((g.n, 1)).astype(np.float32)
     ref = O.graph_wavelet_features(g.to_scipy(), k=K, s=0.8, X0=X, return_all=True)
     H1, S1 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=torch.from_numpy(X), return_S=True)
@@ -831,7 +832,7 @@ def test_chain_solo_directed(K):
     assert_parity(_np(S1), ref["S"], what=f"chain solo directed K={K} S")
     big = np.abs(ref["S"]) > 1e-3 * np.abs(ref["S"]).max()
     assert np.abs(_np(H1)[big] - ref["H"][big]).max() <= 1e-5
-    for knobs in ({"chain_wg": 4}, {"chain": 0}):
+    for knobs in ({"chain_solo": 0, "chain_wg": 4}, {"chain": 0}):
         L.tune(**knobs)
         _, S0 = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=torch.from_numpy(X), return_S=True)
         torch.cuda.synchronize()
