@@ -432,8 +432,9 @@ struct SoloArgs {
   const double* dinv;
   const uint8_t* iso;
   const int32_t* perm;
-  const float* x0;  // [n_act] internal X0 (chain_prologue_kernel)
-  const float* u0;  // [n_act] u_0 = X0 * dinv
+  const float* X0;  // the caller's signal (chain_prologue_kernel's work is done here)
+  int64_t n;        // rows; [n_act, n) are the closed-form rows
+  double coef;      // their S = coef * X0
   float* S;
   float* H;
   double c[kChainMaxK + 1];
@@ -459,12 +460,19 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain_solo_kernel(SoloArgs
   {
     float* ua = reinterpret_cast<float*>(smem);
     float* ub = reinterpret_cast<float*>(smem + a.off_ub);
-    for (int i = tid; i < na; i += kChainThreads) {
-      ua[i] = a.u0[i];
+    for (int i = tid; i < na; i += kChainThreads) {  // chain_prologue_kernel's internal X0 and u_0
+      const float x = a.X0[a.perm[i]];
+      const double di = a.dinv[i];
+      ua[i] = (float)((double)x * di);
       ub[i] = 0.0f;
-      x0[i] = a.x0[i];
-      const float d = (float)a.dinv[i];
-      dv[i] = a.iso[i] ? -d : d;
+      x0[i] = x;
+      dv[i] = a.iso[i] ? -(float)di : (float)di;
+    }
+    for (int64_t i = na + tid; i < a.n; i += kChainThreads) {  // closed-form rows
+      const int32_t r = a.perm[i];
+      const double sv = a.coef * (double)a.X0[r];
+      a.S[r] = (float)sv;
+      a.H[r] = (float)(sv / (fabs(sv) + 1e-8));
     }
     if (tid == 0) ua[na] = ub[na] = 0.0f;  // the pad column
     for (int i = tid; i < a.n_pass; i += kChainThreads) pt[i] = a.passes[i];
@@ -741,8 +749,6 @@ int build_solo_plan(wg_laplacian_s* L, ChainPlan* p, const std::vector<int32_t>&
   if (!rc) rc = upload(&p->swpass, wpass);
   if (!rc) rc = upload(&p->swslots, wslots);
   if (!rc) rc = dmalloc(&p->bar, 4);
-  if (!rc) rc = dmalloc(&p->u0, (size_t)na);
-  if (!rc) rc = dmalloc(&p->x0, (size_t)na);
   if (rc) return rc;
   WG_HIP_TRY(hipMemset(p->bar, 0, 4 * sizeof(int32_t)));
   WG_HIP_TRY(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
@@ -976,10 +982,7 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   const int64_t n = L->n_rows;
   double coef = 0.0;  // closed-form rows: S = X0 * sum_k (-1)^k c_k
   for (int32_t k = 0; k <= K; ++k) coef += ((k & 1) ? -1.0 : 1.0) * std::exp(-s * (double)k);
-  hipLaunchKernelGGL(chain_prologue_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, n,
-                     (int64_t)p->n_act, L->perm, X0, L->dinv, coef, p->x0, p->u0, S, H, p->bar + 3);
-  WG_LAUNCH_CHECK();
-  if (p->solo_E) {  // one workgroup (cheb_chain_solo_kernel)
+  if (p->solo_E) {  // one workgroup (cheb_chain_solo_kernel), its own prologue
     SoloArgs a{};
     a.n_act = p->n_act;
     a.K = K;
@@ -997,8 +1000,9 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
     a.dinv = L->dinv;
     a.iso = L->iso;
     a.perm = L->perm;
-    a.x0 = p->x0;
-    a.u0 = p->u0;
+    a.X0 = X0;
+    a.n = n;
+    a.coef = coef;
     a.S = S;
     a.H = H;
     for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
@@ -1012,6 +1016,9 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
     if (cs == hipStreamCaptureStatusNone) WG_HIP_TRY(hipEventRecord(p->done, stream));
     return prof_mark(L, stream, false);
   }
+  hipLaunchKernelGGL(chain_prologue_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, n,
+                     (int64_t)p->n_act, L->perm, X0, L->dinv, coef, p->x0, p->u0, S, H, p->bar + 3);
+  WG_LAUNCH_CHECK();
   if (int rc = ensure_dyn_lds((const void*)cheb_chain1_kernel, kChainLds)) return rc;
   static int wall_khz[64] = {0};  // the wall clock's rate per device (constant)
   int dev = 0;
