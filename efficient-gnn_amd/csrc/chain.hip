@@ -66,10 +66,12 @@ struct ChainArgs {
   const double* dinv;
   const uint8_t* iso;
   const int32_t* perm;
-  const float* x0;            // [n_act] X0 in internal order
-  const float* u0;            // [n_act] u_0 = X0 * dinv (prologue)
+  const float* X0;            // the caller's signal: internal X0 = X0[perm[row]], u_0 = X0 * dinv on the fly
+  int64_t n;                  // rows; [n_act, n) are the closed-form rows (S = coef * X0)
+  double coef;
   uint64_t* gbuf;             // [2][ustride] tagged granules {float bits, tag << 32}
-  int32_t* bar;               // [2] epoch of the last timed-out launch, [3] launch epoch (bumped by the prologue)
+  int32_t* bar;               // [1] workers finished, [2] epoch of the last timed-out launch, [3] launch epoch
+                              // (bumped by the launch's last worker to finish: every worker read it first)
   int32_t* host_flag;         // host-mapped: epoch of the last timed-out launch (read by the next API call)
   int64_t wait_ticks;         // a granule wait gives up after this many wall-clock ticks (~0.5 s)
   int32_t fault_phase;        // fault injection (tuning key "chain_fault", tests): worker 0 skips this phase's publish
@@ -150,7 +152,12 @@ __device__ __forceinline__ void chain_fail(const ChainArgs& a, int* s_bad, uint3
   }
 }
 
-// direct mode: u of columns c[0 .. n) for phase j -- u_0 (written before the launch) in phase 1,
+// u_0 of internal row c: the caller's X0 row perm[c] times dinv (what the permute-in pass wrote)
+__device__ __forceinline__ float chain_u0(const ChainArgs& a, int c) {
+  return (float)((double)a.X0[a.perm[c]] * a.dinv[c]);
+}
+
+// direct mode: u of columns c[0 .. n) for phase j -- u_0 (from the caller's X0) in phase 1,
 // else the previous phase's granules, all loads in flight at once, re-polled until every tag is
 // `want`; false past the deadline (the values are then NaN)
 __device__ __forceinline__ bool fetch_u(const ChainArgs& a, const uint64_t* gprev, int j, uint32_t want,
@@ -158,7 +165,7 @@ __device__ __forceinline__ bool fetch_u(const ChainArgs& a, const uint64_t* gpre
   if (j == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (i < n) x[i] = a.u0[c[i]];
+      if (i < n) x[i] = chain_u0(a, c[i]);
     return true;
   }
   uint64_t v[4];
@@ -184,27 +191,6 @@ __device__ __forceinline__ bool fetch_u(const ChainArgs& a, const uint64_t* gpre
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if ((pending >> i) & 1) v[i] = ld_sc1_u64(gprev + c[i]);
-  }
-}
-
-// internal X0 of the active rows, u_0 = X0 * dinv into exchange buffer 0, and the
-// closed-form rows' S = coef * X0, H = S / (|S| + 1e-8) straight to the caller's rows
-__global__ void chain_prologue_kernel(int64_t n, int64_t n_act, const int32_t* __restrict__ perm,
-                                      const float* __restrict__ X0, const double* __restrict__ dinv, double coef,
-                                      float* __restrict__ x0int, float* __restrict__ u0, float* __restrict__ S,
-                                      float* __restrict__ H, int32_t* __restrict__ epoch) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row == 0) *epoch = *epoch + 1;  // read by the chain kernel after this launch (stream order)
-  if (row >= n) return;
-  const int32_t r = perm[row];
-  const float x = X0[r];
-  if (row < n_act) {
-    x0int[row] = x;
-    u0[row] = (float)((double)x * dinv[row]);
-  } else {
-    const double s = coef * (double)x;
-    S[r] = (float)s;
-    H[r] = (float)(s / (fabs(s) + 1e-8));
   }
 }
 
@@ -243,23 +229,30 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
     const double di = a.dinv[row0 + i];
     dv[i] = a.iso[row0 + i] ? -di : di;
     rdv[i] = 1.0 / di;
-    x0o[i] = a.x0[row0 + i];
-    cu[i] = a.u0[row0 + i];
+    const float x = a.X0[a.perm[row0 + i]];
+    x0o[i] = x;
+    cu[i] = (float)((double)x * di);
     lrp[i] = a.rowptr[row0 + i] - e0;
   }
   if (tid == 0) lrp[nr] = ne;
+  for (int64_t i = (int64_t)a.n_act + (int64_t)w * kChainThreads + tid; i < a.n; i += (int64_t)a.P * kChainThreads) {
+    const int32_t r = a.perm[i];  // the closed-form rows, dealt over the workers
+    const double sv = a.coef * (double)a.X0[r];
+    a.S[r] = (float)sv;
+    a.H[r] = (float)(sv / (fabs(sv) + 1e-8));
+  }
   const uint16_t* idsrc = a.direct ? a.gids : a.ids;
   for (int i = tid; i < ne; i += kChainThreads) id[i] = idsrc[e0 + i];
   for (int i = tid; i < npass; i += kChainThreads) pas[i] = a.passes[pass0 + i];
   if (a.direct) {
     // no LDS copy of u: the gathers read u_0 and then the granules themselves
   } else if (a.P == 1) {
-    for (int i = tid; i < a.n_act; i += kChainThreads) u[i] = a.u0[i];
+    for (int i = tid; i < a.n_act; i += kChainThreads) u[i] = chain_u0(a, i);
   } else {
     for (int i = tid; i < nu; i += kChainThreads) {
       const int c = a.wcols[wc0 + i];
       wc[i] = (uint16_t)c;
-      u[i] = a.u0[c];
+      u[i] = chain_u0(a, c);
     }
   }
   __syncthreads();
@@ -392,6 +385,13 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
     tr[ntr++] = clock64();
 #endif
   }
+  if (tid == 0) {  // the last worker to finish moves the epoch on for the next launch
+    const int32_t done = __hip_atomic_fetch_add(a.bar + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == a.P - 1) {
+      __hip_atomic_store(a.bar + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.bar + 3, (int32_t)((ep + 1) & 0x3ffffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 #ifdef WG_CHAIN_TRACE
   if (w == 0 && tid == 0) {
     printf("chain1 trace P=%d n_act=%d rows=%d entries=%d passes(wave0)=%d: staged at %lld\n", a.P, a.n_act, nr, ne,
@@ -414,7 +414,8 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
 // scalar compare) the team's sums meet by shuffles and the row's epilogue writes u_k over u_{k+2}:
 //   u_k = dinv (ck X0 - cacc dinv s) - u_{k+2} [- cacc u_{k+1} on isolated rows]
 // (cheb_chain1_kernel's b_k = ck X0 + cacc L_hat b_{k+1} - b_{k+2} times dinv, no division; the
-// last phase's u_0 = S dinv is divided out at the end).  One workgroup barrier per phase.  The plan orders each team's entries slot by slot so that a read
+// last phase's u_0 = S dinv is divided out at the end).  One workgroup barrier per phase.  The kernel
+// does its own prologue (internal X0, u_0, the closed-form rows).  The plan orders each team's entries slot by slot so that a read
 // group's 32 lanes hit distinct LDS banks where they can.  No co-residency, no wait, no timeout.
 constexpr int kSoloBlock = 16;  // loads issued per block before their sums
 constexpr int64_t kSoloMaxNnz = 1 << 15;  // the auto plan's limit (build_chain_plan)
@@ -432,7 +433,7 @@ struct SoloArgs {
   const double* dinv;
   const uint8_t* iso;
   const int32_t* perm;
-  const float* X0;  // the caller's signal (chain_prologue_kernel's work is done here)
+  const float* X0;  // the caller's signal (the permute-in is done here)
   int64_t n;        // rows; [n_act, n) are the closed-form rows
   double coef;      // their S = coef * X0
   float* S;
@@ -460,7 +461,7 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain_solo_kernel(SoloArgs
   {
     float* ua = reinterpret_cast<float*>(smem);
     float* ub = reinterpret_cast<float*>(smem + a.off_ub);
-    for (int i = tid; i < na; i += kChainThreads) {  // chain_prologue_kernel's internal X0 and u_0
+    for (int i = tid; i < na; i += kChainThreads) {  // the internal X0 and u_0
       const float x = a.X0[a.perm[i]];
       const double di = a.dinv[i];
       ua[i] = (float)((double)x * di);
@@ -912,8 +913,6 @@ int build_chain_plan(wg_laplacian_s* L, ChainPlan* p) {
   if (!rc) rc = upload(&p->passes, passes);
   if (!rc) rc = dmalloc(&p->bar, 4);
   if (!rc) rc = dmalloc(&p->gbuf, (size_t)4 * p->ustride);
-  if (!rc) rc = dmalloc(&p->u0, (size_t)std::max<int64_t>(na, 1));
-  if (!rc) rc = dmalloc(&p->x0, (size_t)std::max<int64_t>(na, 1));
   if (rc) return rc;
   WG_HIP_TRY(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
   WG_HIP_TRY(hipHostMalloc((void**)&p->host_flag, sizeof(int32_t), hipHostMallocMapped));
@@ -1016,9 +1015,6 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
     if (cs == hipStreamCaptureStatusNone) WG_HIP_TRY(hipEventRecord(p->done, stream));
     return prof_mark(L, stream, false);
   }
-  hipLaunchKernelGGL(chain_prologue_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, stream, n,
-                     (int64_t)p->n_act, L->perm, X0, L->dinv, coef, p->x0, p->u0, S, H, p->bar + 3);
-  WG_LAUNCH_CHECK();
   if (int rc = ensure_dyn_lds((const void*)cheb_chain1_kernel, kChainLds)) return rc;
   static int wall_khz[64] = {0};  // the wall clock's rate per device (constant)
   int dev = 0;
@@ -1049,8 +1045,9 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.dinv = L->dinv;
   a.iso = L->iso;
   a.perm = L->perm;
-  a.x0 = p->x0;
-  a.u0 = p->u0;
+  a.X0 = X0;
+  a.n = n;
+  a.coef = coef;
   a.gbuf = p->gbuf;
   a.bar = p->bar;
   a.host_flag = p->d_host_flag;
