@@ -363,8 +363,9 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     b_8d = algorithmic_bytes(n_launch, sw.L.nnz, F)
     lds_info = sw.L.lds_plan_info(active_only=False) if (F == 1 and sw.u_len() > 0) else None
     b_step = lds_algorithmic_bytes(lds_info) if lds_info else b_8d
-    kernel = lds_kernel_name(lds_info) + " (rank 0 shard)"
-    tiles_plan = [ln for ln in sw.L.describe(F).splitlines() if ln.startswith("tiles:")]
+    plan_text = sw.L.describe(F)
+    kernel = lds_kernel_name(lds_info, team="team:" in plan_text) + " (rank 0 shard)"
+    tiles_plan = [ln for ln in plan_text.splitlines() if ln.startswith("tiles:")]
     if tiles_plan:   # the hybrid step: dense blocks on MFMA + the tail on the step kernel
         kernel = ("hybrid step: cheb_tiles_kernel + tiles_combine_kernel + the tail on the step kernel "
                   "(cheb_team4_kernel; rank 0 shard)")
