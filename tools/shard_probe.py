@@ -48,6 +48,19 @@ def main():
 
 
 def one_rank(a, b, ip, ix, indptr, deg, dev, K):
+    L, n_own, n_cols = build_shard(a, b, ip, ix, indptr, deg, dev)
+    lib = _lib.load()
+    for knobs in (a.grid.split(";") if a.grid else [""]):
+        kv = dict(lds=a.lds)
+        kv.update({x.split("=")[0]: int(x.split("=")[1]) for x in knobs.split(",") if x})
+        L.tune(**kv)
+        probe(L, lib, n_own, n_cols, K, a, dev, kv)
+    L.close()
+    torch.cuda.empty_cache()
+
+
+def build_shard(a, b, ip, ix, indptr, deg, dev):
+    """Rank a.rank's shard as wats_hip.dist builds it; returns (handle, own rows, columns)."""
     r0, r1 = int(b[a.rank]), int(b[a.rank + 1])
     cols = ix[int(indptr[r0]):int(indptr[r1])].to(torch.int64)
     # the shard as wats_hip.dist builds it: [own | halo], halo grouped by owner, each group in
@@ -72,14 +85,7 @@ def one_rank(a, b, ip, ix, indptr, deg, dev, K):
         offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
         check(_lib.load().wg_laplacian_set_halo_groups(L.handle, a.world, offs.ctypes.data), "set_halo_groups")
     del cols, local
-    lib = _lib.load()
-    for knobs in (a.grid.split(";") if a.grid else [""]):
-        kv = dict(lds=a.lds)
-        kv.update({x.split("=")[0]: int(x.split("=")[1]) for x in knobs.split(",") if x})
-        L.tune(**kv)
-        probe(L, lib, n_own, n_cols, K, a, dev, kv)
-    L.close()
-    torch.cuda.empty_cache()
+    return L, n_own, n_cols
 
 
 def probe(L, lib, n_own, n_cols, K, a, dev, kv):
