@@ -205,6 +205,10 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < 0 || value > kChainMaxK) return fail(WG_ERR_INVALID, "chain_fault must be in [0, %d]", kChainMaxK);
     L->tune.chain_fault = (int32_t)value;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "hyb_conc")) {
+    if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "hyb_conc must be 0, 1 (auto) or 2 (always)");
+    L->tune.hyb_conc = (int32_t)value;
+    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "chain_solo")) {
     if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "chain_solo must be 0, 1 (auto) or 2 (wherever it fits)");
     L->tune.chain_solo = (int32_t)value;  // plans rebuilt

@@ -672,7 +672,7 @@ int wg_dist_wavelet_features(wg_dist_t D, const float* X0, int64_t F, int32_t K,
   // these arguments (it builds the kernel plans and the workspace).  Either way the chain
   // runs on the handle's own non-blocking stream (cap), joined to the caller's: on the legacy
   // null stream the step kernels would wait for every blocking stream's work.
-  if (!D->use_graph || D->L->prof || D->warm == 0) {
+  if (!D->use_graph || D->L->prof || D->warm == 0 || hybrid_conc_in_use(D->L, F)) {
     if (int rc = after_last(D->cap)) return rc;
     WG_HIP_TRY(hipEventRecord(D->fork, st));
     WG_HIP_TRY(hipStreamWaitEvent(D->cap, D->fork, 0));

@@ -249,6 +249,9 @@ struct Tuning {
                              // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
                              // the closed-form rows; team.hip cheb_team4_first_kernel); 2 = a pass writes
                              // u_0 only (the first launch gathers it; the rest as 1); 0 = the full pass
+  int32_t hyb_conc = 1;      // hybrid step with the team-kernel tail: the tail's row sums on a second stream
+                             // beside the dense blocks, then one epilogue pass (step.hip); 1 = when the
+                             // blocks leave the GPU half idle (tiles.hip hybrid_conc_applies), 2 = always
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
   int64_t team_tail = 8 << 20;  // the hybrid step's tail on the team kernel up to this many entries
   int32_t team_order = -1;   // team.hip: wave dispatch order (0 longest rows first, 1 reversed, 2 .. 7 mixed;
@@ -359,6 +362,12 @@ struct wg_laplacian_s {
   bool chain1_failed = false;       // no plan (too large for resident workers / LDS): multi-launch path
   bool chain1_off = false;          // a launch timed out (the GPU is shared?): multi-launch path until a tune
   int32_t chain1_timeouts = 0;      // timed-out launches seen on this handle
+  // the hybrid step's tail beside its dense blocks (tuning key hyb_conc): a second stream, its fork /
+  // join events and the tail's float64 row sums
+  hipStream_t side = nullptr;
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
+  double* tsum = nullptr;
+  int64_t tsum_n = 0;
   // live step-kernel timing (wg_profile_*)
   bool prof = false;
   std::vector<hipEvent_t> ev;  // pool of (start, stop) pairs
@@ -445,6 +454,10 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start);
 // tiles.hip: the hybrid step's plan (*out = nullptr: not applicable) and its dense-block pass,
 // which writes part = sum over the dense entries of u_j (value-free steps) for the planned rows
 bool tiles_wanted(const wg_laplacian_s* L, int64_t F);
+// the hybrid step runs its tail beside the dense blocks (hyb_conc) on a plan already built: a chain that
+// would replay as a hipGraph runs eagerly instead (the captured fork / join replays slower, dist.hip)
+bool hybrid_conc_in_use(const wg_laplacian_s* L, int64_t F);
+bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp);
 int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out);
 int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream);
 void release_tiles(wg_laplacian_s* L);

@@ -525,8 +525,11 @@ wg_laplacian_s::~wg_laplacian_s() {
   for (auto& kv : plans) kv.second.release();
   wg::release_lds1(this);
   for (void* p : {(void*)rowptr, (void*)col, (void*)val, (void*)iso, (void*)perm, (void*)iperm, (void*)rowsum,
-                  (void*)ws, (void*)dinv, (void*)prp, (void*)pcol, (void*)trace_buf})
+                  (void*)ws, (void*)dinv, (void*)prp, (void*)pcol, (void*)trace_buf, (void*)tsum})
     (void)hipFree(p);
+  if (side_fork) (void)hipEventDestroy(side_fork);
+  if (side_join) (void)hipEventDestroy(side_join);
+  if (side) (void)hipStreamDestroy(side);
 }
 
 extern "C" {

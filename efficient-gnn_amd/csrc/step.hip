@@ -484,6 +484,25 @@ __global__ __launch_bounds__(kBlock) void l1_normalize_kernel(int64_t n, int64_t
   for (int64_t f = lane; f < F; f += 64) H[row * F + f] = (float)((double)S[row * F + f] / den);
 }
 
+// the hybrid step with its tail beside the dense blocks (tuning key hyb_conc): each row's tail sums
+// (a.tsum, written by the team kernel on the second stream) + its dense blocks' sums (part_add) and the
+// epilogue the tail pass would have run; LF lanes per row, G rows per wave
+__global__ __launch_bounds__(kBlock) void hybrid_epilogue_kernel(StepArgs a, int64_t n_rows) {
+  const int lane = threadIdx.x & 63;
+  const int LF = a.LF;
+  const int G = 64 / LF;
+  const int sg = lane / LF, fs = lane - sg * LF;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + sg;
+  if (sg >= G || row >= n_rows) return;  // whole sub-groups: the H shuffle stays within a row's lanes
+  EpiIn<4> in;
+  epi_prefetch<4>(a, row, fs, in);
+  const double* p = a.tsum + row * a.ld + fs * 4;
+  const double2 s01 = *reinterpret_cast<const double2*>(p), s23 = *reinterpret_cast<const double2*>(p + 2);
+  double acc[4] = {s01.x, s01.y, s23.x, s23.y};
+  part_add<4>(a, row, fs, acc);
+  step_epilogue<4>(a, row, fs, acc, in, sg * LF);
+}
+
 // smallest divisor of G that is >= want (G itself if none smaller)
 int divisor_at_least(int G, int64_t want) {
   for (int d = 1; d <= G; ++d)
@@ -907,7 +926,12 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
   const bool fuse_h = (H != nullptr) && F <= max_tile;
   if (S_out && !(fuse_h && S)) return fail(WG_ERR_INVALID, "launch_step: fused finalize needs one tile and S");
   // hyb: the hybrid step's tail pass (phase 4 over the tail-first columns, + the blocks' sums)
-  auto tiles_loop = [&](const TilePlan* hyb) -> int {
+  // conc (hyb_conc): the hybrid tail's sums go to L->tsum on the second stream; its arguments are kept
+  // for the epilogue pass (hybrid_epilogue_kernel) that follows the join
+  StepArgs conc_args{};
+  int64_t conc_rows = -1;
+  auto tiles_loop = [&](const TilePlan* hyb, hipStream_t tail_stream = nullptr, double* tsum = nullptr) -> int {
+    if (!tail_stream) tail_stream = stream;
     for (int64_t f0 = 0; f0 < F; f0 += max_tile) {
       const int64_t fw = std::min<int64_t>(max_tile, F - f0);
       const int LF = (int)(fw / vec);
@@ -986,7 +1010,12 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
           if (int rc2 = launch_team4(plan->team, a, L->tune.team, stream, &cl->closed)) return rc2;
           continue;
         }
-        if (int rc2 = launch_team4(plan->team, a, L->tune.team, stream)) return rc2;
+        if (tsum) {
+          conc_args = a;
+          conc_rows = plan->row1;
+          a.tsum = tsum;
+        }
+        if (int rc2 = launch_team4(plan->team, a, L->tune.team, tail_stream)) return rc2;
         continue;
       }
       if (g4 && !hyb) {
@@ -1056,6 +1085,35 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     TilePlan* tp = nullptr;
     if (int rc = get_tile_plan(L, active_only, F, &tp)) return rc;
     if (tp) {
+      const bool conc = vec == 4 && F <= max_tile && hybrid_conc_applies(L, tp) && gather4_applies(L, F);
+      if (conc) {  // the tail's sums on the second stream beside the dense blocks, then one epilogue pass
+        if (!L->side) WG_HIP_TRY(hipStreamCreateWithFlags(&L->side, hipStreamNonBlocking));
+        if (!L->side_fork) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_fork, hipEventDisableTiming));
+        if (!L->side_join) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_join, hipEventDisableTiming));
+        const int64_t need = L->n_rows * F;
+        if (L->tsum_n < need) {
+          (void)hipFree(L->tsum);
+          L->tsum = nullptr;
+          L->tsum_n = 0;
+          if (int rc = dmalloc(&L->tsum, (size_t)need)) return rc;
+          L->tsum_n = need;
+        }
+        WG_HIP_TRY(hipEventRecord(L->side_fork, stream));
+        WG_HIP_TRY(hipStreamWaitEvent(L->side, L->side_fork, 0));
+        if (int rc = tiles_loop(tp, L->side, L->tsum)) return rc;
+        if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
+        WG_HIP_TRY(hipEventRecord(L->side_join, L->side));
+        WG_HIP_TRY(hipStreamWaitEvent(stream, L->side_join, 0));
+        if (conc_rows < 0) return fail(WG_ERR_INVALID, "launch_step: the concurrent hybrid tail did not run");
+        if (conc_rows > 0) {
+          const int G = 64 / conc_args.LF;
+          conc_args.tsum = L->tsum;
+          hipLaunchKernelGGL(hybrid_epilogue_kernel, dim3((unsigned)ceil_div(conc_rows, 4 * (int64_t)G)), dim3(kBlock), 0,
+                             stream, conc_args, conc_rows);
+          WG_LAUNCH_CHECK();
+        }
+        return finish();
+      }
       if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
       if (int rc = tiles_loop(tp)) return rc;
       return finish();

@@ -73,6 +73,7 @@ struct StepArgs {
   // slot), so u_0 = X0 * dinv is never stored; the epilogue reads its own X0 row at caller row
   // perm_in[row] and writes it to x0i (the internal X0 the later steps read)
   int32_t first;
+  double* tsum;  // hybrid tail beside the dense blocks (hyb_conc): the row sums go here, no epilogue
   const double* sdinv;
   const float* x0c;
   float* x0i;

@@ -123,9 +123,9 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
   if (a.probe_h2 == -2) d0.y = 0;  // no ids, no gathers
 #endif
   if (active) {
-    if (!LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
+    if (!LATE && ns == 0 && !part && !a.tsum) epi_prefetch<4>(a, row, fs, in);
     accumulate_sell<CPT, FIRST>(a, int2{d0.x, d0.y}, G, sg, fs, acc);
-    if (LATE && ns == 0 && !part) epi_prefetch<4>(a, row, fs, in);
+    if (LATE && ns == 0 && !part && !a.tsum) epi_prefetch<4>(a, row, fs, in);
   }
   reduce_subgroups<4>(acc, LN, LF, team * LN * LF, fs);  // every lane (shuffles)
   bool emit = active && ns == 0;
@@ -151,7 +151,7 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
     if (!last || lane >= LF) return;
     // the last arriver: lanes 0 .. LF-1 (sub-group 0: fs == lane) sum every part's partial in
     // part order (deterministic) and share the team rows' epilogue below (one inlined copy)
-    epi_prefetch<4>(a, row, lane, in);
+    if (!a.tsum) epi_prefetch<4>(a, row, lane, in);
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = 0.0;
     for (int q = 0; q < d1.y; ++q) {
@@ -163,6 +163,12 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
     lane0 = 0;
   }
   if (emit) {
+    if (a.tsum) {  // the row's sums only (hybrid_epilogue_kernel adds the dense blocks and finishes the row)
+      double* p = a.tsum + row * a.ld + fs * 4;
+      *reinterpret_cast<double2*>(p) = double2{acc[0], acc[1]};
+      *reinterpret_cast<double2*>(p + 2) = double2{acc[2], acc[3]};
+      return;
+    }
     part_add<4>(a, row, fs, acc);
     step_epilogue<4>(a, row, fs, acc, in, lane0);
   }

@@ -655,6 +655,22 @@ bool tiles_wanted(const wg_laplacian_s* L, int64_t F) {
   return L->tune.tiles == 1 || L->nnz >= ((int64_t)8 << 20);
 }
 
+bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp) {
+  if (!tp || !L->tune.hyb_conc || !L->tune.team || L->nnz - tp->dense_nnz > L->tune.team_tail) return false;
+  if (L->tune.hyb_conc == 2) return true;
+  // auto: only a plan whose dense blocks leave the GPU half idle (fewer work items than two per CU: the
+  // 8-way Reddit-size F = 41 shard, 469 items, 156.5 vs 168.7 us per step with its exchange; the 4-way
+  // shard, slower beside: 262.7 vs 251.0, r05 s37-s38)
+  return (int64_t)tp->n_items < 2 * (int64_t)n_cus(L->device);
+}
+
+bool hybrid_conc_in_use(const wg_laplacian_s* L, int64_t F) {
+  if (!tiles_wanted(L, F)) return false;
+  for (const TilePlan* tp : L->tiles)
+    if (hybrid_conc_applies(L, tp)) return true;
+  return false;
+}
+
 int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out) {
   *out = nullptr;
   active_only = active_only && L->reordered;

@@ -102,6 +102,31 @@ def test_tiles_with_signal_tiles():
     assert_parity(_np(H1), ref["H"], what="tile_f=16 H")
 
 
+@pytest.mark.parametrize("k", [1, 3, 16])
+@pytest.mark.parametrize("F", [48, 16])
+def test_tiles_tail_beside_blocks(F, k):
+    """hyb_conc: the tail's row sums on a second stream beside the dense blocks and
+    one epilogue pass after the join (csrc/step.hip hybrid_epilogue_kernel) give the
+    same S and H as the sequential hybrid step, bit for bit (the same float64 sums
+    in the same order), with and without closed-form rows and long tails split over
+    part waves (team_iter 8); and the oracle's."""
+    g = rmat_graph(6000, 150000, seed=F + k)
+    for gg in (g, connect_isolated(g, seed=2)):
+        X = np.random.default_rng(F + 7 * k).standard_normal((gg.n, F)).astype(np.float32)
+        ref = O.graph_wavelet_features(gg.to_scipy(), k=k, s=0.8, X0=X, return_all=True)
+        L = NormalizedLaplacian.from_graph(gg)
+        for knobs in (dict(tile_th=16, tile_max=5, tile_rows=128), dict(tile_th=8, tile_max=3, tile_rows=64, team_iter=8)):
+            H0, S0 = _run(L, X, k, tiles=1, hyb_conc=0, **knobs)
+            H1, S1 = _run(L, X, k, tiles=1, hyb_conc=2, **knobs)
+            H2, S2 = _run(L, X, k, tiles=1, hyb_conc=2, **knobs)
+            torch.cuda.synchronize()
+            assert "tiles:" in L.describe(F)
+            assert torch.equal(S0, S1) and torch.equal(H0, H1), f"F={F} K={k} {knobs}: concurrent tail differs"
+            assert torch.equal(S1, S2) and torch.equal(H1, H2)
+            assert_parity(_np(S1), ref["S"], what=f"F={F} K={k} {knobs} S")
+        L.close()
+
+
 def test_tiles_deterministic():
     g = rmat_graph(4000, 120000, seed=9)
     X = np.random.default_rng(1).standard_normal((g.n, 48)).astype(np.float32)

@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--delays", default="0,30,60")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--graph", type=int, default=1, help="replay the chain as a hipGraph (1) or run it eagerly (0)")
+    ap.add_argument("--knobs", default="", help="tuning keys for the shard's handle, e.g. 'hyb_conc=1'")
     a = ap.parse_args()
     n, nnz_t, K, _ = NAMED_CONFIGS[a.config]
     dev = torch.device("cuda", 0)
@@ -70,6 +71,8 @@ def main():
     w = torch.from_numpy(np.concatenate([deg[r0:r1], deg[halo]]))
     L = wats_hip.NormalizedLaplacian(n_own, torch.from_numpy(indptr[r0:r1 + 1] - indptr[r0]), local, None,
                                      n_cols=n_cols, w_cols=w, device=dev)
+    if a.knobs:
+        L.tune(**{kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.knobs.split(",")})
     # loopback: halo row h is refreshed from own row h % n_own
     caller = torch.from_numpy((np.arange(halo.size) % n_own).astype(np.int32)).to(dev)
     internal = torch.empty_like(caller)
@@ -84,7 +87,7 @@ def main():
     X = torch.randn(n_own, a.F, device=dev)
     S = torch.empty(n_own, a.F, device=dev)
     H = torch.empty(n_own, a.F, device=dev)
-    print(f"shard {a.rank}/{a.world} rows {n_own} halo {halo.size} nnz {L.nnz}", flush=True)
+    print(f"shard {a.rank}/{a.world} rows {n_own} halo {halo.size} nnz {L.nnz} knobs {a.knobs or '-'}", flush=True)
     res = []
     for d in [int(x) for x in a.delays.split(",")]:
         L.tune(xdelay=d)   # a timing-probe build only (rejected as an unknown key otherwise)
