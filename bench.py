@@ -389,14 +389,15 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
         "data": "synthetic",
         "config": {"workload": f"{config}-size R-MAT (GPU generator, seed {seed}), one graph row-sharded over "
                                f"{world} ranks, halo exchange per Chebyshev step "
-                               + {"rccl": "(native: grouped ncclSend/ncclRecv, chain replayed as a hipGraph)",
-                                  "ipc": "(native: one-sided pull from IPC-mapped peer memory, flag-ordered "
-                                         "phases, chain replayed as a hipGraph)",
+                               + {"rccl": "(native: grouped ncclSend/ncclRecv",
+                                  "ipc": "(native: one-sided pull from IPC-mapped peer memory, flag-ordered phases",
                                   "sdma": "(native: owners pack, receivers copy the packed blocks from "
                                           "IPC-mapped peer memory by hipMemcpyAsync on a copy stream, "
-                                          "flag-ordered phases, chain replayed as a hipGraph)",
-                                  "nccl": "(torch all_to_all_single, RCCL)",
-                                  "host": "(torch all_to_all_single on host copies, gloo)"}[exchange]
+                                          "flag-ordered phases",
+                                  "nccl": "(torch all_to_all_single, RCCL",
+                                  "host": "(torch all_to_all_single on host copies, gloo"}[exchange]
+                               + (", chain replayed as a hipGraph)" if dinfo and dinfo.get("captured")
+                                  else ", chain launched eagerly)" if dinfo else ")")
                                + f"; K={K} F={F}",
                    "exchange": exchange,
                    "N": n_t, "nnz_input": nnz_global, "nnz_lhat": nnz_lhat, "K": K, "F": F,
