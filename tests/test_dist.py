@@ -352,6 +352,13 @@ def test_native_chain_loopback_exchange(F, lds, graph, clen, tiles):
         check(lib.wg_dist_info(h, info), "dist_info")
         if tiles:
             assert "tiles:" in L.describe(F), L.describe(F)
+            # the tail beside the dense blocks (hyb_conc): off and forced on, bitwise the same
+            for conc in (0, 2, 1):
+                L.tune(hyb_conc=conc)
+                for _ in range(2):   # eager, then replayed (or eager again where the tail runs beside)
+                    S.fill_(float("nan"))
+                    check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")
+                    assert np.array_equal(S.cpu().numpy(), res[0]), f"hyb_conc={conc}"
         assert info[0] == 0 and info[5] == 2 and info[7] == 1, list(info)
         L.profile_enable(True)
         check(lib.wg_dist_wavelet_features(h, ptr(X), F, K, 0.8, ptr(S), ptr(H), st), "dist_wavelet_features")
