@@ -206,7 +206,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.chain_fault = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hyb_conc")) {
-    if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "hyb_conc must be 0, 1 (auto) or 2 (always)");
+    if (value < 0 || value > 3) return fail(WG_ERR_INVALID, "hyb_conc must be 0, 1 (auto), 2 (always) or 3 (two streams)");
     L->tune.hyb_conc = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "chain_solo")) {

@@ -251,7 +251,8 @@ struct Tuning {
                              // u_0 only (the first launch gathers it; the rest as 1); 0 = the full pass
   int32_t hyb_conc = 1;      // hybrid step with the team-kernel tail: the tail's row sums on a second stream
                              // beside the dense blocks, then one epilogue pass (step.hip); 1 = when the
-                             // blocks leave the GPU half idle (tiles.hip hybrid_conc_applies), 2 = always
+                             // blocks leave the GPU half idle (tiles.hip hybrid_conc_applies), 2 = always;
+                             // one fused launch where the tile shape allows, else (and with 3) two streams
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
   int64_t team_tail = 8 << 20;  // the hybrid step's tail on the team kernel up to this many entries
   int32_t team_order = -1;   // team.hip: wave dispatch order (0 longest rows first, 1 reversed, 2 .. 7 mixed;
@@ -454,12 +455,18 @@ int prof_mark(wg_laplacian_s* L, hipStream_t stream, bool start);
 // tiles.hip: the hybrid step's plan (*out = nullptr: not applicable) and its dense-block pass,
 // which writes part = sum over the dense entries of u_j (value-free steps) for the planned rows
 bool tiles_wanted(const wg_laplacian_s* L, int64_t F);
-// the hybrid step runs its tail beside the dense blocks (hyb_conc) on a plan already built: a chain that
-// would replay as a hipGraph runs eagerly instead (the captured fork / join replays slower, dist.hip)
+// the hybrid step runs its tail beside the dense blocks on a second stream (hyb_conc, a plan already built,
+// not the fused launch's shape): a chain that would replay as a hipGraph runs eagerly instead (the
+// captured fork / join replays slower, dist.hip)
 bool hybrid_conc_in_use(const wg_laplacian_s* L, int64_t F);
-bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp);
+bool hybrid_fused_shape(const wg_laplacian_s* L, const TilePlan* tp, int64_t F);
+bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp, int64_t F);
 int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out);
 int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream);
+// the dense blocks and the team-kernel tail sums (a.tsum) in one launch, then the blocks' combine
+// (WG_ERR_UNSUPPORTED: not the default tile shape)
+int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, const TeamPlan& tp,
+                        const StepArgs& a, hipStream_t stream);
 void release_tiles(wg_laplacian_s* L);
 // u = x * dinv for rows [0, n) of an F-wide signal (in place allowed): the hybrid chain's first
 // step gathers u_0 = X0 * dinv value-free like every later step

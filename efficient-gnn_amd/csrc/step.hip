@@ -928,9 +928,12 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
   // hyb: the hybrid step's tail pass (phase 4 over the tail-first columns, + the blocks' sums)
   // conc (hyb_conc): the hybrid tail's sums go to L->tsum on the second stream; its arguments are kept
   // for the epilogue pass (hybrid_epilogue_kernel) that follows the join
-  StepArgs conc_args{};
+  StepArgs conc_args{}, conc_fused{};
   int64_t conc_rows = -1;
-  auto tiles_loop = [&](const TilePlan* hyb, hipStream_t tail_stream = nullptr, double* tsum = nullptr) -> int {
+  const TeamPlan* conc_team = nullptr;
+  // defer: build the tail's plan and arguments (conc_fused, conc_team) without launching (the fused launch)
+  auto tiles_loop = [&](const TilePlan* hyb, hipStream_t tail_stream = nullptr, double* tsum = nullptr,
+                        bool defer = false) -> int {
     if (!tail_stream) tail_stream = stream;
     for (int64_t f0 = 0; f0 < F; f0 += max_tile) {
       const int64_t fw = std::min<int64_t>(max_tile, F - f0);
@@ -1014,6 +1017,11 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
           conc_args = a;
           conc_rows = plan->row1;
           a.tsum = tsum;
+          if (defer) {
+            conc_fused = a;
+            conc_team = &plan->team;
+            continue;
+          }
         }
         if (int rc2 = launch_team4(plan->team, a, L->tune.team, tail_stream)) return rc2;
         continue;
@@ -1085,11 +1093,13 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
     TilePlan* tp = nullptr;
     if (int rc = get_tile_plan(L, active_only, F, &tp)) return rc;
     if (tp) {
-      const bool conc = vec == 4 && F <= max_tile && hybrid_conc_applies(L, tp) && gather4_applies(L, F);
+      const bool conc = vec == 4 && F <= max_tile && hybrid_conc_applies(L, tp, F) && gather4_applies(L, F);
       if (conc) {  // the tail's sums on the second stream beside the dense blocks, then one epilogue pass
         if (!L->side) WG_HIP_TRY(hipStreamCreateWithFlags(&L->side, hipStreamNonBlocking));
-        if (!L->side_fork) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_fork, hipEventDisableTiming));
-        if (!L->side_join) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_join, hipEventDisableTiming));
+        // device-local ordering only: no system-scope fence on the fork / join records
+        const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
+        if (!L->side_fork) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_fork, evf));
+        if (!L->side_join) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_join, evf));
         const int64_t need = L->n_rows * F;
         if (L->tsum_n < need) {
           (void)hipFree(L->tsum);
@@ -1098,12 +1108,21 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
           if (int rc = dmalloc(&L->tsum, (size_t)need)) return rc;
           L->tsum_n = need;
         }
-        WG_HIP_TRY(hipEventRecord(L->side_fork, stream));
-        WG_HIP_TRY(hipStreamWaitEvent(L->side, L->side_fork, 0));
-        if (int rc = tiles_loop(tp, L->side, L->tsum)) return rc;
-        if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
-        WG_HIP_TRY(hipEventRecord(L->side_join, L->side));
-        WG_HIP_TRY(hipStreamWaitEvent(stream, L->side_join, 0));
+        int frc = WG_ERR_UNSUPPORTED;
+        if (L->tune.hyb_conc != 3) {  // one launch: the dense blocks' workgroups, then the tail's waves
+          if (int rc = tiles_loop(tp, stream, L->tsum, /*defer=*/true)) return rc;
+          if (!conc_team) return fail(WG_ERR_INVALID, "launch_step: the hybrid tail's plan was not built");
+          frc = launch_hybrid_fused(L, tp, F, xm1, *conc_team, conc_fused, stream);
+          if (frc && frc != WG_ERR_UNSUPPORTED) return frc;
+        }
+        if (frc == WG_ERR_UNSUPPORTED) {  // two streams
+          WG_HIP_TRY(hipEventRecord(L->side_fork, stream));
+          WG_HIP_TRY(hipStreamWaitEvent(L->side, L->side_fork, 0));
+          if (int rc = tiles_loop(tp, L->side, L->tsum)) return rc;
+          if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
+          WG_HIP_TRY(hipEventRecord(L->side_join, L->side));
+          WG_HIP_TRY(hipStreamWaitEvent(stream, L->side_join, 0));
+        }
         if (conc_rows < 0) return fail(WG_ERR_INVALID, "launch_step: the concurrent hybrid tail did not run");
         if (conc_rows > 0) {
           const int G = 64 / conc_args.LF;

@@ -38,6 +38,7 @@
 #include <type_traits>
 
 #include "internal.h"
+#include "team_dev.h"
 
 namespace wg {
 namespace {
@@ -48,7 +49,6 @@ constexpr int kItemMax = 256;  // dense blocks per work item (tile_max <= 256)
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -104,7 +104,7 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 // rows; FW = true: wave w multiplies column block w % NFB for RG row groups, so each B
 // fragment read from LDS serves RG row groups (NFB * 8 / RG waves for 128 rows)
 template <int NFB, int NWV, int RG, bool FW>
-__global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 && NFB < 4 ? WG_TILES_MINW : 4)) void cheb_tiles_kernel(TileArgs t) {
+__device__ __forceinline__ void tiles_item(const TileArgs& t, int item) {
   constexpr int NRW = FW ? NWV / NFB : NWV;  // waves along the rows
   constexpr int NFW = FW ? 1 : NFB;          // column blocks per wave
   constexpr int TR = 16 * NRW * RG;    // rows per row block (RG groups of 16 per wave)
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 && NFB < 4 ? WG_TILES_
       d[q] = (((e >> (2 * q)) & 1) ? 0x3F80u : 0u) | (((e >> (2 * q + 1)) & 1) ? 0x3F800000u : 0u);
     lut[e] = make_uint4(d[0], d[1], d[2], d[3]);
   }
-  const int4 it = t.items[blockIdx.x];
+  const int4 it = t.items[item];
   const int64_t rb = it.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int rwave = FW ? wave / NFB : wave;        // the wave's slot along the rows
@@ -308,6 +308,26 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 && NFB < 4 ? WG_TILES_
 #pragma unroll
       for (int fw = 0; fw < NFW; ++fw) dst[16 * (fb0 + fw) + (lane & 15)] = acc[g][fw][i];
     }
+}
+
+template <int NFB, int NWV, int RG, bool FW>
+__global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 && NFB < 4 ? WG_TILES_MINW : 4)) void cheb_tiles_kernel(TileArgs t) {
+  tiles_item<NFB, NWV, RG, FW>(t, (int)blockIdx.x);
+}
+
+// The hybrid step with its tail beside the dense blocks in ONE launch (tuning key hyb_conc): workgroups
+// [0, n_items) are the tile kernel's items (128-row blocks, 8 waves), the rest are 8 team-kernel waves each
+// summing rows' tails into a.tsum (team_wave with tsum: no epilogue).  Tiles first in dispatch order.  No
+// stream fork / join (a captured or eager cross-stream join cost ~10 us per step, r05 s45-s46)
+template <int NFB>
+__global__ __launch_bounds__(512, NFB < 4 ? WG_TILES_MINW : 4) void hybrid_fused_kernel(TileArgs tt, TeamArgs ta,
+                                                                                          int32_t n_items) {
+  if ((int)blockIdx.x < n_items) {
+    tiles_item<NFB, 8, 1, false>(tt, (int)blockIdx.x);
+    return;
+  }
+  const int w = ((int)blockIdx.x - n_items) * 8 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w < ta.n_waves) team_wave<false, 2>(ta, w);
 }
 
 // The same product on v_mfma_f32_32x32x16_bf16 (tile_mfma = 32; widths 48 and 64, 128-row
@@ -655,19 +675,31 @@ bool tiles_wanted(const wg_laplacian_s* L, int64_t F) {
   return L->tune.tiles == 1 || L->nnz >= ((int64_t)8 << 20);
 }
 
-bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp) {
+bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp, int64_t F) {
   if (!tp || !L->tune.hyb_conc || !L->tune.team || L->nnz - tp->dense_nnz > L->tune.team_tail) return false;
-  if (L->tune.hyb_conc == 2) return true;
-  // auto: only a plan whose dense blocks leave the GPU half idle (fewer work items than two per CU: the
-  // 8-way Reddit-size F = 41 shard, 469 items, 156.5 vs 168.7 us per step with its exchange; the 4-way
-  // shard, slower beside: 262.7 vs 251.0, r05 s37-s38)
+  if (L->tune.hyb_conc >= 2) return true;
+  // auto: the one-launch form wherever its tile shape applies (Reddit-size F = 41 shards, step alone:
+  // 8-way 102.0-102.5 vs 131.4-133.5 us, 4-way 208.4-209.3 vs 220.6, r05 s47-s48); the two-stream form
+  // only for a plan whose dense blocks leave the GPU half idle (fewer work items than two per CU: the
+  // 8-way shard 156.5 vs 168.7 us per step with its exchange, the 4-way one slower beside: 262.7 vs
+  // 251.0, r05 s37-s38)
+  if (hybrid_fused_shape(L, tp, F)) return true;
   return (int64_t)tp->n_items < 2 * (int64_t)n_cus(L->device);
 }
 
+// the fused launch's tile shape: 128-row blocks, one 16-row group per wave, the 16x16x32 MFMA
+bool hybrid_fused_shape(const wg_laplacian_s* L, const TilePlan* tp, int64_t F) {
+  const int shape = L->tune.tile_mfma > 0 ? L->tune.tile_mfma : (F == 64 ? 32 : 16);
+  return tp && tp->rows == 128 && L->tune.tile_rg == 1 && shape == 16 && F % 16 == 0 && F <= 64 &&
+         L->tune.hyb_conc != 3;
+}
+
+// a chain whose hybrid step forks a second stream (not the fused launch) runs eagerly
 bool hybrid_conc_in_use(const wg_laplacian_s* L, int64_t F) {
   if (!tiles_wanted(L, F)) return false;
+  const int64_t Fp = F + (-F % 16 + 16) % 16;  // the width the hybrid step runs at
   for (const TilePlan* tp : L->tiles)
-    if (hybrid_conc_applies(L, tp)) return true;
+    if (hybrid_conc_applies(L, tp, Fp) && !hybrid_fused_shape(L, tp, Fp)) return true;
   return false;
 }
 
@@ -709,10 +741,8 @@ int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out
   return WG_OK;
 }
 
-int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream) {
-  if (F % 16 != 0 || F > 64 || F > p->width || (reinterpret_cast<uintptr_t>(u) & 15))
-    return fail(WG_ERR_INVALID, "launch_tiles: width %lld (need a multiple of 16 <= %d, 16-B aligned u)", (long long)F,
-                std::min(64, (int)p->width));
+namespace {
+TileArgs tile_args(const TilePlan* p, int64_t F, const float* u) {
   TileArgs t{};
   t.u = u;
   t.ld = F;
@@ -723,6 +753,57 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
   t.items = p->items;
   t.part = p->part;
   t.slots = p->slots;
+  return t;
+}
+
+int launch_tiles_combine(const TilePlan* p, int64_t F, hipStream_t stream) {
+  if (p->n_multi <= 0) return WG_OK;
+  const dim3 grid((unsigned)ceil_div(p->rows * F, 256), p->n_multi), block(256);
+  const int TR = p->rows;
+  switch (F / 16) {
+    case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+    case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+    case 3: hipLaunchKernelGGL(tiles_combine_kernel<48>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+    default: hipLaunchKernelGGL(tiles_combine_kernel<64>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+  }
+  WG_LAUNCH_CHECK();
+  return WG_OK;
+}
+}  // namespace
+
+int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, const TeamPlan& tp,
+                        const StepArgs& a, hipStream_t stream) {
+  // the default tile shape only: 128-row blocks, one 16-row group per wave, the 16x16x32 MFMA
+  if (!hybrid_fused_shape(L, p, F) || F > p->width || (reinterpret_cast<uintptr_t>(u) & 15) || !a.tsum ||
+      tp.n_waves < 0)
+    return WG_ERR_UNSUPPORTED;
+  const TileArgs tt = tile_args(p, F, u);
+  TeamArgs ta{};
+  ta.a = a;
+  ta.a.sell = tp.sell;
+  ta.wd = tp.wd;
+  ta.n_waves = tp.n_waves;
+  ta.wpart = tp.wpart;
+  ta.warr = tp.warr;
+  const int64_t nb = (int64_t)p->n_items + ceil_div((int64_t)tp.n_waves, 8);
+  if (nb > 0) {
+    const dim3 grid((unsigned)nb), block(512);
+    switch (F / 16) {
+      case 1: hipLaunchKernelGGL(hybrid_fused_kernel<1>, grid, block, 0, stream, tt, ta, p->n_items); break;
+      case 2: hipLaunchKernelGGL(hybrid_fused_kernel<2>, grid, block, 0, stream, tt, ta, p->n_items); break;
+      case 3: hipLaunchKernelGGL(hybrid_fused_kernel<3>, grid, block, 0, stream, tt, ta, p->n_items); break;
+      default: hipLaunchKernelGGL(hybrid_fused_kernel<4>, grid, block, 0, stream, tt, ta, p->n_items); break;
+    }
+    WG_LAUNCH_CHECK();
+  }
+  return launch_tiles_combine(p, F, stream);
+}
+
+int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream) {
+  if (F % 16 != 0 || F > 64 || F > p->width || (reinterpret_cast<uintptr_t>(u) & 15))
+    return fail(WG_ERR_INVALID, "launch_tiles: width %lld (need a multiple of 16 <= %d, 16-B aligned u)", (long long)F,
+                std::min(64, (int)p->width));
+  const TileArgs t = tile_args(p, F, u);
   if (p->n_items > 0) {
     // 128-row blocks: 8 waves of 16 rows, or (tile_rg = 2) 4 waves of two 16-row groups sharing
     // each B fragment (half the LDS reads)
@@ -749,18 +830,7 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
 #undef WG_TILES
     WG_LAUNCH_CHECK();
   }
-  if (p->n_multi > 0) {
-    const dim3 grid((unsigned)ceil_div(p->rows * F, 256), p->n_multi), block(256);
-    const int TR = p->rows;
-    switch (F / 16) {
-      case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
-      case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
-      case 3: hipLaunchKernelGGL(tiles_combine_kernel<48>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
-      default: hipLaunchKernelGGL(tiles_combine_kernel<64>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
-    }
-    WG_LAUNCH_CHECK();
-  }
-  return WG_OK;
+  return launch_tiles_combine(p, F, stream);
 }
 
 }  // namespace wg
