@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--traffic-json", default="auto",
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py); "
-                         "'auto': the committed PMC summary of the default workload (profiles/r04/s48_traffic.json, "
+                         "'auto': the committed PMC summary of the default workload (profiles/r05/s5_traffic.json, "
                          "tools/session.sh pmc) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--sharded-extra", default="reddit-f41,reddit,rmat-8m,ogbn-arxiv",
