@@ -587,11 +587,12 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
     if (nb > 0) rbs.push_back(make_int2((int)rb, first));  // nb == 0: every entry is tail, no part added
   }
   // work items: a row block's dense blocks, split over several workgroups (slots) past tmax;
-  // auto (tile_max <= 0): 128 blocks per workgroup from 100 k rows, else 64 (Reddit-size F=41,
-  // 128 vs 64: whole graph 751 vs 773 us per step, 2-way shard 383 vs 408; the 4- and 8-way
-  // shards want more workgroups: 259 vs 242 and 184 vs 153; profiles/r02/s80-s81)
+  // auto (tile_max <= 0): 128 blocks per workgroup from 40 k rows, else 96.  Reddit-size F=41 (width
+  // 48), us per step: whole graph and 2-way shard 726 / 369 at 128 vs 735 / 382 at 192 (sequential
+  // step); with the fused launch (tiles.hip hybrid_fused_kernel) the 4-way shard 173.4 at 128 vs 212.8
+  // at 64, the 8-way one 101.6 at 96 vs 103.9 at 64 and 103.0 at 112 (r05 s55-s56)
   const int64_t nblk = (int64_t)bct.size();
-  if (tmax <= 0) tmax = n_plan >= 100000 ? 128 : 64;
+  if (tmax <= 0) tmax = n_plan >= 40000 ? 128 : 96;
   tmax = std::min(tmax, kItemMax);
   for (size_t q0 = 0; q0 < rbs.size(); ++q0) {
     const int rb = rbs[q0].x, first = rbs[q0].y;
