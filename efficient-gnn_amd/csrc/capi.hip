@@ -191,7 +191,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.tile_mfma = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_max")) {
-    if (value < 0 || value > 256) return fail(WG_ERR_INVALID, "tile_max must be in [0 (auto), 256]");
+    if (value < 0 || value > 512) return fail(WG_ERR_INVALID, "tile_max must be in [0 (auto), 512]");
     L->tune.tile_max = (int32_t)value;
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;

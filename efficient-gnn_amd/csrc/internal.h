@@ -459,6 +459,7 @@ bool tiles_wanted(const wg_laplacian_s* L, int64_t F);
 // not the fused launch's shape): a chain that would replay as a hipGraph runs eagerly instead (the
 // captured fork / join replays slower, dist.hip)
 bool hybrid_conc_in_use(const wg_laplacian_s* L, int64_t F);
+bool hybrid_tail_on_team(const wg_laplacian_s* L, const TilePlan* tp, int64_t F);
 bool hybrid_fused_shape(const wg_laplacian_s* L, const TilePlan* tp, int64_t F);
 bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp, int64_t F);
 int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out);

@@ -985,8 +985,9 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       const bool g4 = vec == 4 && a.uin && F == fw && gather4_applies(L, F);
       // the hybrid step's tail on independent waves up to team_tail entries: larger tails keep the
       // workgroup kernel and its tiered plan (Reddit-size F = 41, width 48: 1 / 2 / 4 / 8-way shards
-      // 798 / 411 / 224 / 133 us per step with the team tail vs 719 / 367 / 233 / 145; r04 s38)
-      const bool team_here = L->tune.team && (!hyb || L->nnz - hyb->dense_nnz <= L->tune.team_tail);
+      // 798 / 411 / 224 / 133 us per step with the team tail vs 719 / 367 / 233 / 145; r04 s38), up to
+      // twice that where the fused launch takes the step (tiles.hip hybrid_tail_on_team)
+      const bool team_here = L->tune.team && (!hyb || hybrid_tail_on_team(L, hyb, F));
       const bool fold = cl && cl->x0c;  // the folded chain's first launch (team kernel only)
       if (fold && !(g4 && team_here && !hyb && f0 == 0))
         return fail(WG_ERR_INVALID, "launch_step: a folded first launch needs the team kernel");

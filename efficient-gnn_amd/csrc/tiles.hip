@@ -44,7 +44,7 @@ namespace wg {
 namespace {
 
 constexpr int kTC = 32;  // columns per tile (the MFMA's K)
-constexpr int kItemMax = 256;  // dense blocks per work item (tile_max <= 256)
+constexpr int kItemMax = 512;  // dense blocks per work item (tile_max <= 512)
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -586,13 +586,21 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
     const int32_t nb = (int32_t)bct.size() - first;
     if (nb > 0) rbs.push_back(make_int2((int)rb, first));  // nb == 0: every entry is tail, no part added
   }
-  // work items: a row block's dense blocks, split over several workgroups (slots) past tmax;
-  // auto (tile_max <= 0): 128 blocks per workgroup from 40 k rows, else 96.  Reddit-size F=41 (width
-  // 48), us per step: whole graph and 2-way shard 726 / 369 at 128 vs 735 / 382 at 192 (sequential
-  // step); with the fused launch (tiles.hip hybrid_fused_kernel) the 4-way shard 173.4 at 128 vs 212.8
-  // at 64, the 8-way one 101.6 at 96 vs 103.9 at 64 and 103.0 at 112 (r05 s55-s56)
+  // work items: a row block's dense blocks, split over several workgroups (slots) past tmax.  Auto
+  // (tile_max <= 0) for the sequential step: 128 blocks per workgroup from 100 k rows, else 64
+  // (Reddit-size F=41, width 48, us per step: whole graph 726 at 128 vs 735 at 192, 2-way shard 369 vs
+  // 382; smaller shards want more workgroups, profiles/r02/s80-s81).  Where the fused launch takes the
+  // plan (hybrid_fused_kernel: the tail's waves fill the GPU beside the items) fewer, longer items pay,
+  // about n_plan / 310 blocks each: 8-way shard 101.6 at 96 vs 103.9 at 64 and 103.0 at 112, 4-way 173
+  // at 128-192 vs 212.8 at 64 and 196 at 256, 2-way 326-331 at 384 vs 340 at 320 and 368-371 at 512
+  // (r05 s55-s60, profiles/r05/s55_s60_tile_items.log)
   const int64_t nblk = (int64_t)bct.size();
-  if (tmax <= 0) tmax = n_plan >= 40000 ? 128 : 96;
+  if (tmax <= 0) {
+    const bool fused = L->tune.team && L->tune.hyb_conc && L->tune.hyb_conc != 3 && kTR == 128 &&
+                       L->tune.tile_rg == 1 && nnz - dense <= 2 * L->tune.team_tail;  // hybrid_tail_on_team
+    tmax = fused ? (int)std::min<int64_t>(kItemMax, std::max<int64_t>(96, n_plan / 310 / 16 * 16))
+                 : (n_plan >= 100000 ? 128 : 64);
+  }
   tmax = std::min(tmax, kItemMax);
   for (size_t q0 = 0; q0 < rbs.size(); ++q0) {
     const int rb = rbs[q0].x, first = rbs[q0].y;
@@ -676,8 +684,18 @@ bool tiles_wanted(const wg_laplacian_s* L, int64_t F) {
   return L->tune.tiles == 1 || L->nnz >= ((int64_t)8 << 20);
 }
 
+// the hybrid step's tail on the team kernel: up to team_tail entries, or twice that where the fused launch
+// takes the step (2-way Reddit-size shard, 12.1 M tail entries: 350.6 vs 368.3 us per step on the
+// workgroup kernel; one GPU, 24.2 M: 803 vs 720, r05 s59)
+bool hybrid_tail_on_team(const wg_laplacian_s* L, const TilePlan* tp, int64_t F) {
+  if (!tp || !L->tune.team) return false;
+  const int64_t tail = L->nnz - tp->dense_nnz;
+  if (tail <= L->tune.team_tail) return true;
+  return tail <= 2 * L->tune.team_tail && L->tune.hyb_conc && hybrid_fused_shape(L, tp, F);
+}
+
 bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp, int64_t F) {
-  if (!tp || !L->tune.hyb_conc || !L->tune.team || L->nnz - tp->dense_nnz > L->tune.team_tail) return false;
+  if (!tp || !L->tune.hyb_conc || !hybrid_tail_on_team(L, tp, F)) return false;
   if (L->tune.hyb_conc >= 2) return true;
   // auto: the one-launch form wherever its tile shape applies (Reddit-size F = 41 shards, step alone:
   // 8-way 102.0-102.5 vs 131.4-133.5 us, 4-way 208.4-209.3 vs 220.6, r05 s47-s48); the two-stream form
