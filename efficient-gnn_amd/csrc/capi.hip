@@ -184,14 +184,13 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     L->tune.tile_rows = (int32_t)value;
   } else if (!strcmp(key, "tile_rg")) {
     if (value != 1 && value != 2 && value != 4) return fail(WG_ERR_INVALID, "tile_rg must be 1, 2 or 4");
-    L->tune.tile_rg = (int32_t)value;
-    return WG_OK;  // launch-time choice
+    L->tune.tile_rg = (int32_t)value;  // plans rebuilt (the fused launch's tile items)
   } else if (!strcmp(key, "tile_mfma")) {
     if (value != 0 && value != 16 && value != 32) return fail(WG_ERR_INVALID, "tile_mfma must be 0 (auto), 16 or 32");
     L->tune.tile_mfma = (int32_t)value;
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "tile_max")) {
-    if (value < 0 || value > 512) return fail(WG_ERR_INVALID, "tile_max must be in [0 (auto), 512]");
+    if (value < 0 || value > 1024) return fail(WG_ERR_INVALID, "tile_max must be in [0 (auto), 1024]");
     L->tune.tile_max = (int32_t)value;
   } else if (!strcmp(key, "lds_perm")) {
     L->tune.lds_perm = value ? 1 : 0;
@@ -207,8 +206,7 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "hyb_conc")) {
     if (value < 0 || value > 3) return fail(WG_ERR_INVALID, "hyb_conc must be 0, 1 (auto), 2 (always) or 3 (two streams)");
-    L->tune.hyb_conc = (int32_t)value;
-    return WG_OK;  // launch-time choice
+    L->tune.hyb_conc = (int32_t)value;  // plans rebuilt: the fused launch's tile items are longer
   } else if (!strcmp(key, "chain_solo")) {
     if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "chain_solo must be 0, 1 (auto) or 2 (wherever it fits)");
     L->tune.chain_solo = (int32_t)value;  // plans rebuilt
@@ -242,6 +240,9 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "fold must be 0, 1 or 2");
     L->tune.fold = (int32_t)value;
     return WG_OK;  // launch-time choice
+  } else if (!strcmp(key, "hyb_iter")) {
+    if (value < 8 || value > 4096) return fail(WG_ERR_INVALID, "hyb_iter must be in [8, 4096]");
+    L->tune.hyb_iter = (int32_t)value;
   } else if (!strcmp(key, "team_iter")) {
     if (value < 8 || value > 4096) return fail(WG_ERR_INVALID, "team_iter must be in [8, 4096]");
     L->tune.team_iter = (int32_t)value;

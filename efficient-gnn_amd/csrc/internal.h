@@ -254,6 +254,9 @@ struct Tuning {
                              // blocks leave the GPU half idle (tiles.hip hybrid_conc_applies), 2 = always;
                              // one fused launch where the tile shape allows, else (and with 3) two streams
   int32_t team_iter = 96;    // team.hip: target entries per lane sub-group
+  int32_t hyb_iter = 128;    // the same for the hybrid step's tail (8 / 4 / 2-way Reddit-size shards and the
+                             // whole graph, fused launch: 100.1 / 171.4 / 323.5 / 692 us per step vs 101.5 /
+                             // 173.0 / 331.4 / 705 at 96, r05 s58-s65)
   int64_t team_tail = 8 << 20;  // the hybrid step's tail on the team kernel up to this many entries
   int32_t team_order = -1;   // team.hip: wave dispatch order (0 longest rows first, 1 reversed, 2 .. 7 mixed;
                              // -1 auto: 2 for plain steps, 0 for the hybrid step's tail)

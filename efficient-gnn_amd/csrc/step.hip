@@ -993,7 +993,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         return fail(WG_ERR_INVALID, "launch_step: a folded first launch needs the team kernel");
       if (g4 && team_here) {
         if (!plan->team.wd)
-          if (int rc2 = build_team_waves(L, plan->row1, LF, L->tune.team_iter, hyb ? hyb->tcol : L->col,
+          if (int rc2 = build_team_waves(L, plan->row1, LF, hyb ? L->tune.hyb_iter : L->tune.team_iter, hyb ? hyb->tcol : L->col,
                                          hyb ? hyb->tsplit : nullptr,
                                          L->tune.team_order >= 0 ? L->tune.team_order : (hyb ? 0 : 2), &plan->team))
             return rc2;

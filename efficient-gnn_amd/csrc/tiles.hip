@@ -44,7 +44,7 @@ namespace wg {
 namespace {
 
 constexpr int kTC = 32;  // columns per tile (the MFMA's K)
-constexpr int kItemMax = 512;  // dense blocks per work item (tile_max <= 512)
+constexpr int kItemMax = 1024;  // dense blocks per work item (tile_max <= 1024)
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -592,12 +592,12 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   // 382; smaller shards want more workgroups, profiles/r02/s80-s81).  Where the fused launch takes the
   // plan (hybrid_fused_kernel: the tail's waves fill the GPU beside the items) fewer, longer items pay,
   // about n_plan / 310 blocks each: 8-way shard 101.6 at 96 vs 103.9 at 64 and 103.0 at 112, 4-way 173
-  // at 128-192 vs 212.8 at 64 and 196 at 256, 2-way 326-331 at 384 vs 340 at 320 and 368-371 at 512
-  // (r05 s55-s60, profiles/r05/s55_s60_tile_items.log)
+  // at 128-192 vs 212.8 at 64 and 196 at 256, 2-way 326-331 at 384 vs 340 at 320 and 368-371 at 512,
+  // whole graph 692-694 at 640-768 vs 705 at 512 and 745 at 1024 (r05 s55-s65)
   const int64_t nblk = (int64_t)bct.size();
   if (tmax <= 0) {
     const bool fused = L->tune.team && L->tune.hyb_conc && L->tune.hyb_conc != 3 && kTR == 128 &&
-                       L->tune.tile_rg == 1 && nnz - dense <= 2 * L->tune.team_tail;  // hybrid_tail_on_team
+                       L->tune.tile_rg == 1;  // hybrid_fused_shape, less its width checks
     tmax = fused ? (int)std::min<int64_t>(kItemMax, std::max<int64_t>(96, n_plan / 310 / 16 * 16))
                  : (n_plan >= 100000 ? 128 : 64);
   }
@@ -684,14 +684,14 @@ bool tiles_wanted(const wg_laplacian_s* L, int64_t F) {
   return L->tune.tiles == 1 || L->nnz >= ((int64_t)8 << 20);
 }
 
-// the hybrid step's tail on the team kernel: up to team_tail entries, or twice that where the fused launch
-// takes the step (2-way Reddit-size shard, 12.1 M tail entries: 350.6 vs 368.3 us per step on the
-// workgroup kernel; one GPU, 24.2 M: 803 vs 720, r05 s59)
+// the hybrid step's tail on the team kernel: up to team_tail entries in the sequential step (larger tails
+// keep the workgroup kernel's tiered plan), any length where the fused launch takes the step (Reddit-size
+// F = 41, us per step against the sequential workgroup tail: 2-way shard, 12.1 M tail entries, 323.5 vs
+// 368.3; one GPU, 24.2 M, 692 vs 722 -- with longer tile items and hyb_iter 128, r05 s59-s65)
 bool hybrid_tail_on_team(const wg_laplacian_s* L, const TilePlan* tp, int64_t F) {
   if (!tp || !L->tune.team) return false;
-  const int64_t tail = L->nnz - tp->dense_nnz;
-  if (tail <= L->tune.team_tail) return true;
-  return tail <= 2 * L->tune.team_tail && L->tune.hyb_conc && hybrid_fused_shape(L, tp, F);
+  if (L->nnz - tp->dense_nnz <= L->tune.team_tail) return true;
+  return L->tune.hyb_conc && hybrid_fused_shape(L, tp, F);
 }
 
 bool hybrid_conc_applies(const wg_laplacian_s* L, const TilePlan* tp, int64_t F) {

@@ -49,7 +49,7 @@ def test_tiles_vs_oracle_and_gather(F, k):
     for four row groups (tile_rg = 4); the 32x32x16 MFMA shape (tile_mfma = 32,
     widths 48 / 64; narrower widths keep the 16x16x32 kernel); the first step
     gathers u_0 = X0 * dinv value-free (K = 1: the only step); the tail entries on
-    the independent-wave kernel (csrc/team.hip; team_iter 8: long tails as part
+    the independent-wave kernel (csrc/team.hip; hyb_iter 8: long tails as part
     waves) and on the workgroup kernel (team = 0)."""
     g = rmat_graph(4000, 120000, seed=F + k)
     A = g.to_scipy()
@@ -61,7 +61,7 @@ def test_tiles_vs_oracle_and_gather(F, k):
                   dict(tile_th=1, tile_max=1, tile_rows=128, tile_rg=1), dict(tile_th=16, tile_max=5, tile_rows=128, tile_rg=4),
                   dict(tile_th=1, tile_max=1, tile_rows=128, tile_mfma=32),
                   dict(tile_th=16, tile_max=5, tile_rows=128, tile_mfma=32),
-                  dict(tile_th=16, tile_max=5, tile_rows=128, team_iter=8),
+                  dict(tile_th=16, tile_max=5, tile_rows=128, team_iter=8, hyb_iter=8),
                   dict(tile_th=8, tile_max=3, tile_rows=64, team=0, team_iter=96)):
         H1, S1 = _run(L, X, k, tiles=1, **knobs)
         assert "tiles:" in L.describe(F), f"hybrid step not planned: {L.describe(F)}"
@@ -109,13 +109,13 @@ def test_tiles_tail_beside_blocks(F, k):
     one epilogue pass after the join (csrc/step.hip hybrid_epilogue_kernel) give the
     same S and H as the sequential hybrid step, bit for bit (the same float64 sums
     in the same order), with and without closed-form rows and long tails split over
-    part waves (team_iter 8); and the oracle's."""
+    part waves (hyb_iter 8); and the oracle's."""
     g = rmat_graph(6000, 150000, seed=F + k)
     for gg in (g, connect_isolated(g, seed=2)):
         X = np.random.default_rng(F + 7 * k).standard_normal((gg.n, F)).astype(np.float32)
         ref = O.graph_wavelet_features(gg.to_scipy(), k=k, s=0.8, X0=X, return_all=True)
         L = NormalizedLaplacian.from_graph(gg)
-        for knobs in (dict(tile_th=16, tile_max=5, tile_rows=128), dict(tile_th=8, tile_max=3, tile_rows=64, team_iter=8)):
+        for knobs in (dict(tile_th=16, tile_max=5, tile_rows=128), dict(tile_th=8, tile_max=3, tile_rows=64, team_iter=8, hyb_iter=8)):
             H0, S0 = _run(L, X, k, tiles=1, hyb_conc=0, **knobs)
             H1, S1 = _run(L, X, k, tiles=1, hyb_conc=2, **knobs)
             H2, S2 = _run(L, X, k, tiles=1, hyb_conc=2, **knobs)
