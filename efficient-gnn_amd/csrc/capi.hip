@@ -339,8 +339,14 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
     snprintf(buf, sizeof(buf), "split rows: %d pending_arrivals=%d\n", p->n_split, pending(p->arrivals, p->n_split));
     g_text += buf;
   }
-  for (int i = 1; i >= 0; --i)  // the hybrid step's plan, once a chain has built it
-    if (L->tiles[i]) g_text += L->tiles[i]->text;
+  for (int i = 1; i >= 0; --i)  // the hybrid step's plan, once a chain has built it, and the forms it ran in
+    if (L->tiles[i]) {
+      const TilePlan* tp = L->tiles[i];
+      g_text += tp->text;
+      snprintf(buf, sizeof(buf), "hybrid forms: fused=%lld two_stream=%lld sequential=%lld\n",
+               (long long)tp->form_launches[2], (long long)tp->form_launches[1], (long long)tp->form_launches[0]);
+      g_text += buf;
+    }
   if (F == 1) {
     Lds1Plan* lp = nullptr;
     if (!get_lds1_plan(L, true, &lp) && lp) g_text += lp->text;
@@ -785,6 +791,10 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
     }
   }
   WG_HIP_TRY(hipGraphLaunch(g.exec, g.cap));
+  if (L->chain1) {  // the replay may hold the one-launch chain: wg_chain_status waits for this replay
+    WG_HIP_TRY(hipEventRecord(L->chain1->done, g.cap));
+    L->chain1->done_stale = false;
+  }
   WG_HIP_TRY(hipEventRecord(g.join, g.cap));
   WG_HIP_TRY(hipStreamWaitEvent(stream, g.join, 0));
   return WG_OK;

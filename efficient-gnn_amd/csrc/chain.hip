@@ -1013,6 +1013,7 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     WG_HIP_TRY(hipStreamIsCapturing(stream, &cs));
     if (cs == hipStreamCaptureStatusNone) WG_HIP_TRY(hipEventRecord(p->done, stream));
+    p->done_stale = cs != hipStreamCaptureStatusNone;
     return prof_mark(L, stream, false);
   }
   if (int rc = ensure_dyn_lds((const void*)cheb_chain1_kernel, kChainLds)) return rc;
@@ -1063,7 +1064,13 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   WG_HIP_TRY(hipStreamIsCapturing(stream, &cs));
   if (cs == hipStreamCaptureStatusNone) WG_HIP_TRY(hipEventRecord(p->done, stream));
+  p->done_stale = cs != hipStreamCaptureStatusNone;
   return prof_mark(L, stream, false);
+}
+
+void chain1_turn_off(wg_laplacian_s* L) {
+  if (!L->chain1_off) ++L->tune_gen;  // a captured chain holding the one-launch kernel is re-captured
+  L->chain1_off = true;
 }
 
 int chain1_check(wg_laplacian_s* L) {
@@ -1074,7 +1081,7 @@ int chain1_check(wg_laplacian_s* L) {
   const int32_t failed = __atomic_load_n(p->host_flag, __ATOMIC_ACQUIRE);
   if (failed == p->seen) return WG_OK;
   p->seen = failed;
-  L->chain1_off = true;  // later calls take the multi-launch path
+  chain1_turn_off(L);  // later calls take the multi-launch path
   ++L->chain1_timeouts;
   return fail(WG_ERR_TIMEOUT,
               "wg_wavelet_features: a previous one-launch chain (csrc/chain.hip) gave up waiting for a worker; its "
@@ -1085,11 +1092,14 @@ int chain1_status(wg_laplacian_s* L, int32_t* timed_out) {
   *timed_out = 0;
   if (!L->chain1) return WG_OK;
   ChainPlan* p = L->chain1;
-  WG_HIP_TRY(hipEventSynchronize(p->done));  // the handle's last one-launch chain only (no device sync)
+  if (p->done_stale)  // the last launch sits in a graph the caller replays: no event of ours follows it
+    WG_HIP_TRY(hipDeviceSynchronize());
+  else  // the handle's last one-launch chain only (eager, or replayed from the handle's own graph)
+    WG_HIP_TRY(hipEventSynchronize(p->done));
   const int32_t failed = __atomic_load_n(p->host_flag, __ATOMIC_ACQUIRE);
   *timed_out = failed != p->seen ? 1 : 0;  // since the last report (here or by wg_wavelet_features)
   if (*timed_out) {  // later calls take the multi-launch path
-    L->chain1_off = true;
+    chain1_turn_off(L);
     ++L->chain1_timeouts;
   }
   p->seen = failed;

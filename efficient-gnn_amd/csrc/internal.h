@@ -169,11 +169,20 @@ struct TilePlan {
   uint32_t* bmask = nullptr;   // device [n_blocks][rows]: row masks (bit k = column 32 * tile + k)
   int4* items = nullptr;       // device [n_items]: {row block, first block, end block, slot or -1}
   int4* multi = nullptr;       // device [n_multi]: {row block, first slot, slots, 0}
+  // the same blocks as work items of the fused launch (hybrid_fused_kernel: longer items beside the tail's
+  // waves); equal to the set above when both sizes agree (an explicit tile_max)
+  int32_t n_fitems = 0, n_fmulti = 0, n_fslots = 0;
+  int4* fitems = nullptr;
+  int4* fmulti = nullptr;
   int32_t* tcol = nullptr;     // device [nnz]: each row's tail entries first (the rest of its range unused)
   int32_t* tsplit = nullptr;   // device [n_rows]: end of each row's tail (== row end: no dense entries)
   int32_t width = 0;           // doubles per row of part / slots
   double* part = nullptr;      // device [n_rows][width]: the dense blocks' sums
-  double* slots = nullptr;     // device [n_slots][rows][width]
+  double* slots = nullptr;     // device [max(n_slots, n_fslots)][rows][width]
+  // hybrid steps issued per form (captured launches count once, at capture): [0] sequential (the tile
+  // kernel, then the tail with its epilogue), [1] two streams (the tail's sums beside the blocks), [2] fused
+  // (hybrid_fused_kernel); wg_laplacian_describe names them
+  int64_t form_launches[3] = {0, 0, 0};
   std::string text;
   void release();
 };
@@ -286,6 +295,8 @@ struct ChainPlan {
   int32_t* d_host_flag = nullptr;  // its device address
   int32_t seen = 0;                // the host_flag value already reported
   hipEvent_t done = nullptr;       // recorded after every launch: chain1_status waits for it alone
+  bool done_stale = false;         // the last launch was captured into a graph (its replay records done
+                                   // when it is the handle's own, capi.hip; a caller's graph: a device sync)
   uint64_t* gbuf = nullptr;   // device [2][ustride]: tagged u granules {float bits, tag << 32}
   float* u0 = nullptr;        // device [n_act]: u_0 = X0 * dinv
   float* x0 = nullptr;        // device [n_act]: X0 in internal order
@@ -481,6 +492,9 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
                   hipStream_t stream);
 void release_chain1(wg_laplacian_s* L);
 int chain1_status(wg_laplacian_s* L, int32_t* timed_out);
+// a launch timed out: the multi-launch path until the next tune; the tuning generation moves on, so a
+// chain captured with the one-launch kernel (capi.hip ChainGraph) is dropped instead of replayed
+void chain1_turn_off(wg_laplacian_s* L);
 // WG_ERR_TIMEOUT (once) when a launch of the one-launch chain gave up a wait since the last report
 int chain1_check(wg_laplacian_s* L);
 // lds1.hip

@@ -1115,6 +1115,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
           if (!conc_team) return fail(WG_ERR_INVALID, "launch_step: the hybrid tail's plan was not built");
           frc = launch_hybrid_fused(L, tp, F, xm1, *conc_team, conc_fused, stream);
           if (frc && frc != WG_ERR_UNSUPPORTED) return frc;
+          if (!frc) ++tp->form_launches[2];
         }
         if (frc == WG_ERR_UNSUPPORTED) {  // two streams
           WG_HIP_TRY(hipEventRecord(L->side_fork, stream));
@@ -1123,6 +1124,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
           if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
           WG_HIP_TRY(hipEventRecord(L->side_join, L->side));
           WG_HIP_TRY(hipStreamWaitEvent(stream, L->side_join, 0));
+          ++tp->form_launches[1];
         }
         if (conc_rows < 0) return fail(WG_ERR_INVALID, "launch_step: the concurrent hybrid tail did not run");
         if (conc_rows > 0) {
@@ -1136,6 +1138,7 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
       }
       if (int rc = launch_tiles(L, tp, F, xm1, stream)) return rc;
       if (int rc = tiles_loop(tp)) return rc;
+      ++tp->form_launches[0];
       return finish();
     }
   }

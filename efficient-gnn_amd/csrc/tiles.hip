@@ -586,8 +586,9 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
     const int32_t nb = (int32_t)bct.size() - first;
     if (nb > 0) rbs.push_back(make_int2((int)rb, first));  // nb == 0: every entry is tail, no part added
   }
-  // work items: a row block's dense blocks, split over several workgroups (slots) past tmax.  Auto
-  // (tile_max <= 0) for the sequential step: 128 blocks per workgroup from 100 k rows, else 64
+  // work items: a row block's dense blocks, split over several workgroups (slots) past tmax, one list
+  // per form (the plan serves every width; hybrid_fused_shape picks the form per width at launch).  Auto
+  // (tile_max <= 0) for the sequential and two-stream steps: 128 blocks per workgroup from 100 k rows, else 64
   // (Reddit-size F=41, width 48, us per step: whole graph 726 at 128 vs 735 at 192, 2-way shard 369 vs
   // 382; smaller shards want more workgroups, profiles/r02/s80-s81).  Where the fused launch takes the
   // plan (hybrid_fused_kernel: the tail's waves fill the GPU beside the items) fewer, longer items pay,
@@ -595,27 +596,35 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   // at 128-192 vs 212.8 at 64 and 196 at 256, 2-way 326-331 at 384 vs 340 at 320 and 368-371 at 512,
   // whole graph 692-694 at 640-768 vs 705 at 512 and 745 at 1024 (r05 s55-s65)
   const int64_t nblk = (int64_t)bct.size();
-  if (tmax <= 0) {
-    const bool fused = L->tune.team && L->tune.hyb_conc && L->tune.hyb_conc != 3 && kTR == 128 &&
-                       L->tune.tile_rg == 1;  // hybrid_fused_shape, less its width checks
-    tmax = fused ? (int)std::min<int64_t>(kItemMax, std::max<int64_t>(96, n_plan / 310 / 16 * 16))
-                 : (n_plan >= 100000 ? 128 : 64);
-  }
-  tmax = std::min(tmax, kItemMax);
-  for (size_t q0 = 0; q0 < rbs.size(); ++q0) {
-    const int rb = rbs[q0].x, first = rbs[q0].y;
-    const int32_t nb = (int32_t)((q0 + 1 < rbs.size() ? rbs[q0 + 1].y : nblk) - first);
-    const int32_t k = (nb + tmax - 1) / tmax;
-    if (k == 1) {
-      items.push_back(make_int4(rb, first, first + nb, -1));
-    } else {
-      for (int32_t q = 0; q < k; ++q)
-        items.push_back(make_int4(rb, first + (int32_t)((int64_t)nb * q / k), first + (int32_t)((int64_t)nb * (q + 1) / k),
-                                  n_slots + q));
-      multi.push_back(make_int4(rb, n_slots, k, 0));
-      n_slots += k;
+  // one item list per form: {items, multi, slots}
+  auto make_items = [&](int tm, std::vector<int4>& its, std::vector<int4>& mul) {
+    tm = std::max(1, std::min(tm, kItemMax));
+    int32_t ns = 0;
+    for (size_t q0 = 0; q0 < rbs.size(); ++q0) {
+      const int rb = rbs[q0].x, first = rbs[q0].y;
+      const int32_t nb = (int32_t)((q0 + 1 < rbs.size() ? rbs[q0 + 1].y : nblk) - first);
+      const int32_t k = (nb + tm - 1) / tm;
+      if (k == 1) {
+        its.push_back(make_int4(rb, first, first + nb, -1));
+      } else {
+        for (int32_t q = 0; q < k; ++q)
+          its.push_back(make_int4(rb, first + (int32_t)((int64_t)nb * q / k), first + (int32_t)((int64_t)nb * (q + 1) / k),
+                                  ns + q));
+        mul.push_back(make_int4(rb, ns, k, 0));
+        ns += k;
+      }
     }
-  }
+    return ns;
+  };
+  const int tseq = tmax > 0 ? tmax : (n_plan >= 100000 ? 128 : 64);
+  const int tfus = tmax > 0 ? tmax : (int)std::min<int64_t>(kItemMax, std::max<int64_t>(96, n_plan / 310 / 16 * 16));
+  n_slots = make_items(tseq, items, multi);
+  std::vector<int4> fitems, fmulti;
+  // the fused launch's items only where its tile shape can apply (hybrid_fused_shape decides per width)
+  const bool fused_possible = kTR == 128 && L->tune.tile_rg == 1 && L->tune.team && L->tune.hyb_conc &&
+                              L->tune.hyb_conc != 3;
+  int32_t n_fslots = 0;
+  if (fused_possible && tfus != tseq) n_fslots = make_items(tfus, fitems, fmulti);
   p->n_plan = n_plan;
   p->col_limit = col_limit;
   p->n_blocks = (int32_t)bct.size();
@@ -627,12 +636,26 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
   if (!rc) rc = upload(&p->bmask, bmask);
   if (!rc) rc = upload(&p->items, items);
   if (!rc) rc = upload(&p->multi, multi);
+  if (fitems.empty()) {  // the fused launch walks the same items
+    p->fitems = p->items;
+    p->fmulti = p->multi;
+    p->n_fitems = p->n_items;
+    p->n_fmulti = p->n_multi;
+    p->n_fslots = p->n_slots;
+  } else {
+    if (!rc) rc = upload(&p->fitems, fitems);
+    if (!rc) rc = upload(&p->fmulti, fmulti);
+    p->n_fitems = (int32_t)fitems.size();
+    p->n_fmulti = (int32_t)fmulti.size();
+    p->n_fslots = n_fslots;
+  }
   if (!rc) rc = upload(&p->tcol, tcol);
   if (!rc) rc = upload(&p->tsplit, tsplit);
   if (rc) return rc;
   char buf[256];
-  snprintf(buf, sizeof(buf), "tiles: %d dense blocks (%dx32, >= %d entries) hold %lld of %lld entries (%.1f %%); %d items, %d split row blocks\n",
-           p->n_blocks, kTR, th, (long long)dense, (long long)nnz, nnz ? 100.0 * dense / nnz : 0.0, p->n_items, p->n_multi);
+  snprintf(buf, sizeof(buf), "tiles: %d dense blocks (%dx32, >= %d entries) hold %lld of %lld entries (%.1f %%); %d items, %d split row blocks (fused launch: %d items, %d split)\n",
+           p->n_blocks, kTR, th, (long long)dense, (long long)nnz, nnz ? 100.0 * dense / nnz : 0.0, p->n_items, p->n_multi,
+           p->n_fitems, p->n_fmulti);
   p->text = buf;
   return WG_OK;
 }
@@ -642,8 +665,12 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
 void TilePlan::release() {
   (void)hipFree(bct);
   (void)hipFree(bmask);
+  if (fitems != items) (void)hipFree(fitems);
+  if (fmulti != multi) (void)hipFree(fmulti);
   (void)hipFree(items);
   (void)hipFree(multi);
+  fitems = nullptr;
+  fmulti = nullptr;
   (void)hipFree(tcol);
   (void)hipFree(tsplit);
   (void)hipFree(part);
@@ -752,7 +779,7 @@ int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out
     p->slots = nullptr;
     p->width = 0;
     int rc = dmalloc(&p->part, (size_t)std::max<int64_t>(1, L->n_rows) * F);
-    if (!rc) rc = dmalloc(&p->slots, (size_t)std::max(1, p->n_slots) * p->rows * F);
+    if (!rc) rc = dmalloc(&p->slots, (size_t)std::max(1, std::max(p->n_slots, p->n_fslots)) * p->rows * F);
     if (rc) return rc;
     p->width = (int32_t)F;
   }
@@ -761,7 +788,7 @@ int get_tile_plan(wg_laplacian_s* L, bool active_only, int64_t F, TilePlan** out
 }
 
 namespace {
-TileArgs tile_args(const TilePlan* p, int64_t F, const float* u) {
+TileArgs tile_args(const TilePlan* p, int64_t F, const float* u, bool fused = false) {
   TileArgs t{};
   t.u = u;
   t.ld = F;
@@ -769,21 +796,23 @@ TileArgs tile_args(const TilePlan* p, int64_t F, const float* u) {
   t.n_plan = p->n_plan;
   t.bct = p->bct;
   t.bmask = p->bmask;
-  t.items = p->items;
+  t.items = fused ? p->fitems : p->items;
   t.part = p->part;
   t.slots = p->slots;
   return t;
 }
 
-int launch_tiles_combine(const TilePlan* p, int64_t F, hipStream_t stream) {
-  if (p->n_multi <= 0) return WG_OK;
-  const dim3 grid((unsigned)ceil_div(p->rows * F, 256), p->n_multi), block(256);
+int launch_tiles_combine(const TilePlan* p, int64_t F, hipStream_t stream, bool fused = false) {
+  const int32_t nm = fused ? p->n_fmulti : p->n_multi;
+  const int4* multi = fused ? p->fmulti : p->multi;
+  if (nm <= 0) return WG_OK;
+  const dim3 grid((unsigned)ceil_div(p->rows * F, 256), nm), block(256);
   const int TR = p->rows;
   switch (F / 16) {
-    case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
-    case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
-    case 3: hipLaunchKernelGGL(tiles_combine_kernel<48>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
-    default: hipLaunchKernelGGL(tiles_combine_kernel<64>, grid, block, 0, stream, p->multi, p->slots, p->part, F, p->n_plan, TR); break;
+    case 1: hipLaunchKernelGGL(tiles_combine_kernel<16>, grid, block, 0, stream, multi, p->slots, p->part, F, p->n_plan, TR); break;
+    case 2: hipLaunchKernelGGL(tiles_combine_kernel<32>, grid, block, 0, stream, multi, p->slots, p->part, F, p->n_plan, TR); break;
+    case 3: hipLaunchKernelGGL(tiles_combine_kernel<48>, grid, block, 0, stream, multi, p->slots, p->part, F, p->n_plan, TR); break;
+    default: hipLaunchKernelGGL(tiles_combine_kernel<64>, grid, block, 0, stream, multi, p->slots, p->part, F, p->n_plan, TR); break;
   }
   WG_LAUNCH_CHECK();
   return WG_OK;
@@ -796,7 +825,7 @@ int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* 
   if (!hybrid_fused_shape(L, p, F) || F > p->width || (reinterpret_cast<uintptr_t>(u) & 15) || !a.tsum ||
       tp.n_waves < 0)
     return WG_ERR_UNSUPPORTED;
-  const TileArgs tt = tile_args(p, F, u);
+  const TileArgs tt = tile_args(p, F, u, true);
   TeamArgs ta{};
   ta.a = a;
   ta.a.sell = tp.sell;
@@ -804,18 +833,19 @@ int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* 
   ta.n_waves = tp.n_waves;
   ta.wpart = tp.wpart;
   ta.warr = tp.warr;
-  const int64_t nb = (int64_t)p->n_items + ceil_div((int64_t)tp.n_waves, 8);
+  const int32_t ni = p->n_fitems;
+  const int64_t nb = (int64_t)ni + ceil_div((int64_t)tp.n_waves, 8);
   if (nb > 0) {
     const dim3 grid((unsigned)nb), block(512);
     switch (F / 16) {
-      case 1: hipLaunchKernelGGL(hybrid_fused_kernel<1>, grid, block, 0, stream, tt, ta, p->n_items); break;
-      case 2: hipLaunchKernelGGL(hybrid_fused_kernel<2>, grid, block, 0, stream, tt, ta, p->n_items); break;
-      case 3: hipLaunchKernelGGL(hybrid_fused_kernel<3>, grid, block, 0, stream, tt, ta, p->n_items); break;
-      default: hipLaunchKernelGGL(hybrid_fused_kernel<4>, grid, block, 0, stream, tt, ta, p->n_items); break;
+      case 1: hipLaunchKernelGGL(hybrid_fused_kernel<1>, grid, block, 0, stream, tt, ta, ni); break;
+      case 2: hipLaunchKernelGGL(hybrid_fused_kernel<2>, grid, block, 0, stream, tt, ta, ni); break;
+      case 3: hipLaunchKernelGGL(hybrid_fused_kernel<3>, grid, block, 0, stream, tt, ta, ni); break;
+      default: hipLaunchKernelGGL(hybrid_fused_kernel<4>, grid, block, 0, stream, tt, ta, ni); break;
     }
     WG_LAUNCH_CHECK();
   }
-  return launch_tiles_combine(p, F, stream);
+  return launch_tiles_combine(p, F, stream, true);
 }
 
 int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipStream_t stream) {

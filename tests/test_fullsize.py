@@ -75,6 +75,13 @@ def _graph(config, seed=0):
     return _GRAPHS[key]
 
 
+def _forms(describe):
+    """The hybrid step's launches per form, from wg_laplacian_describe's 'hybrid forms:' line."""
+    line = [x for x in describe.splitlines() if x.startswith("hybrid forms:")]
+    assert line, describe
+    return {k: int(v) for k, v in (t.split("=") for t in line[-1].split(":", 1)[1].split())}
+
+
 def _check_H(H, S):
     """H = S / (|S|_1 + 1e-8) (WATS.py:71-72), recomputed from S in float64."""
     Sd = S.astype(np.float64)
@@ -102,7 +109,10 @@ def test_reddit_random_signal_vs_oracle(F, cols):
     H, S = wats_hip.graph_wavelet_features(L, k=16, X0=torch.from_numpy(X), return_S=True)
     S, H = S.cpu().numpy(), H.cpu().numpy()
     if F == 41:
-        assert "tiles:" in L.describe(48), "the hybrid step did not run: " + L.describe(48)
+        d = L.describe(48)
+        assert "tiles:" in d, "the hybrid step did not run: " + d
+        # the shipped form: dense blocks and the tail's waves in one launch (hybrid_fused_kernel), every step
+        assert _forms(d) == {"fused": 16, "two_stream": 0, "sequential": 0}, d
     L.close()
     S_ref, H_ref = _oracle(indptr, indices, X, 16, cols)
     got = S if cols is None else S[:, cols]
@@ -190,8 +200,12 @@ def _shard_worker(rank, world, port, config, F, K, seed_x, q, graph_dir):
         H, S = outs[0]
         same = all(torch.equal(o[1], S) for o in outs)
         path = "u" if (F == 1 and sw.u_len() > 0) else "t"
-        if F > 1 and "tiles:" in sw.L.describe(F + (-F) % 16):
+        d = sw.L.describe(F + (-F) % 16)
+        if F > 1 and "tiles:" in d:
             path = "tiles"   # the hybrid step ran on this shard
+            f = _forms(d)
+            if f["fused"] > 0 and f["two_stream"] == 0 and f["sequential"] == 0:
+                path = "tiles-fused"   # every step in the one-launch form (hybrid_fused_kernel)
         sw.check_exchange()
         sw.close()
         q.put((rank, r0, r1, S.cpu().numpy(), H.cpu().numpy(), same, path))
@@ -240,7 +254,8 @@ def test_sharded_full_size_vs_oracle(world, config, F, cols, tmp_path):
     if F == 1 and config == "reddit":
         assert all(r[6] == "u" for r in res), "Reddit F=1 shards should run the LDS kernel"
     if F == 41:
-        assert all(r[6] == "tiles" for r in res), f"every Reddit F=41 shard should run the hybrid step: {[r[6] for r in res]}"
+        assert all(r[6] == "tiles-fused" for r in res), \
+            f"every Reddit F=41 shard should run the fused hybrid step: {[r[6] for r in res]}"
     S = np.concatenate([r[3] for r in res])
     H = np.concatenate([r[4] for r in res])
     indptr, indices = _graph(config)

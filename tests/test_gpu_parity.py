@@ -2,6 +2,7 @@
 golden vectors and the CPU oracle, on seeded inputs; size-independent
 properties (eigenvector KAT, determinism, relabelling invariance) at the
 named full sizes."""
+import ctypes
 import os
 
 import numpy as np
@@ -888,6 +889,57 @@ def test_chain1_timeout_falls_back():
     torch.cuda.synchronize()
     assert not L.chain_status() and "timeouts" not in L.describe(1).split("chain1:")[0]
     assert torch.equal(S3, S0) and torch.equal(H3, H0)
+    L.close()
+
+
+def test_chain1_timeout_in_replayed_graph():
+    """The one-launch chain captured into the handle's own hipGraph (tuning key
+    graph=1: same X0 / S / H three calls in a row) and replayed with a fault:
+    wg_chain_status waits for the replay itself (an event recorded after the
+    graph launch), reports the timeout, and the handle's captured chain is
+    dropped, so the next call with the same buffers runs the multi-launch path
+    instead of replaying the faulted one-launch chain."""
+    g = rmat_graph(19717, 88648, seed=3)
+    L = NormalizedLaplacian.from_graph(g)
+    L.tune(chain_wg=16, graph=1)
+    lib = wats_hip._lib.load()
+    X = L.log1p_degree()
+    ref = O.graph_wavelet_features(g.to_scipy(), k=16, s=0.8, X0=X.cpu().numpy(), return_all=True)
+    S = torch.zeros(L.n, 1, device=X.device)
+    H = torch.zeros(L.n, 1, device=X.device)
+    st = torch.cuda.current_stream().cuda_stream
+    call = lambda: lib.wg_wavelet_features(L.handle, X.data_ptr(), 1, 16, 0.8, S.data_ptr(), H.data_ptr(), st)
+    for _ in range(4):   # eager, eager, captured + replayed, replayed: no fault
+        assert call() == 0
+    torch.cuda.synchronize()
+    assert "chain1:" in L.describe(1)
+    assert_parity(_np(S), ref["S"], what="replayed one-launch chain S")
+    L.tune(chain_wg=16, graph=1, chain_fault=3)
+    for _ in range(3):   # eager, eager, captured + replayed: every launch gives up a wait (0.5 s each)
+        assert call() == 0
+    t = ctypes.c_int32(0)
+    assert lib.wg_chain_status(L.handle, ctypes.byref(t)) == 0 and t.value == 1
+    assert torch.isnan(S).any()
+    S.zero_()
+    H.zero_()
+    assert call() == 0    # same buffers: the captured (faulted) chain must not be replayed
+    torch.cuda.synchronize()
+    assert torch.isfinite(S).all() and torch.isfinite(H).all()
+    assert_parity(_np(S), ref["S"], what="after a replayed timeout: multi-launch S")
+    for _ in range(3):    # the multi-launch chain captured and replayed with the same buffers
+        assert call() == 0
+    torch.cuda.synchronize()
+    assert lib.wg_chain_status(L.handle, ctypes.byref(t)) == 0 and t.value == 0
+    assert_parity(_np(S), ref["S"], what="multi-launch chain replayed S")
+    # the Python drop-in with results dropped between calls (the caching allocator hands back the
+    # same S / H blocks, so the handle captures): every call's features are finite and oracle-equal
+    L.tune(chain_wg=16, graph=1, chain_fault=3)
+    for _ in range(4):
+        H1, S1 = wats_hip.graph_wavelet_features(L, k=16, s=0.8, return_S=True)
+        torch.cuda.synchronize()
+        assert torch.isfinite(S1).all() and torch.isfinite(H1).all()
+        assert_parity(_np(S1), ref["S"], what="drop-in after a timeout")
+        del H1, S1
     L.close()
 
 

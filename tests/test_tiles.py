@@ -32,6 +32,13 @@ def _run(L, X, k, **knobs):
     return wats_hip.graph_wavelet_features(L, k=k, X0=torch.from_numpy(X), return_S=True)
 
 
+def _forms(describe):
+    """The hybrid step's launches per form since the last tune ('hybrid forms:' line of describe)."""
+    line = [x for x in describe.splitlines() if x.startswith("hybrid forms:")]
+    assert line, describe
+    return {k: int(v) for k, v in (t.split("=") for t in line[-1].split(":", 1)[1].split())}
+
+
 def _close(a, b, what, tol=2e-6):
     a, b = _np(a).astype(np.float64), _np(b).astype(np.float64)
     scale = np.max(np.abs(b), axis=0) + 1e-30
@@ -120,7 +127,11 @@ def test_tiles_tail_beside_blocks(F, k):
             H1, S1 = _run(L, X, k, tiles=1, hyb_conc=2, **knobs)
             H2, S2 = _run(L, X, k, tiles=1, hyb_conc=2, **knobs)
             torch.cuda.synchronize()
-            assert "tiles:" in L.describe(F)
+            d = L.describe(F)
+            assert "tiles:" in d
+            # 128-row blocks: the one-launch form (hybrid_fused_kernel); 64-row blocks: two streams
+            form = "fused" if knobs["tile_rows"] == 128 else "two_stream"
+            assert _forms(d)[form] > 0 and _forms(d)["sequential"] == 0, d
             assert torch.equal(S0, S1) and torch.equal(H0, H1), f"F={F} K={k} {knobs}: concurrent tail differs"
             assert torch.equal(S1, S2) and torch.equal(H1, H2)
             assert_parity(_np(S1), ref["S"], what=f"F={F} K={k} {knobs} S")
@@ -204,3 +215,39 @@ def test_tiles_duplicate_entries_keep_the_gather_kernel():
     H1, S1 = _run(L, X, 6, tiles=1, tile_th=4)
     assert "tiles:" not in L.describe(48)
     assert torch.equal(S0, S1) and torch.equal(H0, H1)
+
+
+@pytest.mark.parametrize("F", [48, 64])
+def test_tiles_auto_items_default_form(F):
+    """The shipped defaults on a graph large enough for long fused items (~n_plan / 310 = 322 blocks per
+    item, past the old 256 cap): at width 48 the step runs in the fused form with its own item list,
+    at width 64 (32x32x16 MFMA, never fused) the sequential step keeps the 128-block items of the
+    sequential rule (the plan is shared across widths).  Both against the oracle and the
+    forced sequential step (hyb_conc = 0); with an explicit tile_max the fused and sequential forms
+    walk the same items and agree bit for bit."""
+    g = rmat_graph(100000, 2_400_000, seed=21)
+    X = np.random.default_rng(F).standard_normal((g.n, F)).astype(np.float32)
+    ref = O.graph_wavelet_features(g.to_scipy(), k=4, s=0.8, X0=X, return_all=True)
+    L = NormalizedLaplacian.from_graph(g)
+    H0, S0 = _run(L, X, 4, tiles=1, hyb_conc=0)
+    d0 = L.describe(F)
+    assert _forms(d0) == {"fused": 0, "two_stream": 0, "sequential": 4}, d0
+    H1, S1 = _run(L, X, 4, tiles=1)                      # defaults: tile_max auto, hyb_conc auto
+    d1 = L.describe(F)
+    items = d1.split("tiles:")[1]
+    n_seq = int(items.split(" items,")[0].split()[-1])
+    n_fus = int(items.split("fused launch: ")[1].split(" items")[0])
+    if F == 48:
+        assert _forms(d1) == {"fused": 4, "two_stream": 0, "sequential": 0}, d1
+        assert n_fus < n_seq, d1                         # longer items in the fused launch
+    else:
+        assert _forms(d1)["fused"] == 0 and _forms(d1)["two_stream"] == 0, d1
+    assert_parity(_np(S1), ref["S"], what=f"auto items F={F} S")
+    assert_parity(_np(H1), ref["H"], what=f"auto items F={F} H")
+    _close(S1, S0, f"auto items F={F} vs sequential")
+    H2, S2 = _run(L, X, 4, tiles=1, tile_max=1024)
+    H3, S3 = _run(L, X, 4, tiles=1, tile_max=1024, hyb_conc=0)
+    torch.cuda.synchronize()
+    assert torch.equal(S2, S3) and torch.equal(H2, H3), f"F={F}: default form vs hyb_conc=0 differ bitwise"
+    assert_parity(_np(S2), ref["S"], what=f"tile_max=1024 F={F} S")
+    L.close()
