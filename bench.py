@@ -768,11 +768,14 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
             "launches": prof["launches"],
             "first_launch_us": first_us,
             "all_launches_avg_us": prof["sum_ms"] / max(1, prof["launches"]) * 1e3,
+            # the same byte model over every launch of the chain, the folded first launch included
+            "frac_all_launches": b_roof / (prof["sum_ms"] / max(1, prof["launches"]) * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "launch_note": ("avg_launch_us / achieved / frac: the K - 1 plain step launches of each pass "
                             "(cheb_team4_kernel, the dominant kernel as rocprof averages it); first_launch_us: "
                             "each pass's first launch (cheb_team4_first_kernel: also reads the caller's X0 "
                             "through perm, writes the internal X0 and the closed-form rows' S / H -- the former "
-                            "permute-in pass)") if folded else None,
+                            "permute-in pass); frac_all_launches: frac's byte model over the mean of all K "
+                            "launches, the first included") if folded else None,
         },
         "chain_ms": prof["sum_ms"] / args.steps,
         "median_step_ms_profiled": median_ms,

@@ -4,7 +4,6 @@
 // (WATS.py:71-72), row permutations, halo gather, profiling and tuning.
 #include <algorithm>
 #include <cmath>
-#include <complex>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -233,9 +232,6 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "team_order")) {
     if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
     L->tune.team_order = (int32_t)value;
-  } else if (!strcmp(key, "prod")) {
-    L->tune.prod = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "fold")) {
     if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "fold must be 0, 1 or 2");
     L->tune.fold = (int32_t)value;
@@ -443,77 +439,6 @@ void ChainGraph::release() {
 
 namespace {
 
-// The heat-kernel polynomial p(x) = sum_k c_k T_k(x), c_k = exp(-s k) (WATS.py:65-68), as a product
-// p(x) = lead * prod_q (x^2 - a_q x + b_q) [* (x - r)]: its roots by Durand-Kerner on the Chebyshev
-// series (complex Clenshaw, no monomial conversion), conjugate pairs merged into real quadratics,
-// ordered alternately from the two ends of the real-part order ("interleaved": the partial products
-// then keep their range on [-1, 1] close to p's, which bounds the float32 storage error;
-// tools/prodform_sim.py).  Fails (false) when the iteration does not converge or the roots do not pair.
-struct ProdFactor {
-  int deg;      // 2: x^2 - a x + b; 1: x - a
-  double a, b;
-};
-bool prod_factors(int32_t K, double s, std::vector<ProdFactor>* out, double* lead) {
-  using cd = std::complex<double>;
-  out->clear();
-  if (K < 1 || K > 64) return false;
-  std::vector<double> c(K + 1);
-  for (int32_t k = 0; k <= K; ++k) c[k] = std::exp(-s * (double)k);
-  *lead = c[K] * std::ldexp(1.0, K - 1);  // T_K's leading coefficient is 2^(K-1)
-  auto p = [&](cd z) {  // Clenshaw in the Chebyshev basis
-    cd b1 = 0.0, b2 = 0.0;
-    for (int32_t k = K; k >= 1; --k) {
-      const cd b = c[k] + 2.0 * z * b1 - b2;
-      b2 = b1;
-      b1 = b;
-    }
-    return c[0] + z * b1 - b2;
-  };
-  std::vector<cd> z(K);
-  for (int32_t i = 0; i < K; ++i) z[i] = std::polar(1.3, 2.0 * M_PI * (i + 0.25) / K);  // off the real axis
-  for (int it = 0; it < 2000; ++it) {
-    double move = 0.0;
-    for (int32_t i = 0; i < K; ++i) {
-      cd den = *lead;
-      for (int32_t j = 0; j < K; ++j)
-        if (j != i) den *= (z[i] - z[j]);
-      const cd dz = p(z[i]) / den;
-      z[i] -= dz;
-      move = std::max(move, std::abs(dz));
-    }
-    if (move < 1e-15) break;
-  }
-  for (int32_t i = 0; i < K; ++i)
-    if (!std::isfinite(z[i].real()) || !std::isfinite(z[i].imag()) || std::abs(p(z[i])) > 1e-9) return false;
-  std::sort(z.begin(), z.end(), [](const cd& x, const cd& y) { return x.real() < y.real(); });
-  std::vector<ProdFactor> f;
-  std::vector<bool> used(K, false);
-  for (int32_t i = 0; i < K; ++i) {
-    if (used[i]) continue;
-    used[i] = true;
-    if (std::abs(z[i].imag()) < 1e-10) {
-      f.push_back(ProdFactor{1, z[i].real(), 0.0});
-      continue;
-    }
-    int32_t j = -1;
-    for (int32_t m = 0; m < K; ++m)
-      if (!used[m] && std::abs(z[m] - std::conj(z[i])) < 1e-8) {
-        j = m;
-        break;
-      }
-    if (j < 0) return false;
-    used[j] = true;
-    const cd r = 0.5 * (z[i] + std::conj(z[j]));
-    f.push_back(ProdFactor{2, 2.0 * r.real(), std::norm(r)});
-  }
-  size_t lo = 0, hi = f.size();
-  while (lo < hi) {  // interleaved: first, last, second, second last, ...
-    out->push_back(f[lo++]);
-    if (lo < hi) out->push_back(f[--hi]);
-  }
-  return true;
-}
-
 // The whole graph_wavelet_features chain (WATS.py:39-74) enqueued on `stream`: permute in, K
 // Chebyshev / Clenshaw steps, finalize.  Eager, or recorded into a hipGraph by the caller.
 int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, double s, float* S, float* H,
@@ -571,7 +496,10 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
   // launch gathers the caller's X0 through caller-row ids scaled by dinv (u_0 on the fly), reads its
   // own X0 rows at perm[row] and writes the internal X0 the later steps read, and finishes the
   // closed-form rows (team.hip cheb_team4_first_kernel): arxiv-size F = 40 -19.6 us of pass per chain
-  const bool fold = u0_fused && g4 && !tp0 && L->tune.fold && L->tune.team && L->tune.uscale &&
+  // the first launch reads a float64 dinv per SELL id slot at twice the ids' 32-bit byte offset: the
+  // slots (at most 2 nnz + 8 N with every row's padding) must stay within 2^31 bytes of it
+  const bool fold_fits = 8 * (2 * L->nnz + 8 * n) < ((int64_t)1 << 31);
+  const bool fold = u0_fused && g4 && !tp0 && L->tune.fold && L->tune.team && L->tune.uscale && fold_fits &&
                     pick_vec(F, {X0, b0, b1, sint, S, H}) == 4;
   const bool fold2 = fold && L->tune.fold == 2;  // a pass writes u_0 (internal order) only
   float* x0int = b0;  // the internal X0 the steps read (fold: written by the first launch)
@@ -581,54 +509,6 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
                                                  stream)
                       : launch_permute_pad(L, F, Fp, X0, b0, stream);
   if (rc) return rc;
-  // the product form (tuning key "prod"): S = lead * prod_q (L^2 - a_q L + b_q) X0.  Per factor two
-  // launches: w = L v (no own-row operand at all), then v' = f (L w - a w + b v) in place (own rows of
-  // w -- the vector just gathered -- and of v).  Two own-row streams per step against Clenshaw's three
-  // (X0, b_{k+2}, b_k); f = lead^(1 / factors).  The first launch is the fold's (caller X0, internal X0
-  // written to b0, closed-form rows); every stored vector is u = x * dinv
-  std::vector<ProdFactor> pf;
-  double lead = 1.0;
-  if (fold && !fold2 && L->tune.prod && prod_factors(K, s, &pf, &lead)) {
-    const double f = std::pow(std::abs(lead), 1.0 / (double)pf.size()) * (lead < 0 ? -1.0 : 1.0);
-    const double fpos = std::abs(f);
-    float* V = sint;  // u of the running product (in place over a factor's second launch)
-    float* W = b1;    // u of L v
-    bool first = true;
-    for (size_t q = 0; q < pf.size(); ++q) {
-      const bool last = q + 1 == pf.size();
-      const double fq = (q == 0) ? f : fpos;  // the sign of lead once
-      auto half = [&](const float* gather, const float* own_x0, int x0u, double ck, double cacc, const float* prev,
-                      int uprev, double cprev, float* out, bool final_) -> int {
-        ClenArgs cl{own_x0, ck, cacc, final_ ? 1 : 0};
-        cl.uin = 1;
-        cl.uprev = uprev;
-        cl.uout = final_ ? 0 : 1;
-        cl.cprev = cprev;
-        cl.x0u = x0u;
-        if (first) {  // the chain's first launch: gathers the caller's X0 (own_x0 / x0u unused)
-          cl.x0c = X0;
-          cl.x0i = x0int;
-          cl.closed = TeamFirst{L->n_active, n, coef, S, H};
-          gather = X0;
-          first = false;
-        }
-        return launch_step(L, 2, Fp, gather, prev, final_ ? nullptr : out, final_ ? sint : nullptr, final_ ? H : nullptr,
-                           1.0, 0.0, stream, true, final_ ? S : nullptr, &cl);
-      };
-      const float* vsrc = (q == 0) ? nullptr : V;  // factor 0 starts from X0 (b0, plain floats)
-      if (pf[q].deg == 2) {
-        // w = L v
-        if ((rc = half(vsrc, nullptr, 0, 0.0, 1.0, nullptr, 0, 0.0, W, false))) return rc;
-        // v' = f (L w - a w + b v): own w as u (x0u), own v as u (or X0 itself for the first factor)
-        if ((rc = half(W, W, 1, -pf[q].a * fq, fq, q == 0 ? x0int : V, q == 0 ? 0 : 1, pf[q].b * fq, V, last))) return rc;
-      } else {
-        // v' = f (L v - a v): gathers v, so it writes W, and the two swap
-        if ((rc = half(vsrc, q == 0 ? x0int : V, q == 0 ? 0 : 1, -pf[q].a * fq, fq, nullptr, 0, 0.0, W, last))) return rc;
-        std::swap(V, W);
-      }
-    }
-    return WG_OK;
-  }
   if (K == 0) WG_HIP_TRY(hipMemcpyAsync(sint, b0, sizeof(float) * n * Fp, hipMemcpyDeviceToDevice, stream));
   if (lp) {
     float* u[2] = {L->ws + 3 * stride, L->ws + 3 * stride + ustride};  // u_{k-1} = T_{k-1} * dinv

@@ -77,6 +77,9 @@ struct ChainArgs {
   int32_t fault_phase;        // fault injection (tuning key "chain_fault", tests): worker 0 skips this phase's publish
   float* S;                   // caller order
   float* H;
+#ifdef WG_DEBUG_BOUNDS
+  int32_t dbg_lds;            // the launch's dynamic LDS bytes
+#endif
   double c[kChainMaxK + 1];   // heat coefficients exp(-s k)
 };
 
@@ -206,6 +209,10 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
   const int wc0 = a.P == 1 ? 0 : a.wcol_off[w];
   const int nu = a.P == 1 ? a.n_act : a.wcol_off[w + 1] - wc0;       // columns this worker gathers
   const ChainLayout lay(nu, nr, ne, npass, a.P == 1);
+  WG_DCHECK(lay.bytes <= a.dbg_lds && row0 >= 0 && nr >= 0 && row0 + nr <= a.n_act && e0 >= 0 && ne >= 0 && nu >= 0 &&
+                nu <= a.n_act,
+            "worker %d: rows [%d, %d) entries %d+%d columns %d need %lld LDS bytes of %d", w, row0, row0 + nr, e0, ne, nu,
+            (long long)lay.bytes, a.dbg_lds);
   float* u = reinterpret_cast<float*>(smem);                         // [nu] the gathered u (local ids)
   float* u2 = reinterpret_cast<float*>(smem + lay.u2);               // [n_act] one worker: the next u
   double* dv = reinterpret_cast<double*>(smem + lay.dv);             // [nr] dinv, negative = isolated row
@@ -242,7 +249,11 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
     a.H[r] = (float)(sv / (fabs(sv) + 1e-8));
   }
   const uint16_t* idsrc = a.direct ? a.gids : a.ids;
-  for (int i = tid; i < ne; i += kChainThreads) id[i] = idsrc[e0 + i];
+  for (int i = tid; i < ne; i += kChainThreads) {
+    id[i] = idsrc[e0 + i];
+    WG_DCHECK(id[i] < (a.direct ? a.n_act : nu), "worker %d entry %d: column id %d past %d", w, e0 + i, (int)id[i],
+              a.direct ? a.n_act : nu);
+  }
   for (int i = tid; i < npass; i += kChainThreads) pas[i] = a.passes[pass0 + i];
   if (a.direct) {
     // no LDS copy of u: the gathers read u_0 and then the granules themselves
@@ -251,6 +262,7 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
   } else {
     for (int i = tid; i < nu; i += kChainThreads) {
       const int c = a.wcols[wc0 + i];
+      WG_DCHECK(c < a.n_act, "worker %d: gathered column %d past %d active rows", w, c, a.n_act);
       wc[i] = (uint16_t)c;
       u[i] = chain_u0(a, c);
     }
@@ -1056,6 +1068,9 @@ int launch_chain1(wg_laplacian_s* L, ChainPlan* p, const float* X0, int32_t K, d
   a.fault_phase = L->tune.chain_fault;
   a.S = S;
   a.H = H;
+#ifdef WG_DEBUG_BOUNDS
+  a.dbg_lds = p->lds_bytes;
+#endif
   for (int32_t k = 0; k <= K; ++k) a.c[k] = std::exp(-s * (double)k);
   if (int rc = prof_mark(L, stream, true)) return rc;
   hipLaunchKernelGGL(cheb_chain1_kernel, dim3((unsigned)(p->P * a.stride)), dim3(kChainThreads), (size_t)p->lds_bytes,

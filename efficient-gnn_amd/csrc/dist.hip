@@ -116,6 +116,9 @@ __global__ __launch_bounds__(256) void ipc_pull_kernel(IpcPull p, int slot, int6
     const int64_t idx = h0 * F + i;  // halo rows [h0, h0 + n_halo)
     const int64_t h = idx / F;
     const int q = owner[h];
+    WG_DCHECK(q >= 0 && q < p.world && q != p.rank && src[h] >= 0 && ((int64_t)src[h] + 1) * F <= p.slot_floats[q],
+              "halo row %lld: owner %d row %d outside its %lld-float slot", (long long)h, q, src[h],
+              (long long)(q >= 0 && q < kMaxPeers ? p.slot_floats[q] : -1));
     const float* from = p.slot_base[q] + slot * p.slot_floats[q] + (int64_t)src[h] * F + (idx - h * F);
     ext[n_own * F + idx] = __hip_atomic_load(from, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -135,6 +138,9 @@ __global__ __launch_bounds__(256) void ipc_pull4_kernel(IpcPull p, int slot, int
     const int64_t h = idx / F4;
     const int64_t c4 = idx - h * F4;
     const int q = owner[h];
+    WG_DCHECK(q >= 0 && q < p.world && q != p.rank && src[h] >= 0 && ((int64_t)src[h] + 1) * F <= p.slot_floats[q],
+              "halo row %lld: owner %d row %d outside its %lld-float slot", (long long)h, q, src[h],
+              (long long)(q >= 0 && q < kMaxPeers ? p.slot_floats[q] : -1));
     const float* base = p.slot_base[q] + slot * p.slot_floats[q];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff,
                                                                         0x00020000);

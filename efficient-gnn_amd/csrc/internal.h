@@ -31,6 +31,24 @@ int n_cus(int dev);
 
 #define WG_LAUNCH_CHECK() WG_HIP_TRY(hipGetLastError())
 
+// Device bounds checks of the debug variant (make VARIANT=debug EXTRA_FLAGS=-DWG_DEBUG_BOUNDS):
+// gathered column ids against the gathered vector, wave descriptors against their plan, LDS indices
+// against the staged sizes, halo rows against their slots.  A failed check prints where and what, then
+// traps (the launch fails with a located message instead of a silent out-of-bounds access).  The shipped
+// library compiles them out.
+#ifdef WG_DEBUG_BOUNDS
+#define WG_DCHECK(cond, fmt, ...)                                                                          \
+  do {                                                                                                     \
+    if (__builtin_expect(!(cond), 0)) {                                                                    \
+      printf("WG_DEBUG_BOUNDS %s:%d block %d thread %d: " fmt "\n", __FILE__, __LINE__, (int)blockIdx.x,   \
+             (int)threadIdx.x, ##__VA_ARGS__);                                                             \
+      __builtin_trap();                                                                                    \
+    }                                                                                                      \
+  } while (0)
+#else
+#define WG_DCHECK(cond, fmt, ...) ((void)0)
+#endif
+
 constexpr int kBlock = 256;   // 4 waves of 64 lanes
 constexpr int kMaxSeg = 24;
 constexpr int kBuckets = 33;  // row-length buckets: b=0: len<=1; b>0: 2^(b-1) < len <= 2^b
@@ -79,6 +97,7 @@ struct TeamPlan {
   int32_t n_waves = 0, n_slots = 0, n_long = 0, width = 0;
   int32_t max_parts = 0, npot_rows = 0;  // long rows: most parts; rows whose part count is not a power of 2
   int64_t n_sell = 0;        // int4 chunks in sell (its padding included)
+  int64_t n_rows = 0;        // rows of the table ([0, n_rows): the debug variant checks descriptors against it)
   int4* sell0 = nullptr;     // device [n_sell]: sell with caller-row ids (the folded chain's first launch)
   double* sdinv = nullptr;   // device [4 n_sell]: dinv of each id slot of sell (0 for pads)
   void release();
@@ -251,8 +270,6 @@ struct Tuning {
   int32_t sell = 1;          // padded-CSR steps: team waves read their ids in SELL order (step.hip build_sell)
   int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 .. 13:
                              // register-budget / turn-size variants (team.hip launch_team4; all time the same)
-  int32_t prod = 0;          // wg_wavelet_features on the team kernel: the heat-kernel polynomial as a product
-                             // of quadratic factors (capi.hip prod_factors): 2 own-row streams per step
                              // instead of Clenshaw's 3; 0 = Clenshaw
   int32_t fold = 1;          // wg_wavelet_features on the team kernel: no permute-in pass (the first launch
                              // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
@@ -422,10 +439,6 @@ struct ClenArgs {
   // unweighted graphs (L->unit): the chain vectors as u = b * dinv (no CSR values read);
   // uin: xm1 is u, uprev: xm2 is u, uout: write u (not on the final step)
   int uin = 0, uprev = 0, uout = 0;
-  // the product-form chain (capi.hip, tuning key "prod"): out = ck * X0' + cacc * (L_hat b) + cprev * b''
-  // with X0' = x0 read as u (divided by dinv) when x0u; x0 == nullptr: no X0 term at all
-  double cprev = -1.0;
-  int x0u = 0;
   // fold (the chain's first launch, team kernel only): gather the caller's X0 (x0c, caller rows) as
   // u = X0 * dinv on the fly, read the own X0 row at perm[row], write the internal X0 (x0i, read by
   // the later steps through x0), and finish the closed-form rows (closed.S / closed.H, caller order)

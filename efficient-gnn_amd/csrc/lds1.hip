@@ -149,6 +149,11 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_lds1_kernel(Lds1Args a) {
         acc += (double)x3;
       }
       for (; e < e1; e += ln) acc += (double)u[bcol[e]];
+#ifdef WG_DEBUG_BOUNDS
+      for (int32_t e2 = rp[row] + q; e2 < e1; e2 += ln)
+        WG_DCHECK(bcol[e2] < a.lchunks * 32, "block %d row %d: local column %d past %d staged", b, row, (int)bcol[e2],
+                  a.lchunks * 32);
+#endif
     }
     for (int o = ln >> 1; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
     if (act && q == 0) {
@@ -198,6 +203,8 @@ __global__ __launch_bounds__(kLdsThreads) void cheb_hub1_kernel(Lds1Args a) {
 #ifdef WG_TIMING_PROBES
     if (a.probe_fold > 0 && c >= H && c != kPadCol) c = H + ((c - H) & (a.probe_fold - 1));
 #endif
+    WG_DCHECK(c == kPadCol || (c >= 0 && (c < H || (uint64_t)(c - gs) * 4u + 4u <= (uint64_t)a.u_bytes)),
+              "hub teams: column %d (hub %d, shift %d) past the %u-byte gathered vector", c, H, gs, (unsigned)a.u_bytes);
     const float xl = u[min(c, H)];
     const uint32_t off = c >= H ? (uint32_t)(c - gs) * 4u : kDrop;
     const float xg = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));

@@ -964,8 +964,6 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.x0 = cl->x0 ? cl->x0 + f0 : nullptr;
         a.ck = cl->ck;
         a.cacc = cl->cacc;
-        a.cprev = cl->cprev;
-        a.x0u = cl->x0u;
         if (!cl->final_) a.S = nullptr;
         a.dinv = L->dinv;
         a.uin = cl->uin;
@@ -1005,6 +1003,9 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         a.probe_ns = L->tune.probe_ns;
         if (fold) {
           if (cl->closed.gather_x0) {
+            if (32 * plan->team.n_sell > (int64_t)0x7fffffff)  // sdinv at 2 x the ids' 32-bit byte offsets
+              return fail(WG_ERR_UNSUPPORTED, "launch_step: %lld id slots: the folded first launch cannot address "
+                          "their dinv", (long long)(4 * plan->team.n_sell));
             if (int rc2 = build_team_first(L, &plan->team)) return rc2;
             a.xm1 = cl->x0c;
           }

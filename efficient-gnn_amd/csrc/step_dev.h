@@ -35,9 +35,7 @@ struct StepArgs {
   int32_t vidx;
   int32_t clen;        // 0 = forward recurrence + heat sum; 1 / 2 = Clenshaw step / final (ClenArgs)
   const float* x0;     // Clenshaw: X0 rows (internal order, stride ld)
-  double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc + cprev * xm2 (cprev -1; x0 nullable: no X0 term)
-  double cprev;
-  int32_t x0u;         // x0 holds u = x * dinv (the product form's own row of the gathered vector)
+  double ck, cacc;     // Clenshaw: out = ck * X0 + cacc * acc - xm2
   // Clenshaw on unweighted graphs (L_hat_ij = -dinv_i dinv_j): the chain carries u = b * dinv, so the
   // gathers need no values (val == nullptr: every value 1).  uin: xm1 holds u; uprev: xm2 holds u;
   // uout: xk gets u.
@@ -78,6 +76,9 @@ struct StepArgs {
   const float* x0c;
   float* x0i;
   const int32_t* perm_in;
+#ifdef WG_DEBUG_BOUNDS
+  uint64_t dbg_sell_bytes;  // bytes of sell (0: unchecked)
+#endif
 };
 
 // a padded-CSR column id whose byte offset (id * row bytes <= 256) lies past every gathered buffer
@@ -249,12 +250,11 @@ __device__ __forceinline__ void step_epilogue(const StepArgs& a, int64_t row, in
     for (int j = 0; j < VEC; ++j) acc[j] -= (double)x[j] * xs;
   }
   double t[VEC];
-  if (a.clen) {  // Clenshaw: b = ck * X0 + cacc * (L_hat b') - b'' (product form: cprev, x0u)
+  if (a.clen) {  // Clenshaw: b = ck * X0 + cacc * (L_hat b') - b''
     const double ps = a.uprev ? 1.0 / in.dinv : 1.0;
-    const double xs0 = a.x0u ? 1.0 / in.dinv : 1.0;
 #pragma unroll
     for (int j = 0; j < VEC; ++j)
-      t[j] = a.ck * ((double)in.sold[j] * xs0) + a.cacc * acc[j] + a.cprev * ((double)in.prev[j] * ps);
+      t[j] = a.ck * (double)in.sold[j] + a.cacc * acc[j] - (double)in.prev[j] * ps;
     if (a.uout && a.xk) {
       double u[VEC];
 #pragma unroll
@@ -659,6 +659,7 @@ __device__ __forceinline__ void sum_turn(const u32x4_t* x, int n, double (&acc)[
 // fl32(x * dinv[c]) (scale_rows' rounding, so the sums are the permute-in path's bit for bit); the
 // chunk's 4 dinv values (32 B per chunk at twice its id offset) are loaded with its gathers
 __device__ __forceinline__ void scale_chunk(const __amdgpu_buffer_rsrc_t& rd, uint32_t off, u32x4_t* x) {
+  WG_DCHECK((uint64_t)off < 0x40000000ull, "first launch: dinv slot at byte %llu past 2^31", 2ull * off);
   const u32x4_t d01 = __builtin_amdgcn_raw_buffer_load_b128(rd, 2u * off, 0, 0);
   const u32x4_t d23 = __builtin_amdgcn_raw_buffer_load_b128(rd, 2u * off + 16u, 0, 0);
   const double d[4] = {__hiloint2double((int)d01.y, (int)d01.x), __hiloint2double((int)d01.w, (int)d01.z),
@@ -686,8 +687,14 @@ __device__ __forceinline__ void accumulate_sell(const StepArgs& a, int2 wm, int 
   uint32_t off = ((uint32_t)wm.x + (uint32_t)g) * 16u;  // byte offset of this sub-group's chunk 0
   const uint32_t cstep = (uint32_t)G * 16u;                // next chunk of the same sub-group
   // volatile (aux bit 31): the next turn's ids are not sunk to their use (accumulate_u4)
-  auto ld = [&](uint32_t o) { return __builtin_amdgcn_raw_buffer_load_b128(ri, o, 0, (int)(1u << 31)); };
+  auto ld = [&](uint32_t o) {
+    WG_DCHECK(a.dbg_sell_bytes == 0 || (uint64_t)o + 16u <= a.dbg_sell_bytes, "SELL id load at byte %u of %llu", o,
+              (unsigned long long)a.dbg_sell_bytes);
+    return __builtin_amdgcn_raw_buffer_load_b128(ri, o, 0, (int)(1u << 31));
+  };
   auto gather = [&](uint32_t c) -> u32x4_t {
+    WG_DCHECK(c == (uint32_t)kPadCol || (uint64_t)c * rb + lo + 16u <= a.u_bytes,
+              "gathered column %u (row bytes %u, lane offset %u) past the %u-byte gathered vector", c, rb, lo, a.u_bytes);
 #ifdef WG_TIMING_PROBES
     if (a.probe_fold > 0 && c != (uint32_t)kPadCol) c &= (uint32_t)(a.probe_fold - 1);
     if (a.probe_h2 == -1) return u32x4_t{c, 0u, 0u, 0u};

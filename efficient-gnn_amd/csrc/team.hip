@@ -215,6 +215,7 @@ int build_team_waves(wg_laplacian_s* L, int64_t n, int LF, int iter, const int32
   }
   tp->n_waves = (int32_t)(wd.size() / 2);
   tp->n_sell = (int64_t)sell.size();
+  tp->n_rows = n;
   tp->n_slots = slots;
   tp->n_long = longs;
   tp->width = LF * 4;
@@ -238,6 +239,7 @@ int launch_team4(const TeamPlan& tp, const StepArgs& a, int variant, hipStream_t
   t.wpart = tp.wpart;
   t.warr = tp.warr;
   t.a.sell = tp.sell;
+  team_args_debug(t, tp);
   if (first) {  // the folded chain's first launch
     const bool gx = first->gather_x0;
     if (gx && !tp.sell0) return fail(WG_ERR_INVALID, "launch_team4: no first-launch table");

@@ -25,7 +25,23 @@ struct TeamArgs {
   double coef;
   float* cS;
   float* cH;
+#ifdef WG_DEBUG_BOUNDS
+  int64_t dbg_rows, dbg_slots, dbg_long;  // the table's rows, partial slots and long rows
+#endif
 };
+
+// the debug variant's plan sizes (WG_DEBUG_BOUNDS; nothing in the shipped library)
+inline void team_args_debug(TeamArgs& t, const TeamPlan& tp) {
+#ifdef WG_DEBUG_BOUNDS
+  t.dbg_rows = tp.n_rows;
+  t.dbg_slots = tp.n_slots;
+  t.dbg_long = tp.n_long;
+  t.a.dbg_sell_bytes = 16ull * (uint64_t)tp.n_sell;
+#else
+  (void)t;
+  (void)tp;
+#endif
+}
 
 constexpr int kClosedRG = 4;  // row groups per closed-form wave (their loads all issued before any use)
 
@@ -92,6 +108,9 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
   const int ns = sg - team * LN;
   const int64_t row = (int64_t)d0.z + team;
   const bool active = sg < G && team < tpw;
+  WG_DCHECK(d0.z >= 0 && (int64_t)d0.z + (part ? 1 : tpw) <= t.dbg_rows && d0.y >= 0 && LN >= 1 && (part || tpw * LN <= G),
+            "wave %d: descriptor {%d, %d, %d, %#x} outside the %lld-row table", w, d0.x, d0.y, d0.z, d0.w,
+            (long long)t.dbg_rows);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   EpiIn<4> in;
 #ifdef WG_TIMING_PROBES
@@ -113,6 +132,10 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
   if (part) {  // a share of a long row: float64 partial (sc1), drained, then one arrival per wave
     const int4 d1 = t.wd[2 * w + 1];
     const int width = LF * 4;
+    WG_DCHECK(d1.x >= 0 && d1.x < d1.y && d1.z >= 0 && (int64_t)d1.z + d1.y <= t.dbg_slots && d1.w >= 0 &&
+                  d1.w < t.dbg_long,
+              "part wave %d: {%d, %d, %d, %d} outside %lld slots / %lld long rows", w, d1.x, d1.y, d1.z, d1.w,
+              (long long)t.dbg_slots, (long long)t.dbg_long);
     if (lane < LF) {
       double* p = t.wpart + (int64_t)(d1.z + d1.x) * width + lane * 4;
 #pragma unroll

@@ -75,6 +75,9 @@ struct TileArgs {
   const int4* items;
   double* part;          // [rows][ld]
   double* slots;         // [slot][rows per block][W]
+#ifdef WG_DEBUG_BOUNDS
+  int64_t dbg_blocks, dbg_slots;  // dense blocks and float64 slots of the plan
+#endif
 };
 
 // u = hi + mid + lo exactly, each piece a bf16 (the high half of a float32)
@@ -133,8 +136,16 @@ __device__ __forceinline__ void tiles_item(const TileArgs& t, int item) {
   const int mrow = 16 * RG * rwave + (lane & 15);  // this lane's A row of row group 0 (of the block)
   const int mshift = 8 * (lane >> 4);              // its byte of the 32-bit row mask
   const int32_t b0 = it.y, n = it.z - it.y;  // n <= kItemMax (build_tile_plan)
+  WG_DCHECK(b0 >= 0 && n >= 0 && n <= kItemMax && (int64_t)it.z <= t.dbg_blocks && it.w < (int)t.dbg_slots &&
+                rb * TR < t.n_plan,
+            "tile item %d: {%d, %d, %d, %d} outside %lld blocks / %lld slots / %lld rows", item, it.x, it.y, it.z, it.w,
+            (long long)t.dbg_blocks, (long long)t.dbg_slots, (long long)t.n_plan);
   __shared__ int32_t sbct[kItemMax];         // the item's column tiles: no global load ahead of each tile load
-  for (int e = tid; e < n; e += NT) sbct[e] = t.bct[b0 + e];
+  for (int e = tid; e < n; e += NT) {
+    sbct[e] = t.bct[b0 + e];
+    WG_DCHECK(sbct[e] >= 0 && (int64_t)sbct[e] * kTC < t.col_limit, "block %d: column tile %d past %lld columns",
+              b0 + e, sbct[e], (long long)t.col_limit);
+  }
   __syncthreads();
 
   // a tile's loads, in a register ring RD tiles deep: PER float4 of u (staged into LDS) and the
@@ -365,6 +376,9 @@ __global__ __launch_bounds__(512, WG_TILES32_MINW) void cheb_tiles32_kernel(Tile
   const int64_t rb = it.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int32_t b0 = it.y, n = it.z - it.y;
+  WG_DCHECK(b0 >= 0 && n >= 0 && n <= kItemMax && (int64_t)it.z <= t.dbg_blocks && it.w < (int)t.dbg_slots,
+            "tile item %d: {%d, %d, %d, %d} outside %lld blocks / %lld slots", (int)blockIdx.x, it.x, it.y, it.z, it.w,
+            (long long)t.dbg_blocks, (long long)t.dbg_slots);
   __shared__ int32_t sbct[kItemMax];
   for (int e = tid; e < n; e += NT) sbct[e] = t.bct[b0 + e];
   __syncthreads();
@@ -797,6 +811,10 @@ TileArgs tile_args(const TilePlan* p, int64_t F, const float* u, bool fused = fa
   t.bct = p->bct;
   t.bmask = p->bmask;
   t.items = fused ? p->fitems : p->items;
+#ifdef WG_DEBUG_BOUNDS
+  t.dbg_blocks = p->n_blocks;
+  t.dbg_slots = fused ? p->n_fslots : p->n_slots;
+#endif
   t.part = p->part;
   t.slots = p->slots;
   return t;
@@ -833,6 +851,7 @@ int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* 
   ta.n_waves = tp.n_waves;
   ta.wpart = tp.wpart;
   ta.warr = tp.warr;
+  team_args_debug(ta, tp);
   const int32_t ni = p->n_fitems;
   const int64_t nb = (int64_t)ni + ceil_div((int64_t)tp.n_waves, 8);
   if (nb > 0) {

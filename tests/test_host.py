@@ -32,6 +32,17 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
 
 
+def test_shipped_library_has_no_debug_checks():
+    """The bounds-checked variant (make VARIANT=debug EXTRA_FLAGS=-DWG_DEBUG_BOUNDS, tools/debug_suite.sh)
+    is a separate library: the shipped one carries none of its checks (their message tag is absent
+    from every code object), and the Makefile builds the variant under its own name."""
+    shipped = os.path.join(REPO, "efficient-gnn_amd", "wats_hip", "libwats_hip.so")
+    assert os.path.exists(shipped)
+    assert b"WG_DEBUG_BOUNDS" not in open(shipped, "rb").read()
+    mk = open(os.path.join(REPO, "efficient-gnn_amd", "csrc", "Makefile")).read()
+    assert "libwats_hip_$(VARIANT).so" in mk and "debug:" in mk
+
+
 def test_library_abi_version_and_errors():
     lib = _lib.load()
     assert lib.wg_abi_version() == 1
