@@ -70,9 +70,9 @@ struct ChainArgs {
   int64_t n;                  // rows; [n_act, n) are the closed-form rows (S = coef * X0)
   double coef;
   uint64_t* gbuf;             // [2][ustride] tagged granules {float bits, tag << 32}
-  int32_t* bar;               // [1] workers finished, [2] epoch of the last timed-out launch, [3] launch epoch
+  int32_t* bar;               // [1] workers finished, [2] epoch + 1 of the last timed-out launch, [3] launch epoch
                               // (bumped by the launch's last worker to finish: every worker read it first)
-  int32_t* host_flag;         // host-mapped: epoch of the last timed-out launch (read by the next API call)
+  int32_t* host_flag;         // host-mapped: epoch + 1 of the last timed-out launch (read by the next API call)
   int64_t wait_ticks;         // a granule wait gives up after this many wall-clock ticks (~0.5 s)
   int32_t fault_phase;        // fault injection (tuning key "chain_fault", tests): worker 0 skips this phase's publish
   float* S;                   // caller order
@@ -150,8 +150,9 @@ __device__ __forceinline__ bool stage_tagged(float* u, const uint64_t* g, const 
 // a granule wait that gave up: the launch's epoch recorded (once per worker) for the next API call
 __device__ __forceinline__ void chain_fail(const ChainArgs& a, int* s_bad, uint32_t ep) {
   if (atomicExch(s_bad, 1) == 0) {
-    __hip_atomic_store(a.bar + 2, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.host_flag) __hip_atomic_store(a.host_flag, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // epoch + 1: a fresh plan's flag starts at 0 (nothing reported), so its first launch (epoch 0) counts too
+    __hip_atomic_store(a.bar + 2, (int32_t)(ep + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.host_flag) __hip_atomic_store(a.host_flag, (int32_t)(ep + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -387,8 +388,8 @@ __global__ __launch_bounds__(kChainThreads) void cheb_chain1_kernel(ChainArgs a)
       u2 = t;
     } else if (!stage_tagged(u, gnext, wc, nu, (uint32_t)(tag >> 32), tid, a.wait_ticks)) {
       if (atomicExch(&s_bad, 1) == 0) {  // one lane per worker records the failed launch
-        __hip_atomic_store(a.bar + 2, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (a.host_flag) __hip_atomic_store(a.host_flag, (int32_t)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.bar + 2, (int32_t)(ep + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.host_flag) __hip_atomic_store(a.host_flag, (int32_t)(ep + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     __syncthreads();

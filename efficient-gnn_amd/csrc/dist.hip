@@ -126,17 +126,20 @@ __global__ __launch_bounds__(256) void ipc_pull_kernel(IpcPull p, int slot, int6
 
 // The same pull with 16-B loads (F % 4 == 0: every row and slot is 16-B aligned): one
 // system-scope (sc0 sc1: no stale cached copy of the owner's slot) dwordx4 buffer load
-// per lane, 4x fewer remote transactions than ipc_pull_kernel for the F = 44 rows.
+// per lane, 4x fewer remote transactions than ipc_pull_kernel for the F = 44 rows.  Only the
+// first Fr columns of each row move (the signal's own columns rounded up to 4: F = 41 at width 48
+// pulls 176 of its 192 bytes); the halo rows' pad columns stay zero (transfer() zeroes them once).
 __global__ __launch_bounds__(256) void ipc_pull4_kernel(IpcPull p, int slot, int64_t n_own, int64_t h0, int64_t n_halo,
-                                                        int64_t F, const int32_t* __restrict__ owner,
+                                                        int64_t F, int64_t Fr, const int32_t* __restrict__ owner,
                                                         const int32_t* __restrict__ src, float* __restrict__ ext) {
   constexpr int kSysCoherent = 1 | 16;  // cache policy sc0 | sc1 (gfx940+ CPol bits)
-  const int64_t F4 = F >> 2;
-  const int64_t total = n_halo * F4;
+  const int64_t F4 = F >> 2, R4 = Fr >> 2;
+  const int64_t total = n_halo * R4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t idx = h0 * F4 + i;  // halo rows [h0, h0 + n_halo)
-    const int64_t h = idx / F4;
-    const int64_t c4 = idx - h * F4;
+    const int64_t hr = i / R4;
+    const int64_t c4 = i - hr * R4;
+    const int64_t h = h0 + hr;  // halo rows [h0, h0 + n_halo)
+    const int64_t idx = h * F4 + c4;
     const int q = owner[h];
     WG_DCHECK(q >= 0 && q < p.world && q != p.rank && src[h] >= 0 && ((int64_t)src[h] + 1) * F <= p.slot_floats[q],
               "halo row %lld: owner %d row %d outside its %lld-float slot", (long long)h, q, src[h],
@@ -254,6 +257,8 @@ struct wg_dist_s {
   std::vector<void*> peer_region;     // IPC-mapped, nullptr for self
   int64_t** peer_flags = nullptr;     // device array [world]
   IpcPull pull{};
+  int64_t F_sig = 0;        // the signal columns of the running chain (<= the exchanged width)
+  int64_t pads_zeroed = 0;  // the width whose halo pad columns the region holds as zeros
   // exchange mode "sdma" (wg_dist_ipc_sdma, after wg_dist_ipc_connect): each rank packs the rows
   // its peers asked for into one of two send buffers of its region; the receiver copies each
   // owner's packed block into its halo rows with hipMemcpyAsync on a copy stream (DMA engines
@@ -368,11 +373,19 @@ struct wg_dist_s {
       if (int rc = ipc_wait_only(st, /*signal_first=*/true)) return rc;
       const int64_t total = n_halo * F;
       const bool v4 = (F % 4 == 0) && slot_floats * 4 < ((int64_t)1 << 31);
+      // the columns that carry the signal (pad columns beyond them are zero on every owner)
+      const int64_t Fr = std::min<int64_t>(F, (F_sig + 3) / 4 * 4);
+      if (v4 && Fr < F && pads_zeroed != F) {  // pad columns of the halo rows (both slots) are never pulled
+        for (int sl = 0; sl < 2; ++sl)
+          WG_HIP_TRY(hipMemsetAsync(region + sl * slot_floats + n_own * F, 0, sizeof(float) * n_halo * F, st));
+        pads_zeroed = F;
+      }
       if (total > 0) {
-        const int blocks = (int)std::min<int64_t>(65535, ceil_div(v4 ? total / 4 : total, 256));
+        const int64_t work = v4 ? n_halo * (Fr / 4) : total;
+        const int blocks = (int)std::min<int64_t>(65535, ceil_div(work, 256));
         if (v4)
           hipLaunchKernelGGL(ipc_pull4_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, (int64_t)0, n_halo, F,
-                             halo_owner, halo_src, ext);
+                             Fr, halo_owner, halo_src, ext);
         else
           hipLaunchKernelGGL(ipc_pull_kernel, dim3(blocks), dim3(256), 0, st, pull, slot, n_own, (int64_t)0, n_halo, F,
                              halo_owner, halo_src, ext);
@@ -412,6 +425,7 @@ struct wg_dist_s {
     if (F == 1 && K >= 1)
       if (int rc = get_lds1_plan(L, /*active_only=*/false, &lp)) return rc;
     const int64_t Fp = lp ? F : padded_features(L, F);  // internal width (zero pad columns, float4 lanes)
+    F_sig = F;
     const size_t ext = ((size_t)n_cols * Fp + 63) / 64 * 64;
     const size_t own = ((size_t)n_own * Fp + 63) / 64 * 64;
     const size_t snd = ((size_t)std::max<int64_t>(n_send, 1) * Fp + 63) / 64 * 64;
