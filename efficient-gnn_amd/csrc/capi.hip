@@ -232,9 +232,6 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
   } else if (!strcmp(key, "team_order")) {
     if (value < -1 || value > 7) return fail(WG_ERR_INVALID, "team_order must be -1 (auto) or in [0, 7]");
     L->tune.team_order = (int32_t)value;
-  } else if (!strcmp(key, "closed_side")) {
-    L->tune.closed_side = value ? 1 : 0;
-    return WG_OK;  // launch-time choice
   } else if (!strcmp(key, "fold")) {
     if (value < 0 || value > 2) return fail(WG_ERR_INVALID, "fold must be 0, 1 or 2");
     L->tune.fold = (int32_t)value;
@@ -505,20 +502,6 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
   const bool fold = u0_fused && g4 && !tp0 && L->tune.fold && L->tune.team && L->tune.uscale && fold_fits &&
                     pick_vec(F, {X0, b0, b1, sint, S, H}) == 4;
   const bool fold2 = fold && L->tune.fold == 2;  // a pass writes u_0 (internal order) only
-  // closed_side: the closed-form rows on the handle's second stream beside the whole chain (the first
-  // launch then finishes none); joined back before the chain's end
-  const bool cside = fold && !fold2 && L->tune.closed_side && L->n_active < n;
-  const int64_t closed_from = cside ? n : L->n_active;
-  if (cside) {
-    if (!L->side) WG_HIP_TRY(hipStreamCreateWithFlags(&L->side, hipStreamNonBlocking));
-    const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
-    if (!L->side_fork) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_fork, evf));
-    if (!L->side_join) WG_HIP_TRY(hipEventCreateWithFlags(&L->side_join, evf));
-    WG_HIP_TRY(hipEventRecord(L->side_fork, stream));
-    WG_HIP_TRY(hipStreamWaitEvent(L->side, L->side_fork, 0));
-    if (int rc0 = launch_closed_rows(L, F, X0, coef, S, H, L->side)) return rc0;
-    WG_HIP_TRY(hipEventRecord(L->side_join, L->side));
-  }
   float* x0int = b0;  // the internal X0 the steps read (fold: written by the first launch)
   int rc = fold2 ? launch_permute_u0(L, F, X0, L->ws + 3 * stride, stream)
            : fold ? WG_OK
@@ -570,7 +553,7 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
       if (fold && bk1 == b0) {  // the first launch (fold): X0 in caller order, the internal copy written
         cl.x0c = X0;
         cl.x0i = x0int;
-        cl.closed = TeamFirst{closed_from, n, coef, S, H, !fold2};
+        cl.closed = TeamFirst{L->n_active, n, coef, S, H, !fold2};
       }
       rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold && !fold2 ? X0 : ub) : bk1, bk2, out, nullptr, nullptr, 1.0, 0.0,
                        stream, /*active_only=*/true, nullptr, &cl);
@@ -586,12 +569,11 @@ int wavelet_chain(wg_laplacian_t L, const float* X0, int64_t F, int32_t K, doubl
     cl.uprev = useu && K >= 3;
     if (fold && bk1 == b0) {  // K == 1: the final step is the first launch
       cl.x0c = X0;
-      cl.closed = TeamFirst{closed_from, n, coef, S, H, !fold2};
+      cl.closed = TeamFirst{L->n_active, n, coef, S, H, !fold2};
     }
     rc = launch_step(L, 2, Fp, (bk1 == b0 && u0) ? (fold && !fold2 ? X0 : ub) : bk1, K >= 3 ? bk2 : nullptr, nullptr, sint, fuse_fin ? H : nullptr,
                      1.0, 0.0, stream, /*active_only=*/true, fuse_fin ? S : nullptr, &cl);
     if (rc) return rc;
-    if (cside) WG_HIP_TRY(hipStreamWaitEvent(stream, L->side_join, 0));
   } else {
     for (int32_t k = 1; k <= K; ++k) {
       const float* xm1 = (k & 1) ? b0 : b1;

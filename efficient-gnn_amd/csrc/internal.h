@@ -271,8 +271,6 @@ struct Tuning {
   int32_t team = 1;          // padded-CSR steps as independent waves (team.hip cheb_team4_kernel); 7 .. 13:
                              // register-budget / turn-size variants (team.hip launch_team4; all time the same)
                              // instead of Clenshaw's 3; 0 = Clenshaw
-  int32_t closed_side = 0;   // folded chains: the closed-form rows' S / H by a kernel on a second stream beside the
-                             // chain (forked at its start, joined at its end) instead of in the first launch
   int32_t fold = 1;          // wg_wavelet_features on the team kernel: no permute-in pass (the first launch
                              // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
                              // the closed-form rows; team.hip cheb_team4_first_kernel); 2 = a pass writes
@@ -465,9 +463,6 @@ bool step_single_tile(wg_laplacian_s* L, int64_t F, std::initializer_list<const 
 int launch_permute_u0(wg_laplacian_s* L, int64_t F, const float* src, float* u, hipStream_t stream);
 int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, float* dst, double coef, float* S,
                              float* H, float* u, hipStream_t stream, float* zero = nullptr);
-// the closed-form rows [n_active, n_rows) alone: S = coef X0 and H at their caller rows
-int launch_closed_rows(wg_laplacian_s* L, int64_t F, const float* src, double coef, float* S, float* H,
-                       hipStream_t stream);
 // caller rows (stride F) -> internal rows (stride Fp), pad columns zeroed
 int launch_permute_pad(wg_laplacian_s* L, int64_t F, int64_t Fp, const float* src, float* dst, hipStream_t stream);
 int launch_permute(wg_laplacian_s* L, int direction, int64_t F, const float* src, float* dst, hipStream_t stream);

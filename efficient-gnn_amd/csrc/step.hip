@@ -1251,22 +1251,6 @@ int launch_permute_in_closed(wg_laplacian_s* L, int64_t F, const float* src, flo
   return WG_OK;
 }
 
-int launch_closed_rows(wg_laplacian_s* L, int64_t F, const float* src, double coef, float* S, float* H,
-                       hipStream_t stream) {
-  const int64_t nc = L->n_rows - L->n_active;
-  if (nc <= 0) return WG_OK;
-  if (F % 4 || F > 256) return fail(WG_ERR_INVALID, "closed_rows: F %lld", (long long)F);
-  const int LF = (int)(F / 4);
-  const int G = 64 / LF;
-  constexpr int kRG = 4;
-  // rows relative to n_active (perm shifted): every row is closed, nothing else is written
-  hipLaunchKernelGGL((permute_in_closed_kernel<4, kRG>), dim3((unsigned)ceil_div(nc, 4 * G * kRG)), dim3(kBlock), 0,
-                     stream, nc, F, LF, L->perm + L->n_active, src, (float*)nullptr, (int64_t)0, coef, S, H,
-                     (const double*)nullptr, (float*)nullptr, (int64_t)0, (float*)nullptr);
-  WG_LAUNCH_CHECK();
-  return WG_OK;
-}
-
 namespace {
 // mean 128-B cache lines one gathered row of W floats spans (rows back to back from a
 // 256-B aligned base; the offsets mod 128 repeat with period <= 32 rows)

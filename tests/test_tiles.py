@@ -219,33 +219,37 @@ def test_tiles_duplicate_entries_keep_the_gather_kernel():
 
 @pytest.mark.parametrize("F", [48, 64])
 def test_tiles_auto_items_default_form(F):
-    """The shipped defaults on a graph large enough for long fused items (~n_plan / 310 = 322 blocks per
-    item, past the old 256 cap): at width 48 the step runs in the fused form with its own item list,
-    at width 64 (32x32x16 MFMA, never fused) the sequential step keeps the 128-block items of the
-    sequential rule (the plan is shared across widths).  Both against the oracle and the
-    forced sequential step (hyb_conc = 0); with an explicit tile_max the fused and sequential forms
-    walk the same items and agree bit for bit."""
-    g = rmat_graph(100000, 2_400_000, seed=21)
+    """The shipped defaults on a graph large enough for long fused items (~n_plan / 310 blocks per item,
+    past the former 256 cap): at width 48 the step runs in the fused form with its own item list, at
+    width 64 (32x32x16 MFMA, never fused) the sequential step keeps the sequential rule's 128-block items
+    (one plan serves every width).  Both against the oracle and the forced sequential step
+    (hyb_conc = 0); with an explicit tile_max the default form (fused at 48, two streams at 64: fewer
+    items than two per CU) and the sequential one walk the same items and agree bit for bit."""
+    g = rmat_graph(150000, 3_600_000, seed=21)
     X = np.random.default_rng(F).standard_normal((g.n, F)).astype(np.float32)
     ref = O.graph_wavelet_features(g.to_scipy(), k=4, s=0.8, X0=X, return_all=True)
     L = NormalizedLaplacian.from_graph(g)
-    H0, S0 = _run(L, X, 4, tiles=1, hyb_conc=0)
-    d0 = L.describe(F)
-    assert _forms(d0) == {"fused": 0, "two_stream": 0, "sequential": 4}, d0
     H1, S1 = _run(L, X, 4, tiles=1)                      # defaults: tile_max auto, hyb_conc auto
     d1 = L.describe(F)
     items = d1.split("tiles:")[1]
     n_seq = int(items.split(" items,")[0].split()[-1])
     n_fus = int(items.split("fused launch: ")[1].split(" items")[0])
+    n_act = int(d1.split("active_rows=")[1].split()[0])
+    assert n_act // 310 > 256, d1
     if F == 48:
         assert _forms(d1) == {"fused": 4, "two_stream": 0, "sequential": 0}, d1
         assert n_fus < n_seq, d1                         # longer items in the fused launch
-    else:
-        assert _forms(d1)["fused"] == 0 and _forms(d1)["two_stream"] == 0, d1
+    else:   # not the fused shape: sequential, or two streams when the items leave the GPU half idle
+        assert _forms(d1)["fused"] == 0 and _forms(d1)["two_stream"] + _forms(d1)["sequential"] == 4, d1
+    H0, S0 = _run(L, X, 4, tiles=1, hyb_conc=0)
+    d0 = L.describe(F)
+    assert _forms(d0) == {"fused": 0, "two_stream": 0, "sequential": 4}, d0
     assert_parity(_np(S1), ref["S"], what=f"auto items F={F} S")
     assert_parity(_np(H1), ref["H"], what=f"auto items F={F} H")
     _close(S1, S0, f"auto items F={F} vs sequential")
-    H2, S2 = _run(L, X, 4, tiles=1, tile_max=1024)
+    H2, S2 = _run(L, X, 4, tiles=1, tile_max=1024, hyb_conc=1)
+    if F == 48:
+        assert _forms(L.describe(F))["fused"] == 4
     H3, S3 = _run(L, X, 4, tiles=1, tile_max=1024, hyb_conc=0)
     torch.cuda.synchronize()
     assert torch.equal(S2, S3) and torch.equal(H2, H3), f"F={F}: default form vs hyb_conc=0 differ bitwise"
