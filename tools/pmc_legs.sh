@@ -18,6 +18,6 @@ for leg in ${legs//,/ }; do
     rmat8m) bash tools/pmc_run.sh "$name/rmat8m" python3 tools/sweep.py --config rmat-8m --grid "hub_iter=16" --reps 1 --warm-s 0 || exit $? ;;
     reddit41) bash tools/pmc_run.sh "$name/reddit41" python3 tools/sweep.py --config reddit-f41 --grid "tile_th=96" --reps 1 --warm-s 0 || exit $? ;;
     # rank 0's shard of the 8-way Reddit-size F = 41 split, stepped alone (the fused hybrid launch, round 6)
-    shard8) bash tools/pmc_run.sh "$name/shard8" python3 tools/shard_probe.py --config reddit --world 8 --F 41 --reps 3 || exit $? ;;
+    shard8) bash tools/pmc_run.sh "$name/shard8" python3 tools/shard_probe.py --config reddit --world 8 --F 48 --reps 3 || exit $? ;;
   esac
 done
