@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "libwats_oracle.so")
+# WATS_ORACLE_LIB selects another build of the same source (make -C oracle asan: the sanitizer build)
+LIB_PATH = os.environ.get("WATS_ORACLE_LIB") or os.path.join(_HERE, "build", "libwats_oracle.so")
 _lib = None
 
 
