@@ -203,9 +203,6 @@ int wg_laplacian_tune(wg_laplacian_t L, const char* key, int64_t value) {
     if (value < 0 || value > kChainMaxK) return fail(WG_ERR_INVALID, "chain_fault must be in [0, %d]", kChainMaxK);
     L->tune.chain_fault = (int32_t)value;
     return WG_OK;  // launch-time choice
-  } else if (!strcmp(key, "hyb_fep")) {
-    L->tune.hyb_fep = value ? 1 : 0;
-    return WG_OK;  // launch-time choice (the plan keeps its flags either way)
   } else if (!strcmp(key, "hyb_conc")) {
     if (value < 0 || value > 3) return fail(WG_ERR_INVALID, "hyb_conc must be 0, 1 (auto), 2 (always) or 3 (two streams)");
     L->tune.hyb_conc = (int32_t)value;  // plans rebuilt: the fused launch's tile items are longer
@@ -345,12 +342,6 @@ const char* wg_laplacian_describe(wg_laplacian_t L, int64_t F) {
       snprintf(buf, sizeof(buf), "hybrid forms: fused=%lld two_stream=%lld sequential=%lld\n",
                (long long)tp->form_launches[2], (long long)tp->form_launches[1], (long long)tp->form_launches[0]);
       g_text += buf;
-      if (tp->fep_sync) {  // the fused launches with the epilogue in the tail's waves, and their timed-out waits
-        uint32_t to = 0;
-        if (hipMemcpy(&to, tp->fep_sync + 2, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) to = 0xFFFFFFFFu;
-        snprintf(buf, sizeof(buf), "hybrid in-wave epilogue: launches=%lld timeouts=%u\n", (long long)tp->fep_launches, to);
-        g_text += buf;
-      }
     }
   if (F == 1) {
     Lds1Plan* lp = nullptr;

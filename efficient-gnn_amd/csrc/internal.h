@@ -193,13 +193,6 @@ struct TilePlan {
   int32_t n_fitems = 0, n_fmulti = 0, n_fslots = 0;
   int4* fitems = nullptr;
   int4* fmulti = nullptr;
-  // the fused launch with the epilogue in the tail's waves (hyb_fep): per 128-row block its split items'
-  // slots {first, count} (count 0: one item), and device words [0] finished workgroups, [1] launch epoch,
-  // [2] timed-out waits, [4, 4 + n_rb) row-block flags (the epoch + 1 of the launch that finished the
-  // block's dense sums), then n_rb arrival counters of split blocks (reset by the completing item)
-  int2* fep_rbm = nullptr;
-  uint32_t* fep_sync = nullptr;
-  int64_t n_rb = 0;
   int32_t* tcol = nullptr;     // device [nnz]: each row's tail entries first (the rest of its range unused)
   int32_t* tsplit = nullptr;   // device [n_rows]: end of each row's tail (== row end: no dense entries)
   int32_t width = 0;           // doubles per row of part / slots
@@ -209,7 +202,6 @@ struct TilePlan {
   // kernel, then the tail with its epilogue), [1] two streams (the tail's sums beside the blocks), [2] fused
   // (hybrid_fused_kernel); wg_laplacian_describe names them
   int64_t form_launches[3] = {0, 0, 0};
-  int64_t fep_launches = 0;  // of the fused ones: the epilogue in the tail's waves (hyb_fep)
   std::string text;
   void release();
 };
@@ -283,9 +275,6 @@ struct Tuning {
                              // gathers the caller's X0 scaled by dinv, writes the internal X0, finishes
                              // the closed-form rows; team.hip cheb_team4_first_kernel); 2 = a pass writes
                              // u_0 only (the first launch gathers it; the rest as 1); 0 = the full pass
-  int32_t hyb_fep = 0;       // the fused hybrid launch runs each row's epilogue in its tail wave (no tail-sum
-                             // buffer, no combine / epilogue passes): row blocks' dense sums handed over by
-                             // per-row-block flags inside the launch (tiles.hip hybrid_fused_kernel<., true>)
   int32_t hyb_conc = 1;      // hybrid step with the team-kernel tail: the tail's row sums on a second stream
                              // beside the dense blocks, then one epilogue pass (step.hip); 1 = when the
                              // blocks leave the GPU half idle (tiles.hip hybrid_conc_applies), 2 = always;
@@ -505,7 +494,7 @@ int launch_tiles(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, hipS
 // the dense blocks and the team-kernel tail sums (a.tsum) in one launch, then the blocks' combine
 // (WG_ERR_UNSUPPORTED: not the default tile shape)
 int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, const TeamPlan& tp,
-                        const StepArgs& a, hipStream_t stream, bool fep = false);
+                        const StepArgs& a, hipStream_t stream);
 void release_tiles(wg_laplacian_s* L);
 // u = x * dinv for rows [0, n) of an F-wide signal (in place allowed): the hybrid chain's first
 // step gathers u_0 = X0 * dinv value-free like every later step

@@ -1114,11 +1114,9 @@ int launch_step(wg_laplacian_s* L, int32_t k, int64_t F, const float* xm1, const
         if (L->tune.hyb_conc != 3) {  // one launch: the dense blocks' workgroups, then the tail's waves
           if (int rc = tiles_loop(tp, stream, L->tsum, /*defer=*/true)) return rc;
           if (!conc_team) return fail(WG_ERR_INVALID, "launch_step: the hybrid tail's plan was not built");
-          const int64_t fep_before = tp->fep_launches;
-          frc = launch_hybrid_fused(L, tp, F, xm1, *conc_team, conc_fused, stream, L->tune.hyb_fep != 0);
+          frc = launch_hybrid_fused(L, tp, F, xm1, *conc_team, conc_fused, stream);
           if (frc && frc != WG_ERR_UNSUPPORTED) return frc;
           if (!frc) ++tp->form_launches[2];
-          if (!frc && tp->fep_launches > fep_before) return finish();  // every row finished in its tail wave
         }
         if (frc == WG_ERR_UNSUPPORTED) {  // two streams
           WG_HIP_TRY(hipEventRecord(L->side_fork, stream));

@@ -25,11 +25,6 @@ struct TeamArgs {
   double coef;
   float* cS;
   float* cH;
-  // the fused hybrid launch with the epilogue in the tail's waves (hyb_fep, tiles.hip): a row with dense
-  // entries waits for its 128-row block's flag to hold this launch's token, then adds the block sums
-  const uint32_t* fep_flag;
-  uint32_t* fep_sync;
-  int64_t fep_ticks;
 #ifdef WG_DEBUG_BOUNDS
   int64_t dbg_rows, dbg_slots, dbg_long;  // the table's rows, partial slots and long rows
 #endif
@@ -91,34 +86,11 @@ __device__ __forceinline__ void closed_wave(const TeamArgs& t, int64_t cw) {
   }
 }
 
-// hyb_fep: the row's dense-block sums (the tile items of its 128-row block, possibly on other XCDs) once the
-// block's flag holds this launch's token; the sums are read with agent-scope loads (the writers stored them
-// write-through and drained before the flag).  A wait past fep_ticks counts a timeout (wg_laplacian_describe)
-// and goes on: never a hang
-__device__ __forceinline__ void fep_part_add(const TeamArgs& t, int64_t row, int fs, double (&acc)[4], uint32_t tok) {
-  const StepArgs& a = t.a;
-  if (a.rsplit[row] == a.rowptr[row + 1]) return;  // no dense entries
-  const uint32_t* f = t.fep_flag + (row >> 7);
-  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok) {
-    const uint64_t dl = wall_clock64() + (uint64_t)t.fep_ticks;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tok) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() > dl) {
-        __hip_atomic_fetch_add(t.fep_sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  const double* p = a.part + row * a.ld + (int64_t)fs * 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] += __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // MINW: minimum waves per SIMD the registers are held to (6 = the natural 77 VGPRs); LATE: the
 // epilogue's X0 / previous-row operands loaded after the gathers instead of before (fewer live
 // registers in the loop)
-template <bool LATE, int CPT, bool FIRST = false, bool FEP = false>
-__device__ __forceinline__ void team_wave(const TeamArgs& t, int w, uint32_t tok = 0) {
+template <bool LATE, int CPT, bool FIRST = false>
+__device__ __forceinline__ void team_wave(const TeamArgs& t, int w) {
   const StepArgs& a = t.a;
 #ifdef WG_TIMING_PROBES
   if (a.probe_h2 == -4) return;  // launch + wave dispatch only
@@ -200,8 +172,7 @@ __device__ __forceinline__ void team_wave(const TeamArgs& t, int w, uint32_t tok
       *reinterpret_cast<double2*>(p + 2) = double2{acc[2], acc[3]};
       return;
     }
-    if constexpr (FEP) fep_part_add(t, row, fs, acc, tok);
-    else part_add<4>(a, row, fs, acc);
+    part_add<4>(a, row, fs, acc);
     step_epilogue<4>(a, row, fs, acc, in, lane0);
   }
 }

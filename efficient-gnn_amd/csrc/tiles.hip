@@ -75,11 +75,6 @@ struct TileArgs {
   const int4* items;
   double* part;          // [rows][ld]
   double* slots;         // [slot][rows per block][W]
-  // hyb_fep (hybrid_fused_kernel<., true>): per row block {first slot, slots} of split blocks, the flags and
-  // the split blocks' arrival counters (TilePlan::fep_sync)
-  const int2* fep_rbm;
-  uint32_t* fep_flag;
-  uint32_t* fep_cnt;
 #ifdef WG_DEBUG_BOUNDS
   int64_t dbg_blocks, dbg_slots;  // dense blocks and float64 slots of the plan
 #endif
@@ -111,8 +106,8 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
 // NWV waves; FW = false: every wave multiplies all NFB column blocks for its RG groups of 16
 // rows; FW = true: wave w multiplies column block w % NFB for RG row groups, so each B
 // fragment read from LDS serves RG row groups (NFB * 8 / RG waves for 128 rows)
-template <int NFB, int NWV, int RG, bool FW, bool FEP = false>
-__device__ __forceinline__ void tiles_item(const TileArgs& t, int item, uint32_t tok = 0) {
+template <int NFB, int NWV, int RG, bool FW>
+__device__ __forceinline__ void tiles_item(const TileArgs& t, int item) {
   constexpr int NRW = FW ? NWV / NFB : NWV;  // waves along the rows
   constexpr int NFW = FW ? 1 : NFB;          // column blocks per wave
   constexpr int TR = 16 * NRW * RG;    // rows per row block (RG groups of 16 per wave)
@@ -322,50 +317,8 @@ __device__ __forceinline__ void tiles_item(const TileArgs& t, int item, uint32_t
       if (it.w < 0 && row >= t.n_plan) continue;
       double* dst = it.w < 0 ? t.part + row * t.ld : t.slots + ((int64_t)it.w * TR + rl) * W;
 #pragma unroll
-      for (int fw = 0; fw < NFW; ++fw) {
-        if constexpr (FEP)  // write-through: the rows' tail waves on other XCDs read them in this launch
-          __hip_atomic_store(dst + 16 * (fb0 + fw) + (lane & 15), acc[g][fw][i], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        else
-          dst[16 * (fb0 + fw) + (lane & 15)] = acc[g][fw][i];
-      }
+      for (int fw = 0; fw < NFW; ++fw) dst[16 * (fb0 + fw) + (lane & 15)] = acc[g][fw][i];
     }
-  if constexpr (FEP) {
-    // hand the row block over: every store drained, then (split blocks) one arrival on the block's counter;
-    // the item completing the block sums its slots into part in slot order (tiles_combine_kernel's sums,
-    // bitwise), and the block's flag takes the launch's token (MI355X_MICROARCH.md hand-off, row 1)
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      int last = 1;
-      if (it.w >= 0) {
-        const int2 m = t.fep_rbm[rb];
-        const uint32_t old = __hip_atomic_fetch_add(t.fep_cnt + rb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old + 1u == (uint32_t)m.y;
-        if (last) __hip_atomic_store(t.fep_cnt + rb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    if (it.w >= 0) {
-      const int2 m = t.fep_rbm[rb];
-      const int64_t step = (int64_t)TR * W;
-      for (int e = tid; e < TR * W; e += NT) {
-        const int rl = e / W, f = e - rl * W;
-        const int64_t row = rb * TR + rl;
-        if (row >= t.n_plan) continue;
-        const double* p = t.slots + ((int64_t)m.x * TR + rl) * W + f;
-        double s = 0.0;
-        for (int q = 0; q < m.y; ++q) s += __hip_atomic_load(p + q * step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(t.part + row * t.ld + f, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    if (tid == 0) __hip_atomic_store(t.fep_flag + rb, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 template <int NFB, int NWV, int RG, bool FW>
@@ -377,36 +330,15 @@ __global__ __launch_bounds__(64 * NWV, FW ? 2 : (NWV == 8 && NFB < 4 ? WG_TILES_
 // [0, n_items) are the tile kernel's items (128-row blocks, 8 waves), the rest are 8 team-kernel waves each
 // summing rows' tails into a.tsum (team_wave with tsum: no epilogue).  Tiles first in dispatch order.  No
 // stream fork / join (a captured or eager cross-stream join cost ~10 us per step, r05 s45-s46)
-// FEP (tuning key hyb_fep): no tail-sum buffer, combine or epilogue pass -- each tail wave runs its rows'
-// epilogue once their 128-row block's dense sums are handed over (tiles_item, fep_part_add).  Items never
-// wait and come first in dispatch order, so a waiting wave waits only on items already dispatched.  The
-// launch's token is the epoch + 1 read at every workgroup's start; the last workgroup to finish moves the
-// epoch on (every workgroup has read it by then), so flags left by earlier launches never match.
-template <int NFB, bool FEP = false>
+template <int NFB>
 __global__ __launch_bounds__(512, NFB < 4 ? WG_TILES_MINW : 4) void hybrid_fused_kernel(TileArgs tt, TeamArgs ta,
                                                                                           int32_t n_items) {
-  __shared__ uint32_t s_epoch;
-  if constexpr (FEP) {
-    if (threadIdx.x == 0) s_epoch = __hip_atomic_load(ta.fep_sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-  }
-  const uint32_t tok = FEP ? s_epoch + 1u : 0u;
   if ((int)blockIdx.x < n_items) {
-    tiles_item<NFB, 8, 1, false, FEP>(tt, (int)blockIdx.x, tok);
-  } else {
-    const int w = ((int)blockIdx.x - n_items) * 8 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (w < ta.n_waves) team_wave<false, 2, false, FEP>(ta, w, tok);
+    tiles_item<NFB, 8, 1, false>(tt, (int)blockIdx.x);
+    return;
   }
-  if constexpr (FEP) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t done = __hip_atomic_fetch_add(ta.fep_sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-      if (done == gridDim.x) {
-        __hip_atomic_store(ta.fep_sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ta.fep_sync + 1, s_epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
+  const int w = ((int)blockIdx.x - n_items) * 8 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w < ta.n_waves) team_wave<false, 2>(ta, w);
 }
 
 // The same product on v_mfma_f32_32x32x16_bf16 (tile_mfma = 32; widths 48 and 64, 128-row
@@ -731,16 +663,6 @@ int build_tile_plan(wg_laplacian_s* L, bool active_only, TilePlan* p) {
     p->n_fmulti = (int32_t)fmulti.size();
     p->n_fslots = n_fslots;
   }
-  if (!rc && fused_possible) {  // hyb_fep: the fused items' split blocks and the hand-off words
-    const std::vector<int4>& fm = fitems.empty() ? multi : fmulti;
-    p->n_rb = n_rb;
-    std::vector<int2> rbm((size_t)std::max<int64_t>(1, n_rb), make_int2(0, 0));
-    for (const int4& m : fm) rbm[m.x] = make_int2(m.y, m.z);
-    rc = upload(&p->fep_rbm, rbm);
-    if (!rc) rc = dmalloc(&p->fep_sync, (size_t)(4 + 2 * n_rb));
-    if (!rc && hipMemset(p->fep_sync, 0, sizeof(uint32_t) * (4 + 2 * n_rb)) != hipSuccess)
-      rc = fail(WG_ERR_HIP, "tiles: hand-off words");
-  }
   if (!rc) rc = upload(&p->tcol, tcol);
   if (!rc) rc = upload(&p->tsplit, tsplit);
   if (rc) return rc;
@@ -759,10 +681,6 @@ void TilePlan::release() {
   (void)hipFree(bmask);
   if (fitems != items) (void)hipFree(fitems);
   if (fmulti != multi) (void)hipFree(fmulti);
-  (void)hipFree(fep_rbm);
-  (void)hipFree(fep_sync);
-  fep_rbm = nullptr;
-  fep_sync = nullptr;
   (void)hipFree(items);
   (void)hipFree(multi);
   fitems = nullptr;
@@ -920,26 +838,14 @@ int launch_tiles_combine(const TilePlan* p, int64_t F, hipStream_t stream, bool 
 }  // namespace
 
 int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* u, const TeamPlan& tp,
-                        const StepArgs& a, hipStream_t stream, bool fep) {
+                        const StepArgs& a, hipStream_t stream) {
   // the default tile shape only: 128-row blocks, one 16-row group per wave, the 16x16x32 MFMA
   if (!hybrid_fused_shape(L, p, F) || F > p->width || (reinterpret_cast<uintptr_t>(u) & 15) || !a.tsum ||
       tp.n_waves < 0)
     return WG_ERR_UNSUPPORTED;
-  fep = fep && p->fep_sync && p->fep_rbm && p->rows == 128;
-  TileArgs tt = tile_args(p, F, u, true);
+  const TileArgs tt = tile_args(p, F, u, true);
   TeamArgs ta{};
   ta.a = a;
-  if (fep) {  // the epilogue in the tail's waves: no tail sums, no combine, no epilogue pass
-    tt.fep_rbm = p->fep_rbm;
-    tt.fep_flag = p->fep_sync + 4;
-    tt.fep_cnt = p->fep_sync + 4 + p->n_rb;
-    ta.a.tsum = nullptr;
-    ta.fep_flag = p->fep_sync + 4;
-    ta.fep_sync = p->fep_sync;
-    int khz = 100000;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, L->device) != hipSuccess || khz <= 0) khz = 100000;
-    ta.fep_ticks = (int64_t)khz * 200;  // 0.2 s
-  }
   ta.a.sell = tp.sell;
   ta.wd = tp.wd;
   ta.n_waves = tp.n_waves;
@@ -950,21 +856,13 @@ int launch_hybrid_fused(wg_laplacian_s* L, TilePlan* p, int64_t F, const float* 
   const int64_t nb = (int64_t)ni + ceil_div((int64_t)tp.n_waves, 8);
   if (nb > 0) {
     const dim3 grid((unsigned)nb), block(512);
-#define WG_FUSED(NFB)                                                                                  \
-  if (fep) hipLaunchKernelGGL((hybrid_fused_kernel<NFB, true>), grid, block, 0, stream, tt, ta, ni); \
-  else hipLaunchKernelGGL((hybrid_fused_kernel<NFB, false>), grid, block, 0, stream, tt, ta, ni);
     switch (F / 16) {
-      case 1: WG_FUSED(1) break;
-      case 2: WG_FUSED(2) break;
-      case 3: WG_FUSED(3) break;
-      default: WG_FUSED(4) break;
+      case 1: hipLaunchKernelGGL(hybrid_fused_kernel<1>, grid, block, 0, stream, tt, ta, ni); break;
+      case 2: hipLaunchKernelGGL(hybrid_fused_kernel<2>, grid, block, 0, stream, tt, ta, ni); break;
+      case 3: hipLaunchKernelGGL(hybrid_fused_kernel<3>, grid, block, 0, stream, tt, ta, ni); break;
+      default: hipLaunchKernelGGL(hybrid_fused_kernel<4>, grid, block, 0, stream, tt, ta, ni); break;
     }
-#undef WG_FUSED
     WG_LAUNCH_CHECK();
-  }
-  if (fep) {
-    ++p->fep_launches;
-    return WG_OK;
   }
   return launch_tiles_combine(p, F, stream, true);
 }

@@ -255,34 +255,3 @@ def test_tiles_auto_items_default_form(F):
     assert torch.equal(S2, S3) and torch.equal(H2, H3), f"F={F}: default form vs hyb_conc=0 differ bitwise"
     assert_parity(_np(S2), ref["S"], what=f"tile_max=1024 F={F} S")
     L.close()
-
-
-@pytest.mark.parametrize("k", [1, 3, 16])
-@pytest.mark.parametrize("F", [48, 16])
-def test_tiles_in_wave_epilogue(F, k):
-    """hyb_fep: the fused launch with each row's epilogue in its tail wave (no tail-sum buffer, no combine
-    or epilogue pass): the row blocks' dense sums are handed over inside the launch by per-block flags, split
-    blocks summed by the item that completes them.  Bitwise the two-pass fused form and the sequential step
-    (the same float64 sums in the same order), on plans with split row blocks (tile_max 3 / 5), with and
-    without closed-form rows, long tails as part waves (hyb_iter 8); repeated launches never match an
-    earlier launch's flags (no timeouts); and the oracle's."""
-    g = rmat_graph(6000, 150000, seed=F + k + 1)
-    for gg in (g, connect_isolated(g, seed=3)):
-        X = np.random.default_rng(F + 5 * k).standard_normal((gg.n, F)).astype(np.float32)
-        ref = O.graph_wavelet_features(gg.to_scipy(), k=k, s=0.8, X0=X, return_all=True)
-        L = NormalizedLaplacian.from_graph(gg)
-        for knobs in (dict(tile_th=16, tile_max=5, tile_rows=128), dict(tile_th=8, tile_max=3, tile_rows=128, hyb_iter=8)):
-            H0, S0 = _run(L, X, k, tiles=1, hyb_conc=0, hyb_fep=0, **knobs)
-            H1, S1 = _run(L, X, k, tiles=1, hyb_conc=2, hyb_fep=0, **knobs)
-            H2, S2 = _run(L, X, k, tiles=1, hyb_conc=2, hyb_fep=1, **knobs)
-            H3, S3 = _run(L, X, k, tiles=1, hyb_conc=2, hyb_fep=1, **knobs)
-            torch.cuda.synchronize()
-            d = L.describe(F)
-            assert "hybrid in-wave epilogue: launches=" in d, d
-            line = [x for x in d.splitlines() if x.startswith("hybrid in-wave epilogue")][0]
-            assert line.endswith("timeouts=0") and int(line.split("launches=")[1].split()[0]) >= k, d
-            assert torch.equal(S0, S1) and torch.equal(S1, S2) and torch.equal(H1, H2), f"F={F} K={k} {knobs}"
-            assert torch.equal(S2, S3) and torch.equal(H2, H3)
-            assert_parity(_np(S2), ref["S"], what=f"in-wave epilogue F={F} K={k} {knobs} S")
-            assert_parity(_np(H2), ref["H"], what=f"in-wave epilogue F={F} K={k} {knobs} H")
-        L.close()
