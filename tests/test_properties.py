@@ -70,3 +70,77 @@ def test_random_graphs_lds_kernels(spec, K, lds):
     L.tune(lds=lds, lds_cb=64)   # small blocks / hub: several blocks and a tail even on tiny graphs
     _, S = wats_hip.graph_wavelet_features(L, k=K, s=0.8, X0=torch.from_numpy(X), return_S=True)
     assert_parity(S.cpu().numpy(), ref["S"], what=f"{spec} lds={lds} K={K} S")
+
+
+# ------------------------------------------------------------ size-independent properties at the named sizes
+def _colwise_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().amax(dim=0) / (b.abs().amax(dim=0) + 1e-30)).max().item()
+
+
+def _features(L, X, k):
+    H, S = wats_hip.graph_wavelet_features(L, k=k, s=0.8, X0=X, return_S=True)
+    torch.cuda.synchronize()
+    return H, S
+
+
+@pytest.mark.gpu
+def test_headline_linearity_relabelling_determinism():
+    """The metric's config (ogbn-arxiv-size R-MAT, K=16, F=40: the team kernel with the folded first launch):
+    S is linear in X0 (S(X + 2Y) = S(X) + 2 S(Y)), equivariant under a relabelling of the nodes
+    (S(P A P^T, P X) = P S(A, X): a different internal order, so a different summation order), and bitwise
+    reproducible -- column-wise within the parity tolerance, at the full size, without the oracle."""
+    from wats_hip import NormalizedLaplacian
+    from wats_hip.graphgen import CSRGraph, named_graph
+    g = named_graph("ogbn-arxiv")
+    n = g.n
+    gen = torch.Generator().manual_seed(7)
+    X = torch.randn(n, 40, generator=gen).cuda()
+    Y = torch.randn(n, 40, generator=gen).cuda()
+    L = NormalizedLaplacian.from_graph(g)
+    _, SX = _features(L, X, 16)
+    _, SY = _features(L, Y, 16)
+    _, SZ = _features(L, X + 2 * Y, 16)
+    assert "team:" in L.describe(40)
+    assert _colwise_err(SZ, SX + 2 * SY) <= 1e-5
+    _, SX2 = _features(L, X, 16)
+    assert torch.equal(SX, SX2), "the chain must be bitwise reproducible"
+    L.close()
+    # relabel: new id of node v is p[v]
+    p = np.random.default_rng(3).permutation(n)
+    A = g.to_scipy().tocoo()
+    import scipy.sparse as sp
+    B = sp.csr_matrix((A.data, (p[A.row], p[A.col])), shape=A.shape)
+    B.sort_indices()
+    gp = CSRGraph(n, B.indptr.astype(np.int64), B.indices.astype(np.int32), None)
+    Lp = NormalizedLaplacian.from_graph(gp)
+    pt = torch.from_numpy(p).cuda()
+    Xp = torch.empty_like(X)
+    Xp[pt] = X
+    Hp, Sp = _features(Lp, Xp, 16)
+    assert _colwise_err(Sp[pt], SX) <= 1e-5
+    Lp.close()
+
+
+@pytest.mark.gpu
+def test_reddit_f41_linearity_and_determinism():
+    """Reddit-size K=16 F=41 (the fused hybrid step: dense blocks on the matrix cores, the tail's waves in the
+    same launch): S linear in X0 and bitwise reproducible, at the full size."""
+    from wats_hip import NormalizedLaplacian
+    from wats_hip.graphgen import NAMED_CONFIGS, rmat_graph_device
+    n, nnz, _, _ = NAMED_CONFIGS["reddit"]
+    ip, ix = rmat_graph_device(n, nnz, seed=0, device="cuda")
+    L = NormalizedLaplacian(n, ip, ix)
+    del ip, ix
+    gen = torch.Generator().manual_seed(11)
+    X = torch.randn(n, 41, generator=gen).cuda()
+    Y = torch.randn(n, 41, generator=gen).cuda()
+    _, SX = _features(L, X, 16)
+    _, SY = _features(L, Y, 16)
+    _, SZ = _features(L, X - 0.5 * Y, 16)
+    d = L.describe(48)
+    assert "tiles:" in d and "hybrid forms: fused=" in d, d
+    assert _colwise_err(SZ, SX - 0.5 * SY) <= 1e-5
+    _, SX2 = _features(L, X, 16)
+    assert torch.equal(SX, SX2)
+    L.close()
