@@ -366,9 +366,15 @@ def run_sharded(config, K, F, steps, warmup, seed, s_heat, world, rank, device, 
     plan_text = sw.L.describe(F)
     kernel = lds_kernel_name(lds_info, team="team:" in plan_text) + " (rank 0 shard)"
     tiles_plan = [ln for ln in plan_text.splitlines() if ln.startswith("tiles:")]
-    if tiles_plan:   # the hybrid step: dense blocks on MFMA + the tail on the step kernel
-        kernel = ("hybrid step: cheb_tiles_kernel + tiles_combine_kernel + the tail on the step kernel "
-                  "(cheb_team4_kernel; rank 0 shard)")
+    if tiles_plan:   # the hybrid step: dense blocks on MFMA + the tail, in the form that ran
+        forms = [ln for ln in plan_text.splitlines() if ln.startswith("hybrid forms:")]
+        f = dict(t.split("=") for t in forms[-1].split(":", 1)[1].split()) if forms else {}
+        if int(f.get("fused", 0)) > 0 and int(f.get("two_stream", 0)) == 0 and int(f.get("sequential", 0)) == 0:
+            kernel = ("hybrid step, fused form: hybrid_fused_kernel (dense-block items + the tail's team waves in "
+                      "one launch) + tiles_combine_kernel + hybrid_epilogue_kernel (rank 0 shard)")
+        else:
+            kernel = ("hybrid step: cheb_tiles_kernel + tiles_combine_kernel + the tail on the step kernel "
+                      f"(forms run: {forms[-1] if forms else 'unknown'}; rank 0 shard)")
     avg_ms = prof["step_ms"]
     sw.close()
     del sw
