@@ -237,11 +237,15 @@ int wg_wavelet_features(wg_laplacian_t L, const float* X0, int64_t F, int32_t K,
  * missing data and records the failure in host-mapped memory, and the NEXT
  * wg_wavelet_features call on the handle returns WG_ERR_TIMEOUT without
  * launching.  wg_chain_status waits for the handle's last one-launch chain
- * (an event: no device-wide sync) and reports a failure since the last report
+ * (an event recorded after it, also after a replay of the handle's own
+ * captured chain; no device-wide sync -- except after a chain captured into a
+ * graph the CALLER replays, which records no event of the handle's, where it
+ * synchronises the device) and reports a failure since the last report
  * in *timed_out_host (1 = a chain's results are invalid; tuning key
  * "chain_fault" = j injects one: worker 0 skips publishing phase j).  Either
- * report switches the handle to the multi-launch path (until the next tune),
- * so calling again recomputes the features there (the Python
+ * report switches the handle to the multi-launch path (until the next tune)
+ * and drops a chain the handle captured with the one-launch kernel, so calling
+ * again recomputes the features there (the Python
  * graph_wavelet_features does so by itself).  The plan never asks for more
  * workers than the occupancy query lets be resident (one per CU at most);
  * when the graph would need more, the multi-launch path runs. */
