@@ -380,6 +380,7 @@ struct wg_dist_s {
           WG_HIP_TRY(hipMemsetAsync(region + sl * slot_floats + n_own * F, 0, sizeof(float) * n_halo * F, st));
         pads_zeroed = F;
       }
+      if (Fr >= F) pads_zeroed = 0;  // a full-width pull writes the columns a narrower signal leaves zero
       if (total > 0) {
         const int64_t work = v4 ? n_halo * (Fr / 4) : total;
         const int blocks = (int)std::min<int64_t>(65535, ceil_div(work, 256));
