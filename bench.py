@@ -81,8 +81,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--traffic-json", default="auto",
                     help="per-launch HBM bytes of the step kernel from a rocprofv3 --pmc pass (tools/pmc_traffic.py); "
-                         "'auto': the committed PMC summary of the default workload (profiles/r05/s5_traffic.json, "
-                         "tools/session.sh pmc) when the workload is the default one; 'none' to omit")
+                         "'auto': the committed PMC summary of the default workload (profiles/r06/s13_traffic.json, "
+                         "tools/pmc_legs.sh arxiv + tools/traffic_json.py) when the workload is the default one; 'none' to omit")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--sharded-extra", default="reddit-f41,reddit,rmat-8m,ogbn-arxiv",
                     help="comma-separated configs also measured row-sharded over all ranks (halo exchange), attached "
@@ -714,7 +714,7 @@ def single_gpu_line(args, g, config, K, F, world, rank, device, full=True):
     traffic, traffic_src = None, None
     tj = args.traffic_json
     if tj == "auto":
-        tj = os.path.join(REPO, "profiles", "r05", "s5_traffic.json") \
+        tj = os.path.join(REPO, "profiles", "r06", "s13_traffic.json") \
             if (config == "ogbn-arxiv" and F == 40 and K == 16) else None
     if tj and tj != "none" and os.path.exists(tj):
         traffic = json.load(open(tj)).get("bytes_per_launch")
