@@ -470,3 +470,69 @@ def test_ipc_chain_with_an_empty_shard(F, exchange):
     X = np.random.default_rng(0).standard_normal((g.n, F)).astype(np.float32)
     ref = O.graph_wavelet_features(g.to_scipy(), k=5, s=0.8, X0=X, return_all=True)
     assert_parity(np.concatenate([r[1] for r in res]), ref["S"], what=f"empty shard F={F}")
+
+
+def _width_worker(rank, world, port, widths, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "efficient-gnn_amd"))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from wats_hip.dist import ShardedWavelet
+        g = rmat_graph(4000, 120000, seed=9)
+        bounds = partition_rows(g.indptr, world)
+        r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+        lo, hi = g.indptr[r0], g.indptr[r1]
+        sw = ShardedWavelet(g.indptr[r0:r1 + 1] - lo, g.indices[lo:hi], None, g.n, bounds, exchange="ipc",
+                            device="cuda:0", max_features=max(widths))
+        sw.L.tune(tiles=1, tile_th=8, tile_max=3)
+        out = []
+        for F in widths:
+            X = np.random.default_rng(F).standard_normal((g.n, F)).astype(np.float32)
+            H, S = sw.wavelet_features(torch.from_numpy(X[r0:r1]), k=6, s=0.8)
+            torch.cuda.synchronize()
+            out.append(S.cpu().numpy())
+        sw.check_exchange()
+        sw.close()
+        q.put((rank, out))
+    except Exception as exc:  # noqa: BLE001
+        import traceback
+        q.put((rank, f"{exc!r}\n{traceback.format_exc()}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_ipc_chain_width_changes():
+    """The IPC pull moves only a signal's own columns (F = 41: 44 of the 48 exchanged, the halo rows' pad
+    columns zeroed once per width), and a full-width pull (F = 48) invalidates those zeros: one handle runs
+    F = 41, 48, 41, 16 in turn on 2 ranks sharing the GPU (the hybrid step on both shards), every result
+    against the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    widths = [41, 48, 41, 16]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_width_worker, args=(r, 2, port, widths, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        for _ in range(2):
+            res.append(q.get(timeout=170))
+            if isinstance(res[-1][1], str):
+                pytest.fail(f"rank {res[-1][0]}: {res[-1][1]}")
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    res.sort(key=lambda t: t[0])
+    g = rmat_graph(4000, 120000, seed=9)
+    for i, F in enumerate(widths):
+        X = np.random.default_rng(F).standard_normal((g.n, F)).astype(np.float32)
+        ref = O.graph_wavelet_features(g.to_scipy(), k=6, s=0.8, X0=X, return_all=True)
+        assert_parity(np.concatenate([r[1][i] for r in res]), ref["S"], what=f"IPC width change F={F} (call {i})")
